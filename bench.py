@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mray/s of the path-tracing kernel, 1920x1080, 8 bounces.
+
+Workload (BASELINE.json configs[1]): the RTIOW cover scene (488 spheres),
+1920x1080, 8 bounces, 1 sample per pixel per frame, accumulation on. One
+"step" = one Renderer.compute_frame (one kernel launch over the frame). Inputs
+are resident in HBM before timing; the timed region holds exactly `--steps`
+frames bracketed by barrier + device synchronize.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+the fixed 1920x1080 image is tile-split across ranks (8x8 tile t -> rank t % N,
+SURVEY §8e), so total work is fixed ("scaling": "strong"). No collective runs in
+the timed loop; one RCCL gather of the accumulated RGBA32F tiles to rank 0 runs
+afterwards and is reported separately as gather_ms.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Mray/s (primary+bounce) at 1920x1080, 8 bounces; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(owned_pixels: int, rays: float, scene_bytes: int) -> float:
+    """B = 52 B/px (ray dir 16 + accum 16 read + 16 write + RGBA8 4)
+    + 4 B per counted ray (one RGBA8 texel: texture on hit, env map on miss)
+    + the scene arrays read once."""
+    return 52.0 * owned_pixels + 4.0 * rays + scene_bytes
+
+
+def scene_bytes(scene) -> int:
+    objs, subs, tris = scene.flatten()
+    return int(scene.spheres.nbytes + scene.materials.nbytes + objs.nbytes + subs.nbytes + tris.shape[0] * 80)
+
+
+def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
+    """The CPU oracle (scalar C restatement, OpenMP over the host cores) on a bounded
+    sample of the same workload: the tiles t % sample_world == 0, frames k = 1, 2, ...
+    until min_seconds have elapsed."""
+    from oracle import oracle as O
+
+    O.build()
+    o = O.Oracle(scene)
+    threads = O.lib().oracle_num_threads()
+    accum = np.zeros((o.height, o.width, 4), np.float32)
+    out = np.zeros((o.height, o.width), np.uint32)
+    rays = 0
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        frames += 1
+        p = scene.params(accumulation_index=frames)
+        rays += o.render_frame(p, bounces, accum, out, rank=0, world_size=sample_world, threads=threads)
+        el = time.perf_counter() - t0
+        if el >= min_seconds or frames >= 64:
+            break
+    return {
+        "value": rays / el / 1e6,
+        "unit": "Mray/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"CPU oracle (oracle/pathtrace_oracle.c, -O2 scalar f32, OpenMP {threads} threads) on "
+                   f"1/{sample_world} of the 8x8 tiles of the same {o.width}x{o.height} {bounces}-bounce frame, "
+                   f"{frames} frame(s), {rays} rays in {el:.1f} s"),
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2_rtiow")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-sample-world", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    assert torch.cuda.is_available(), "bench.py needs a HIP device"
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from rust_gpu_raytracing_amd import Renderer
+    from rust_gpu_raytracing_amd import build as native_build
+    from rust_gpu_raytracing_amd.scene import build_config
+
+    if rank == 0:
+        native_build.build(verbose=False)
+    if world > 1:
+        dist.barrier()
+
+    scene, default_bounces = build_config(args.config, width=args.width, height=args.height)
+    bounces = args.bounces or default_bounces
+    r = Renderer(scene, device=local_rank, rank=rank, world_size=world)
+    owned_px = r.owned_pixel_count()
+
+    def barrier_sync():
+        r.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        r.compute_frame(bounces)
+    barrier_sync()
+    r.reset_ray_count()
+    r.reset_timing()
+    r.set_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        r.compute_frame(bounces)
+        if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
+            log(f"step {i + 1}/{args.steps}")
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    r.set_timing(False)
+    rays = r.ray_count()
+    kern_ms, n_timed = r.dispatch_time_total()
+
+    stats = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        t_max = stats[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = stats[1:2].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed_max, rays_total = float(t_max.item()), float(tot.item())
+    else:
+        elapsed_max, rays_total = elapsed, float(rays)
+
+    gather_ms = None
+    if world > 1 and not args.no_gather:
+        from rust_gpu_raytracing_amd.distributed import gather_accumulation
+
+        barrier_sync()
+        g0 = time.perf_counter()
+        gather_accumulation(r, dst=0)
+        barrier_sync()
+        gather_ms = (time.perf_counter() - g0) * 1e3
+
+    if rank == 0:
+        avg_kernel_s = kern_ms / max(n_timed, 1) / 1e3
+        rays_per_launch = rays / max(args.steps, 1)
+        b_launch = algorithmic_bytes(owned_px, rays_per_launch, scene_bytes(scene))
+        achieved = b_launch / avg_kernel_s / 1e9
+        result = {
+            "metric": METRIC,
+            "value": rays_total / elapsed_max / 1e6,
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config} {args.width}x{args.height}, {bounces} bounces, 1 spp/frame, accumulate",
+                "width": args.width,
+                "height": args.height,
+                "bounces": bounces,
+                "spheres": int(scene.spheres.shape[0]),
+                "triangles": int(scene.flatten()[2].shape[0]),
+                "parallelism": f"tile{world}" if world > 1 else "single",
+                "rays_per_step": rays_total / args.steps,
+                "nominal_rays_per_step": args.width * args.height * bounces,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "rt_pathtrace_kernel",
+                "kernel_ms_avg": avg_kernel_s * 1e3,
+                "bytes_per_launch": b_launch,
+                "note": "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction",
+            },
+        }
+        if gather_ms is not None:
+            result["gather_ms"] = gather_ms
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline ...")
+            result["cpu_baseline"] = cpu_baseline(scene, bounces, args.cpu_seconds, args.cpu_sample_world)
+        print(json.dumps(result), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

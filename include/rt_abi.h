@@ -1,0 +1,269 @@
+/*
+ * rt_abi.h — C ABI of the MI355X path-tracing hot path.
+ *
+ * This is the drop-in boundary for juhotuho10/rust_GPU_raytracing's per-frame
+ * compute path. In the reference, `Renderer` (src/renderer.rs) owns a
+ * `DataBuffers` (src/buffers.rs) of 10 wgpu buffers + 2 textures and records
+ * one compute pass of `compute_shader.wgsl::main` per frame. Here the same
+ * surface is a handful of `extern "C"` functions over an opaque context that
+ * owns hipMalloc'd buffers, a pinned staging ring and one HIP stream. The
+ * Rust side would bind these with a plain `extern "C" { ... }` block (see
+ * INTEGRATION.md); nothing in the signatures is a C++ or torch type.
+ *
+ * POD layouts below are byte-for-byte the reference's `#[repr(C)]` structs
+ * (src/buffers.rs:7-129) — the host arrays the reference already builds can be
+ * handed over with no conversion.
+ *
+ * Conventions
+ *   - every call returns int: RT_OK (0) or a negative RT_E* code; the message
+ *     of the last failure is available from rt_last_error(ctx).
+ *   - host arrays passed in are copied before the call returns (async copies
+ *     go through the context's pinned staging ring); the caller keeps
+ *     ownership.
+ *   - one context = one device + one stream; calls on one context are not
+ *     thread-safe (the reference's Renderer is owned by the event-loop thread,
+ *     src/main.rs:240-496).
+ *   - all device work is stream-ordered, exactly like wgpu queue submission
+ *     order (src/renderer.rs:249): an update issued before rt_compute_frame is
+ *     visible to that frame's dispatch.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define RT_API __attribute__((visibility("default")))
+#else
+#define RT_API
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define RT_OK 0
+#define RT_E_INVALID -1   /* bad argument (null, size mismatch, index out of range) */
+#define RT_E_HIP -2       /* HIP runtime call failed */
+#define RT_E_NOMEM -3     /* host or device allocation failed */
+#define RT_E_CAPACITY -4  /* update larger than the buffer created at rt_create (wgpu would panic) */
+#define RT_E_NODEVICE -5  /* no HIP device / device index out of range */
+
+/* ---- POD scene types: src/buffers.rs:7-129 ----------------------------- */
+
+/* src/buffers.rs:9-22 (Params) / compute_shader.wgsl:43-58. 48 bytes. */
+typedef struct rt_params {
+    uint32_t screen_width;
+    uint32_t accumulation_index;
+    uint32_t accumulate;
+    uint32_t sphere_count;
+    uint32_t object_count;
+    uint32_t compute_per_frame;
+    uint32_t texture_width;
+    uint32_t texture_height;
+    uint32_t texture_count; /* `textue_count` in the reference */
+    uint32_t env_map_width;
+    uint32_t env_map_height;
+    uint32_t _padding;
+} rt_params;
+
+/* src/buffers.rs:26-29 (RayCamera). 16 bytes. */
+typedef struct rt_ray_camera {
+    float origin[3];
+    uint32_t _padding;
+} rt_ray_camera;
+
+/* src/buffers.rs:33-36 (Ray): a cached per-pixel camera ray direction. 16 bytes. */
+typedef struct rt_ray {
+    float direction[3];
+    uint32_t _padding;
+} rt_ray;
+
+/* src/buffers.rs:40-45 (SceneSphere). 32 bytes. */
+typedef struct rt_scene_sphere {
+    float position[3];
+    float radius;
+    uint32_t material_index;
+    uint32_t _padding[3];
+} rt_scene_sphere;
+
+/* src/buffers.rs:49-64 (SceneTriangle), built by SceneTriangle::new
+ * (src/buffers.rs:66-95): edge_ab = b-a, edge_ac = c-a,
+ * calc_normal = edge_ab x edge_ac, face_normal = normalize(calc_normal).
+ * 112 bytes. min/max_bounds are host-only (the kernel never reads them). */
+typedef struct rt_scene_triangle {
+    float a[3];           uint32_t _padding0;
+    float edge_ab[3];     uint32_t _padding1;
+    float edge_ac[3];     uint32_t _padding2;
+    float calc_normal[3]; uint32_t _padding3;
+    float face_normal[3]; uint32_t _padding4;
+    float min_bounds[3];  uint32_t _padding5;
+    float max_bounds[3];  uint32_t _padding6;
+} rt_scene_triangle;
+
+/* src/buffers.rs:100-109 (SceneMaterial). 32 bytes. */
+typedef struct rt_scene_material {
+    uint32_t texture_index;
+    float roughness;
+    float emission_power;
+    float specular;
+    float specular_scatter;
+    float glass;
+    float refraction_index;
+    uint32_t _padding;
+} rt_scene_material;
+
+/* src/buffers.rs:113-120 (ObjectInfo). 48 bytes. */
+typedef struct rt_object_info {
+    float min_bounds[3];
+    uint32_t first_sub_object_index;
+    float max_bounds[3];
+    uint32_t sub_object_count;
+    uint32_t material_index;
+    uint32_t _padding[3];
+} rt_object_info;
+
+/* src/buffers.rs:124-129 (SubObjectInfo). 32 bytes. */
+typedef struct rt_sub_object_info {
+    float min_bounds[3];
+    uint32_t first_triangle_index;
+    float max_bounds[3];
+    uint32_t triangle_count;
+} rt_sub_object_info;
+
+/* ---- context ------------------------------------------------------------ */
+
+typedef struct rt_ctx rt_ctx;
+
+/* Everything DataBuffers::new (src/buffers.rs:159-170) receives, plus the
+ * framebuffer height (Params carries only the width) and the device.
+ * Array capacities are fixed here, as wgpu buffer sizes are fixed at
+ * creation; later rt_update_* calls must fit. Zero-length arrays are allowed
+ * (the reference needs a dummy element because WGSL arrays cannot be empty). */
+typedef struct rt_create_info {
+    uint32_t width;
+    uint32_t height;
+    int32_t device;              /* HIP device ordinal */
+    uint32_t _reserved;
+    rt_ray_camera camera;        /* binding 3 */
+    const rt_ray* camera_rays;   /* binding 1, width*height entries */
+    const rt_scene_material* materials; uint32_t material_count;   /* binding 4 */
+    const rt_scene_sphere* spheres;     uint32_t sphere_count;     /* binding 5 */
+    const rt_scene_triangle* triangles; uint32_t triangle_count;   /* binding 7 */
+    const rt_object_info* objects;      uint32_t object_count;     /* binding 8 */
+    const rt_sub_object_info* sub_objects; uint32_t sub_object_count; /* binding 10 */
+    rt_params params;            /* binding 0: initial Params (Renderer::new, src/main.rs:131-144) */
+    /* Tile partition for multi-GPU: the image is cut into 8x8
+     * pixel tiles, tile t is rendered by rank (t % world_size). A context
+     * with world_size == 1 renders every pixel, as the reference does. */
+    uint32_t rank;
+    uint32_t world_size;
+} rt_create_info;
+
+/* Renderer::new -> DataBuffers::new (src/renderer.rs:42-101,
+ * src/buffers.rs:159-298). Allocates and fills every device buffer. Unlike the
+ * reference (accumulation created uninitialised, src/buffers.rs:217-222) the
+ * accumulation buffer starts zeroed. The renderer's accumulation counter k
+ * starts at 1 (src/renderer.rs:96). */
+RT_API int rt_create(const rt_create_info* info, rt_ctx** out_ctx);
+RT_API void rt_destroy(rt_ctx* ctx);
+RT_API const char* rt_last_error(const rt_ctx* ctx); /* never NULL; "" when no error */
+RT_API int rt_abi_version(void);
+
+/* DataBuffers::update_texture_buffer (src/buffers.rs:479-511): `layers`
+ * RGBA8 (sRGB-encoded, Rgba8UnormSrgb) images of width x height, tightly
+ * packed, row 0 first. Resizes the texture array when the size changes. */
+RT_API int rt_upload_textures(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height, uint32_t layers);
+/* DataBuffers::update_environment_map_buffer (src/buffers.rs:513-539). */
+RT_API int rt_upload_env_map(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height);
+
+/* DataBuffers::update_accumulation (src/buffers.rs:557-559): write Params. */
+RT_API int rt_update_params(rt_ctx* ctx, const rt_params* params);
+/* DataBuffers::reset_accumulation (src/buffers.rs:545-555): zero the
+ * accumulation buffer and write Params; also resets the context's
+ * accumulation counter to params->accumulation_index (Renderer sets it to 1,
+ * src/renderer.rs:131-151). */
+RT_API int rt_reset_accumulation(rt_ctx* ctx, const rt_params* params);
+
+/* DataBuffers::update_* (src/buffers.rs:541-595) and the camera write in
+ * Renderer::on_update (src/renderer.rs:116-125). Writes start at element 0;
+ * `count` must not exceed the capacity given at rt_create. */
+RT_API int rt_update_ray_directions(rt_ctx* ctx, const rt_ray* rays, uint32_t count);
+RT_API int rt_update_camera(rt_ctx* ctx, const rt_ray_camera* camera);
+RT_API int rt_update_spheres(rt_ctx* ctx, const rt_scene_sphere* spheres, uint32_t count);
+RT_API int rt_update_triangles(rt_ctx* ctx, const rt_scene_triangle* triangles, uint32_t count);
+RT_API int rt_update_object_info(rt_ctx* ctx, const rt_object_info* objects, uint32_t count);
+RT_API int rt_update_sub_object_info(rt_ctx* ctx, const rt_sub_object_info* sub_objects, uint32_t count);
+RT_API int rt_update_materials(rt_ctx* ctx, const rt_scene_material* materials, uint32_t count);
+
+/* The compute pass of Renderer::compute_frame (src/renderer.rs:238-249):
+ * one launch of the path-tracing kernel with the Params currently on the
+ * device. `bounces` is the per-path bounce limit (the reference hard-codes
+ * 10, compute_shader.wgsl:150). Asynchronous. */
+RT_API int rt_dispatch(rt_ctx* ctx, uint32_t bounces);
+
+/* Renderer::compute_frame (src/renderer.rs:201-252): if Params.accumulate
+ * is 1, write Params with accumulation_index = k and then k += 1; then
+ * rt_dispatch. Asynchronous. */
+RT_API int rt_compute_frame(rt_ctx* ctx, uint32_t bounces);
+
+/* Blocks until all work on the context's stream has finished. */
+RT_API int rt_synchronize(rt_ctx* ctx);
+
+/* Readback (new: the reference only blits output_data to the swapchain,
+ * src/renderer.rs:254-283). Synchronous; whole framebuffer, row-major
+ * width*height. Pixels of tiles owned by another rank are left as they were
+ * (zero unless written). */
+RT_API int rt_read_output(rt_ctx* ctx, uint32_t* rgba8_out);
+RT_API int rt_read_accumulation(rt_ctx* ctx, float* rgba_f32_out);
+
+/* Counted ray segments (every trace_ray call: primary + bounce, a path that
+ * escapes to the environment stops counting), summed over all dispatches
+ * since creation or the last rt_reset_ray_count. Synchronous. */
+RT_API int rt_ray_count(rt_ctx* ctx, uint64_t* out);
+RT_API int rt_reset_ray_count(rt_ctx* ctx);
+
+/* Current accumulation counter k (the value the next rt_compute_frame uses). */
+RT_API int rt_accumulation_index(const rt_ctx* ctx, uint32_t* out);
+
+/* Timing of the last rt_dispatch/rt_compute_frame launch, measured with HIP
+ * events recorded on the context's stream around the kernel (milliseconds);
+ * requires rt_set_timing(ctx, 1) before the launch. Synchronous. */
+RT_API int rt_set_timing(rt_ctx* ctx, int enable);
+RT_API int rt_last_dispatch_ms(rt_ctx* ctx, float* out_ms);
+/* Sum of the timed dispatch durations since the last rt_reset_timing, and
+ * how many dispatches were timed (each one's events are read back at the next
+ * launch or on this call, so timing a long run adds no host sync per frame). */
+RT_API int rt_dispatch_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed);
+RT_API int rt_reset_timing(rt_ctx* ctx);
+
+/* Multi-GPU gather support. The pixels owned by this context's
+ * rank, in tile order, are packed into / unpacked from a contiguous device
+ * buffer so one RCCL collective moves them. Sizes are in pixels. */
+RT_API int rt_owned_pixel_count(const rt_ctx* ctx, uint32_t rank, uint32_t world_size, uint64_t* out);
+/* Pack this rank's accumulation (float4 per pixel) into device memory `dst`
+ * (rt_owned_pixel_count * 16 bytes). Stream-ordered on the context's stream. */
+RT_API int rt_pack_owned_accumulation(rt_ctx* ctx, void* dst_device);
+/* Unpack a block packed by `src_rank` of `world_size` into this context's
+ * accumulation buffer and re-pack the RGBA8 output for those pixels with
+ * the given accumulation divisor (k*c, src/compute_shader.wgsl:166). */
+RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size,
+                           uint32_t divisor);
+
+/* The context's HIP stream (hipStream_t), for callers that want to order
+ * their own device work (e.g. an RCCL collective) after a frame. */
+RT_API void* rt_stream(rt_ctx* ctx);
+
+/* The 256-entry sRGB -> linear table the kernel decodes Rgba8UnormSrgb
+ * texels with (IEC 61966-2-1, rounded to f32). For tests. */
+RT_API int rt_srgb_table(float out[256]);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RT_ABI_H */

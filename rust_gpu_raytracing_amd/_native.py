@@ -1,0 +1,174 @@
+"""ctypes binding of the C ABI in ``include/rt_abi.h``.
+
+The shared library ``librt_pathtrace.so`` (HIP kernel + host runtime) is built
+in-tree by ``rust_gpu_raytracing_amd.build``. There is no fallback: if the
+library is missing or fails to load, every entry point raises
+:class:`NativeLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import buffers as B
+
+LIB_NAME = "librt_pathtrace.so"
+LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+
+RT_OK = 0
+RT_E_INVALID = -1
+RT_E_HIP = -2
+RT_E_NOMEM = -3
+RT_E_CAPACITY = -4
+RT_E_NODEVICE = -5
+
+_ERR_NAMES = {
+    RT_E_INVALID: "RT_E_INVALID",
+    RT_E_HIP: "RT_E_HIP",
+    RT_E_NOMEM: "RT_E_NOMEM",
+    RT_E_CAPACITY: "RT_E_CAPACITY",
+    RT_E_NODEVICE: "RT_E_NODEVICE",
+}
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP extension is missing or could not be loaded."""
+
+
+class RtError(RuntimeError):
+    """A C-ABI call returned a negative status."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{_ERR_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+class rt_ray_camera(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_float * 3), ("_padding", ctypes.c_uint32)]
+
+
+class rt_params(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_uint32) for name in B.PARAMS.names]
+
+
+class rt_create_info(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_uint32),
+        ("height", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("_reserved", ctypes.c_uint32),
+        ("camera", rt_ray_camera),
+        ("camera_rays", ctypes.c_void_p),
+        ("materials", ctypes.c_void_p),
+        ("material_count", ctypes.c_uint32),
+        ("spheres", ctypes.c_void_p),
+        ("sphere_count", ctypes.c_uint32),
+        ("triangles", ctypes.c_void_p),
+        ("triangle_count", ctypes.c_uint32),
+        ("objects", ctypes.c_void_p),
+        ("object_count", ctypes.c_uint32),
+        ("sub_objects", ctypes.c_void_p),
+        ("sub_object_count", ctypes.c_uint32),
+        ("params", rt_params),
+        ("rank", ctypes.c_uint32),
+        ("world_size", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(rt_params) == 48
+assert ctypes.sizeof(rt_ray_camera) == 16
+
+# name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+SIGNATURES = {
+    "rt_create": (ctypes.c_int, [ctypes.POINTER(rt_create_info), ctypes.POINTER(_P)]),
+    "rt_destroy": (None, [_P]),
+    "rt_last_error": (ctypes.c_char_p, [_P]),
+    "rt_abi_version": (ctypes.c_int, []),
+    "rt_upload_textures": (ctypes.c_int, [_P, _P, _U32, _U32, _U32]),
+    "rt_upload_env_map": (ctypes.c_int, [_P, _P, _U32, _U32]),
+    "rt_update_params": (ctypes.c_int, [_P, ctypes.POINTER(rt_params)]),
+    "rt_reset_accumulation": (ctypes.c_int, [_P, ctypes.POINTER(rt_params)]),
+    "rt_update_ray_directions": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_update_camera": (ctypes.c_int, [_P, ctypes.POINTER(rt_ray_camera)]),
+    "rt_update_spheres": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_update_triangles": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_update_object_info": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_update_sub_object_info": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_update_materials": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_dispatch": (ctypes.c_int, [_P, _U32]),
+    "rt_compute_frame": (ctypes.c_int, [_P, _U32]),
+    "rt_synchronize": (ctypes.c_int, [_P]),
+    "rt_read_output": (ctypes.c_int, [_P, _P]),
+    "rt_read_accumulation": (ctypes.c_int, [_P, _P]),
+    "rt_ray_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_reset_ray_count": (ctypes.c_int, [_P]),
+    "rt_accumulation_index": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
+    "rt_last_dispatch_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
+    "rt_dispatch_time_total": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_reset_timing": (ctypes.c_int, [_P]),
+    "rt_owned_pixel_count": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_pack_owned_accumulation": (ctypes.c_int, [_P, _P]),
+    "rt_unpack_accumulation": (ctypes.c_int, [_P, _P, _U32, _U32, _U32]),
+    "rt_stream": (_P, [_P]),
+    "rt_srgb_table": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
+}
+
+_lib = None
+
+
+def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load (once) and return the HIP extension; raise if it is unavailable."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise NativeLibraryError(
+            f"{p} not found: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    try:
+        lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    except OSError as exc:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"could not load {p}: {exc}") from exc
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(ctx, rc: int) -> None:
+    if rc != RT_OK:
+        msg = load_library().rt_last_error(ctx)
+        raise RtError(rc, msg.decode() if msg else "")
+
+
+def ptr(a: np.ndarray | None) -> int | None:
+    if a is None or a.size == 0:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays handed to the C ABI must be C-contiguous"
+    return a.ctypes.data
+
+
+def params_struct(p: np.ndarray) -> rt_params:
+    s = rt_params()
+    for name in B.PARAMS.names:
+        setattr(s, name, int(p[name]))
+    return s
+
+
+def srgb_table() -> np.ndarray:
+    out = np.zeros(256, np.float32)
+    rc = load_library().rt_srgb_table(out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    if rc != RT_OK:
+        raise RtError(rc, "rt_srgb_table")
+    return out

@@ -1,0 +1,444 @@
+// pathtrace.hip — the per-pixel path-tracing kernel for gfx950 (CDNA4).
+//
+// Replaces src/compute_shader.wgsl::main (:146-189) and everything it calls.
+// Behaviour is the reference's, decision for decision (SURVEY.md §8a rows
+// a6-a18); the numeric contract that makes it bit-exact against the CPU
+// oracle is in rt_device_math.h. What is MI355X-specific:
+//
+//  * Work unit = one 8x8 pixel tile per wave64 (the reference's workgroup,
+//    :146), four tiles per 256-thread workgroup. Tiles are dealt to ranks
+//    round-robin (tile t -> rank t % world) so a multi-GPU split is a launch
+//    argument, not a different kernel; seeds depend only on the global pixel
+//    index (:217), so any split is bitwise identical to one GPU.
+//  * Scene staging: spheres (as centre + radius^2), materials and objects are
+//    copied once per workgroup into LDS; every wave then sweeps the sphere and
+//    object lists with wave-uniform indices (LDS broadcast reads, no bank
+//    conflicts). Sub-objects and triangles are read from HBM/L2 with
+//    wave-uniform addresses (scalar loads).
+//  * Textures stay RGBA8 (4 B per fetch) and are decoded with a 256-entry
+//    sRGB table in LDS, as the Rgba8UnormSrgb format does in hardware.
+//  * Counted ray segments are summed per workgroup in LDS and added to one
+//    64-bit device counter with a single atomic per workgroup.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_device_math.h"
+#include "rt_kernel_args.h"
+
+#pragma clang fp contract(off)
+
+using namespace rtk;
+
+namespace {
+
+struct Hit {
+    float t;
+    f3 p;
+    f3 n;
+    uint32_t material_index;
+    bool front_face;
+    float u, v;
+};
+
+struct SceneView {
+    const float4* sph;        // LDS or global: centre.xyz, radius^2
+    const uint32_t* sph_mat;  // material index per sphere
+    const RtMaterial* mat;    // LDS
+    const RtObject* obj;      // LDS
+    const float* srgb;        // LDS, 256 entries
+};
+
+__device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
+
+__device__ __forceinline__ int texel_coord(float c, uint32_t size) {
+    // Truncate toward zero, then clamp to [0, size-1]; NaN -> 0 (naga Restrict).
+    if (!(c >= 0.0f)) return 0;
+    if (c >= (float)size) return (int)size - 1;
+    const int i = (int)c;
+    return i > (int)size - 1 ? (int)size - 1 : i;
+}
+
+__device__ __forceinline__ f4 decode_texel(uint32_t texel, const float* srgb) {
+    return f4{srgb[texel & 0xffu], srgb[(texel >> 8) & 0xffu], srgb[(texel >> 16) & 0xffu],
+              (float)(texel >> 24) / 255.0f};
+}
+
+// check_spheres, compute_shader.wgsl:355-404. Returns the closest index or -1.
+__device__ __forceinline__ int closest_sphere(const SceneView& sv, uint32_t count, f3 o, f3 d, float& t_out) {
+    float closest = kF32Max;
+    int closest_i = -1;
+    const float a = dot(d, d);
+    const float four_a = 4.0f * a;
+    const float two_a = 2.0f * a;
+    for (uint32_t i = 0; i < count; ++i) {
+        const float4 s = sv.sph[i];
+        const f3 oc = o - ld3(s);
+        const float b = 2.0f * dot(d, oc);
+        const float c = dot(oc, oc) - s.w;
+        const float disc = b * b - four_a * c;
+        if (disc >= 0.0f) {
+            const float t = (-b - sqrt_rn(disc)) / two_a;
+            if (t > 0.0f && t < closest) {
+                closest = t;
+                closest_i = (int)i;
+            }
+        }
+    }
+    t_out = closest;
+    return closest_i;
+}
+
+// ray_in_bounds, compute_shader.wgsl:407-419.
+__device__ __forceinline__ bool ray_in_bounds(f3 o, f3 inv, const float* mn, const float* mx) {
+    const float tminx = (mn[0] - o.x) * inv.x, tmaxx = (mx[0] - o.x) * inv.x;
+    const float tminy = (mn[1] - o.y) * inv.y, tmaxy = (mx[1] - o.y) * inv.y;
+    const float tminz = (mn[2] - o.z) * inv.z, tmaxz = (mx[2] - o.z) * inv.z;
+    const float near_t = fmax_nn(fmax_nn(fmin_nn(tminx, tmaxx), fmin_nn(tminy, tmaxy)), fmin_nn(tminz, tmaxz));
+    const float far_t = fmin_nn(fmin_nn(fmax_nn(tminx, tmaxx), fmax_nn(tminy, tmaxy)), fmax_nn(tminz, tmaxz));
+    return near_t <= far_t && far_t >= 0.0f;
+}
+
+// check_triangles, compute_shader.wgsl:422-517. Updates `h` when a triangle
+// is closer than `closest` (which starts at F32_MAX, independent of spheres).
+__device__ __forceinline__ void closest_triangle(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, Hit& h) {
+    float closest = kF32Max;
+    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint32_t n_obj = ka.object_count;
+    for (uint32_t oi = 0; oi < n_obj; ++oi) {
+        const RtObject& ob = sv.obj[oi];
+        if (!ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds)) continue;
+        const uint32_t first_sub = ob.first_sub_object_index;
+        const uint32_t n_sub = ob.sub_object_count;
+        for (uint32_t i = 0; i < n_sub; ++i) {
+            const uint32_t si = min(first_sub + i, ka.sub_object_count - 1u);
+            const RtSubObject sub = ka.sub_objects[si];
+            if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
+            for (uint32_t j = 0; j < sub.triangle_count; ++j) {
+                const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
+                const RtTriangleHot& tr = ka.triangles[ti];
+                const f3 cn = ld3(tr.calc_normal);
+                const float det = -dot(d, cn);
+                const float inv_det = 1.0f / det;
+                const f3 ao = o - ld3(tr.a);
+                const float dist = dot(ao, cn) * inv_det;
+                if (dist < 0.0f || dist >= closest) continue;
+                const f3 dao = cross(ao, d);
+                const float v = -dot(ld3(tr.edge_ab), dao) * inv_det;
+                if (v < 0.0f) continue;
+                const float u = dot(ld3(tr.edge_ac), dao) * inv_det;
+                if (u < 0.0f) continue;
+                const float w = 1.0f - u - v;
+                if (w < 0.0f) continue;
+                const f3 fn = ld3(tr.face_normal);
+                h.front_face = det > 0.0f;
+                h.n = h.front_face ? fn : -fn;
+                closest = dist;
+                h.t = dist;
+                h.p = o + d * dist;
+                // object_texture_coords, :568-578 (uv from the OBJECT bounds)
+                h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
+                h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
+                h.material_index = ob.material_index;
+            }
+        }
+    }
+}
+
+// trace_ray, compute_shader.wgsl:342-353: sphere wins only if strictly closer.
+__device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d) {
+    Hit h;
+    h.t = kF32Max;
+    h.p = mk(0.f, 0.f, 0.f);
+    h.n = mk(0.f, 0.f, 0.f);
+    h.material_index = 0;
+    h.front_face = false;
+    h.u = 0.f;
+    h.v = 0.f;
+    if (ka.object_count != 0) closest_triangle(sv, ka, o, d, h);
+    float ts;
+    const int si = closest_sphere(sv, ka.sphere_count, o, d, ts);
+    if (si >= 0 && ts < h.t) {
+        // sphere_hit, :530-555, and sphere_texture_coords, :557-566
+        const float4 s = sv.sph[si];
+        const f3 p = o + d * ts;
+        const f3 outward = normalize(p - ld3(s));
+        const float theta = acosf_c(-outward.y);
+        const float phi = atan2f_c(-outward.z, outward.x) + kWgslPi;
+        h.t = ts;
+        h.p = p;
+        h.u = phi / kTwoPiWgsl;
+        h.v = theta / kWgslPi;
+        h.front_face = dot(d, outward) < 0.0f;
+        h.n = h.front_face ? outward : -outward;
+        h.material_index = sv.sph_mat[si];
+    }
+    return h;
+}
+
+__device__ __forceinline__ f4 sample_texture(const KernelArgs& ka, const float* srgb, uint32_t layer, float u,
+                                             float v) {
+    const int x = texel_coord(u * (float)(int32_t)ka.texture_width, ka.tex_w);
+    const int y = texel_coord(v * (float)(int32_t)ka.texture_height, ka.tex_h);
+    const uint32_t l = min(layer, ka.tex_layers - 1u);
+    const size_t off = ((size_t)l * ka.tex_h + (size_t)y) * ka.tex_w + (size_t)x;
+    return decode_texel(ka.textures[off], srgb);
+}
+
+__device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb, f3 d) {
+    // environment_map_coords, :580-585
+    const float u = 0.5f + atan2f_c(d.z, d.x) / kTwoPiWgsl;
+    const float v = 0.5f + asinf_c(d.y) / kWgslPi;
+    const int x = texel_coord(u * (float)(int32_t)ka.env_map_width, ka.env_w);
+    const int y = texel_coord(v * (float)(int32_t)ka.env_map_height, ka.env_h);
+    return decode_texel(ka.env[(size_t)y * ka.env_w + (size_t)x], srgb);
+}
+
+// per_pixel, compute_shader.wgsl:210-314.
+__device__ __forceinline__ f4 per_pixel(const SceneView& sv, const KernelArgs& ka, uint32_t index,
+                                        uint32_t random_index, uint32_t& rays) {
+    f3 o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
+    const float4 cr = ka.camera_rays[index];
+    f3 d = mk(cr.x, cr.y, cr.z);
+    uint32_t seed = index * random_index * 326624u;
+    {
+        const float rx = random01(seed), ry = random01(seed), rz = random01(seed);
+        const f3 jit = mk(rx * 2.0f - 1.0f, ry * 2.0f - 1.0f, rz * 2.0f - 1.0f);
+        d = d + jit * 0.0005f;  // not renormalised (:219)
+    }
+    f4 contrib{1.0f, 1.0f, 1.0f, 1.0f};
+    f4 light{0.0f, 0.0f, 0.0f, 0.0f};
+    for (uint32_t i = 0; i < ka.bounces; ++i) {
+        const Hit h = trace_ray(sv, ka, o, d);
+        ++rays;
+        if (h.t == kF32Max) {
+            const f4 c = sample_env(ka, sv.srgb, d);
+            light.x = light.x + c.x * contrib.x;
+            light.y = light.y + c.y * contrib.y;
+            light.z = light.z + c.z * contrib.z;
+            light.w = light.w + c.w * contrib.w;
+            break;
+        }
+        const RtMaterial m = sv.mat[min(h.material_index, ka.material_count - 1u)];
+        const float gx = normal01(seed);
+        const float gy = normal01(seed);
+        const float gz = normal01(seed);
+        const f3 diffuse = normalize(h.n + mk(gx, gy, gz));
+        const f3 specular = d - h.n * (2.0f * dot(h.n, d));  // reflect(d, n)
+        const f4 color = sample_texture(ka, sv.srgb, m.texture_index, h.u, h.v);
+        const float e = m.emission_power;
+        light.x = light.x + (color.x * e) * contrib.x;
+        light.y = light.y + (color.y * e) * contrib.y;
+        light.z = light.z + (color.z * e) * contrib.z;
+        light.w = light.w + (color.w * e) * contrib.w;
+        const bool is_glass = m.glass > random01(seed);
+        bool tint;
+        if (is_glass) {
+            float ior = m.refraction_index;
+            if (h.front_face) ior = 1.0f / ior;
+            const float cos_t = fmin_nn(dot(-d, h.n), 1.0f);
+            const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
+            const bool reflects = ior * sin_t > 1.0f;
+            float r0 = (1.0f - ior) / (1.0f + ior);  // specular_percentage, :328-334
+            r0 = r0 * r0;
+            const float sp = r0 + (1.0f - r0) * pow5(1.0f - cos_t);
+            const bool is_spec = (m.specular * sp) > random01(seed);
+            if (reflects || is_spec) {
+                d = lerp(specular, diffuse, m.specular_scatter);
+                o = h.p + h.n * 0.0001f;
+                tint = false;
+            } else {
+                // refract, :316-325
+                const f3 perp = (d + h.n * cos_t) * ior;
+                const float len = sqrt_rn(dot(perp, perp));
+                const float len_sq = len * len;
+                const f3 refr = perp + h.n * (-sqrt_rn(__builtin_fabsf(1.0f - len_sq)));
+                d = lerp(refr, diffuse, m.roughness / 10.0f);
+                o = h.p - h.n * 0.0001f;
+                tint = true;
+            }
+        } else {
+            const bool is_spec = m.specular > random01(seed);
+            if (is_spec) {
+                d = lerp(specular, diffuse, m.specular_scatter);
+                tint = false;
+            } else {
+                d = lerp(specular, diffuse, m.roughness);
+                tint = true;
+            }
+            o = h.p + h.n * 0.0001f;
+        }
+        if (tint) {
+            contrib.x = contrib.x * color.x;
+            contrib.y = contrib.y * color.y;
+            contrib.z = contrib.z * color.z;
+            contrib.w = contrib.w * color.w;
+        }
+    }
+    return light;
+}
+
+__device__ __forceinline__ float clamp01(float x) { return fmin_nn(fmax_nn(x, 0.0f), 1.0f); }
+
+// pack_to_u32, compute_shader.wgsl:192-208.
+__device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float a) {
+    const uint32_t br = (uint32_t)(r * 255.0f) & 0xffu;
+    const uint32_t bg = (uint32_t)(g * 255.0f) & 0xffu;
+    const uint32_t bb = (uint32_t)(b * 255.0f) & 0xffu;
+    const uint32_t ba = (uint32_t)(a * 255.0f) & 0xffu;
+    return br | (bg << 8) | (bb << 16) | (ba << 24);
+}
+
+}  // namespace
+
+// Dynamic LDS image, in this order (all 16-byte aligned):
+//   float4   spheres[sphere_count]   centre.xyz, radius^2
+//   RtMaterial materials[material_count]
+//   RtObject objects[object_count]
+//   uint32   sphere_material[sphere_count]
+//   float    srgb[256]
+// kSceneInLds = false keeps spheres/materials/objects in global memory (for
+// scenes beyond the LDS budget); the sRGB table is always staged.
+template <bool kSceneInLds>
+__global__ void __launch_bounds__(kBlockThreads) rt_pathtrace_kernel(KernelArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t block_rays;
+
+    const uint32_t tid = threadIdx.x;
+    float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
+    const float4* sph = ka.sphere_hot;
+    const uint32_t* smat = ka.sphere_material;
+    const RtMaterial* mat = ka.materials;
+    const RtObject* obj = ka.objects;
+    if (tid == 0) block_rays = 0;
+    if constexpr (kSceneInLds) {
+        float4* l_sph = reinterpret_cast<float4*>(lds);
+        RtMaterial* l_mat = reinterpret_cast<RtMaterial*>(lds + ka.lds_mat_offset);
+        RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
+        uint32_t* l_smat = reinterpret_cast<uint32_t*>(lds + ka.lds_smat_offset);
+        for (uint32_t i = tid; i < ka.sphere_count; i += kBlockThreads) {
+            l_sph[i] = ka.sphere_hot[i];
+            l_smat[i] = ka.sphere_material[i];
+        }
+        for (uint32_t i = tid; i < ka.material_count; i += kBlockThreads) l_mat[i] = ka.materials[i];
+        for (uint32_t i = tid; i < ka.object_count; i += kBlockThreads) l_obj[i] = ka.objects[i];
+        sph = l_sph;
+        smat = l_smat;
+        mat = l_mat;
+        obj = l_obj;
+    }
+    for (uint32_t i = tid; i < 256u; i += kBlockThreads) l_srgb[i] = ka.srgb[i];
+    __syncthreads();
+
+    const SceneView sv{sph, smat, mat, obj, l_srgb};
+
+    const uint32_t wave = tid >> 6;
+    const uint32_t lane = tid & 63u;
+    const uint32_t local_tile = blockIdx.x * kTilesPerBlock + wave;
+    uint32_t rays = 0;
+    if (local_tile < ka.owned_tiles) {
+        const uint32_t tile = local_tile * ka.world_size + ka.rank;
+        const uint32_t x = (tile % ka.tiles_x) * 8u + (lane & 7u);
+        const uint32_t y = (tile / ka.tiles_x) * 8u + (lane >> 3);
+        if (x < ka.width && y < ka.height) {
+            const uint32_t index = y * ka.width + x;
+            float r, g, b, a;
+            if (ka.accumulate == 1u) {
+                float4 px = ka.accum[index];
+                uint32_t random_index = ka.accumulation_index;
+                for (uint32_t i = 0; i < ka.compute_per_frame; ++i) {
+                    const f4 l = per_pixel(sv, ka, index, random_index, rays);
+                    px.x = px.x + l.x;
+                    px.y = px.y + l.y;
+                    px.z = px.z + l.z;
+                    px.w = px.w + l.w;
+                    random_index = random_index + 1u;
+                }
+                ka.accum[index] = px;
+                const float div = (float)(ka.accumulation_index * ka.compute_per_frame);
+                r = clamp01(px.x / div);
+                g = clamp01(px.y / div);
+                b = clamp01(px.z / div);
+                a = clamp01(px.w / div);
+            } else {
+                const f4 l = per_pixel(sv, ka, index, ka.accumulation_index, rays);
+                r = clamp01(l.x);
+                g = clamp01(l.y);
+                b = clamp01(l.z);
+                a = clamp01(l.w);
+            }
+            ka.output[index] = pack_rgba8(r, g, b, a);
+        }
+    }
+    atomicAdd(&block_rays, rays);
+    __syncthreads();
+    if (tid == 0 && block_rays != 0) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
+}
+
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t lds_bytes, uint32_t blocks,
+                               hipStream_t stream) {
+    if (scene_in_lds) {
+        hipLaunchKernelGGL(rt_pathtrace_kernel<true>, dim3(blocks), dim3(kBlockThreads), lds_bytes, stream, ka);
+    } else {
+        hipLaunchKernelGGL(rt_pathtrace_kernel<false>, dim3(blocks), dim3(kBlockThreads), lds_bytes, stream, ka);
+    }
+    return hipGetLastError();
+}
+
+// Gather support: pack the accumulation of this rank's tiles, in
+// local-tile order (64 float4 per tile), into a contiguous buffer.
+extern "C" __global__ void __launch_bounds__(256) rt_pack_tiles_kernel(const float4* __restrict__ accum,
+                                                                      float4* __restrict__ dst, uint32_t width,
+                                                                      uint32_t height, uint32_t tiles_x,
+                                                                      uint32_t owned_tiles, uint32_t rank,
+                                                                      uint32_t world) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t local_tile = gid >> 6;
+    if (local_tile >= owned_tiles) return;
+    const uint32_t lane = (uint32_t)(gid & 63u);
+    const uint32_t tile = (uint32_t)local_tile * world + rank;
+    const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u);
+    const uint32_t y = (tile / tiles_x) * 8u + (lane >> 3);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (x < width && y < height) v = accum[(size_t)y * width + x];
+    dst[gid] = v;
+}
+
+extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(const float4* __restrict__ src,
+                                                                        float4* __restrict__ accum,
+                                                                        uint32_t* __restrict__ output, uint32_t width,
+                                                                        uint32_t height, uint32_t tiles_x,
+                                                                        uint32_t owned_tiles, uint32_t rank,
+                                                                        uint32_t world, float divisor) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t local_tile = gid >> 6;
+    if (local_tile >= owned_tiles) return;
+    const uint32_t lane = (uint32_t)(gid & 63u);
+    const uint32_t tile = (uint32_t)local_tile * world + rank;
+    const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u);
+    const uint32_t y = (tile / tiles_x) * 8u + (lane >> 3);
+    if (x >= width || y >= height) return;
+    const float4 v = src[gid];
+    const size_t idx = (size_t)y * width + x;
+    accum[idx] = v;
+    output[idx] = pack_rgba8(clamp01(v.x / divisor), clamp01(v.y / divisor), clamp01(v.z / divisor),
+                             clamp01(v.w / divisor));
+}
+
+hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
+                          uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream) {
+    const uint64_t threads = (uint64_t)owned_tiles * 64u;
+    const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
+    hipLaunchKernelGGL(rt_pack_tiles_kernel, dim3(blocks), dim3(256), 0, stream, accum, dst, width, height, tiles_x,
+                       owned_tiles, rank, world);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
+                            uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, float divisor,
+                            hipStream_t stream) {
+    const uint64_t threads = (uint64_t)owned_tiles * 64u;
+    const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
+    hipLaunchKernelGGL(rt_unpack_tiles_kernel, dim3(blocks), dim3(256), 0, stream, src, accum, output, width, height,
+                       tiles_x, owned_tiles, rank, world, divisor);
+    return hipGetLastError();
+}

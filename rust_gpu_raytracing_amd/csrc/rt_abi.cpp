@@ -1,0 +1,736 @@
+// rt_abi.cpp — host implementation of include/rt_abi.h.
+//
+// Replaces the wgpu side of the reference's per-frame path:
+//   DataBuffers (src/buffers.rs:140-596)  -> hipMalloc'd device buffers, updated
+//                                            through a pinned staging buffer with
+//                                            hipMemcpyAsync on the context stream
+//   Renderer::compute_frame (src/renderer.rs:201-252)
+//                                         -> Params shadow + hipLaunchKernelGGL
+// Stream order gives the same visibility guarantees as wgpu's queue order.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_abi.h"
+#include "rt_kernel_args.h"
+
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t lds_bytes, uint32_t blocks,
+                               hipStream_t stream);
+hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
+                          uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
+hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
+                            uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, float divisor,
+                            hipStream_t stream);
+
+static_assert(sizeof(rt_params) == 48, "Params is 48 bytes (src/buffers.rs:9-22)");
+static_assert(sizeof(rt_ray_camera) == 16, "RayCamera is 16 bytes");
+static_assert(sizeof(rt_ray) == 16, "Ray is 16 bytes");
+static_assert(sizeof(rt_scene_sphere) == 32, "SceneSphere is 32 bytes");
+static_assert(sizeof(rt_scene_triangle) == 112, "SceneTriangle is 112 bytes");
+static_assert(sizeof(rt_scene_material) == 32, "SceneMaterial is 32 bytes");
+static_assert(sizeof(rt_object_info) == 48, "ObjectInfo is 48 bytes");
+static_assert(sizeof(rt_sub_object_info) == 32, "SubObjectInfo is 32 bytes");
+static_assert(sizeof(rt_scene_material) == sizeof(RtMaterial), "material record");
+static_assert(sizeof(rt_object_info) == sizeof(RtObject), "object record");
+static_assert(sizeof(rt_sub_object_info) == sizeof(RtSubObject), "sub-object record");
+
+namespace {
+
+constexpr size_t kLdsSceneBudget = 64 * 1024;  // dynamic LDS the scene may take per workgroup
+
+thread_local std::string g_create_error;
+
+struct EventPair {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
+}  // namespace
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t width = 0, height = 0;
+    uint64_t n_pixels = 0;
+    uint32_t rank = 0, world = 1;
+    uint32_t tiles_x = 0, tiles_y = 0, owned_tiles = 0;
+
+    rt_params params{};  // shadow of binding 0
+    uint32_t k = 1;      // Renderer::accumulation_index (src/renderer.rs:37)
+    rt_ray_camera camera{};
+
+    uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
+    // extents the kernel clamps against (>= 1 so clamps never underflow)
+    uint32_t n_mat_dev = 1, n_tri_dev = 1, n_sub_dev = 1;
+
+    float4* d_rays = nullptr;
+    float4* d_accum = nullptr;
+    uint32_t* d_out = nullptr;
+    unsigned long long* d_counter = nullptr;
+    float4* d_sph_hot = nullptr;
+    uint32_t* d_sph_mat = nullptr;
+    RtMaterial* d_mat = nullptr;
+    RtObject* d_obj = nullptr;
+    RtSubObject* d_sub = nullptr;
+    RtTriangleHot* d_tri = nullptr;
+    uint32_t* d_tex = nullptr;
+    uint32_t tex_w = 0, tex_h = 0, tex_layers = 0;
+    uint32_t* d_env = nullptr;
+    uint32_t env_w = 0, env_h = 0;
+    float* d_srgb = nullptr;
+
+    // host-side copies used for validation of index ranges
+    std::vector<rt_object_info> h_obj;
+    std::vector<rt_sub_object_info> h_sub;
+
+    // pinned staging (one buffer, reused after its last copy completes)
+    void* pinned = nullptr;
+    size_t pinned_cap = 0;
+    hipEvent_t staging_done = nullptr;
+    bool staging_busy = false;
+
+    // timing
+    bool timing = false;
+    std::vector<EventPair> pending;
+    std::vector<EventPair> pool;
+    double total_ms = 0.0;
+    uint64_t n_timed = 0;
+    float last_ms = 0.0f;
+
+    std::string err;
+};
+
+namespace {
+
+int fail(rt_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg; else g_create_error = msg;
+    return code;
+}
+
+int hip_fail(rt_ctx* ctx, const char* what, hipError_t e) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(ctx, RT_E_HIP, m);
+}
+
+#define RT_HIP(ctx, call)                                \
+    do {                                                 \
+        hipError_t e_ = (call);                          \
+        if (e_ != hipSuccess) return hip_fail(ctx, #call, e_); \
+    } while (0)
+
+void srgb_table(float out[256]) {
+    // IEC 61966-2-1 decode of an 8-bit Rgba8UnormSrgb channel, rounded to f32.
+    for (int i = 0; i < 256; i++) {
+        const double c = (double)i / 255.0;
+        const double l = c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4);
+        out[i] = (float)l;
+    }
+}
+
+uint32_t owned_tile_count(uint32_t n_tiles, uint32_t rank, uint32_t world) {
+    if (rank >= n_tiles) return 0;
+    return (n_tiles - rank + world - 1) / world;
+}
+
+// Returns a pinned host region of at least `bytes`, waiting for any copy
+// still reading the previous contents.
+int staging(rt_ctx* ctx, size_t bytes, void** out) {
+    if (ctx->staging_busy) {
+        RT_HIP(ctx, hipEventSynchronize(ctx->staging_done));
+        ctx->staging_busy = false;
+    }
+    if (bytes > ctx->pinned_cap) {
+        if (ctx->pinned) RT_HIP(ctx, hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_cap = 0;
+        size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+        RT_HIP(ctx, hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault));
+        ctx->pinned_cap = cap;
+    }
+    *out = ctx->pinned;
+    return RT_OK;
+}
+
+int staged_copy(rt_ctx* ctx, void* dst, size_t bytes) {
+    if (bytes == 0) return RT_OK;
+    RT_HIP(ctx, hipMemcpyAsync(dst, ctx->pinned, bytes, hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(ctx, hipEventRecord(ctx->staging_done, ctx->stream));
+    ctx->staging_busy = true;
+    return RT_OK;
+}
+
+int upload_raw(rt_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return RT_OK;
+    void* p;
+    int rc = staging(ctx, bytes, &p);
+    if (rc) return rc;
+    std::memcpy(p, src, bytes);
+    return staged_copy(ctx, dst, bytes);
+}
+
+int upload_spheres(rt_ctx* ctx, const rt_scene_sphere* s, uint32_t n) {
+    if (n == 0) return RT_OK;
+    void* p;
+    int rc = staging(ctx, (size_t)n * 20, &p);
+    if (rc) return rc;
+    float4* hot = static_cast<float4*>(p);
+    uint32_t* mat = reinterpret_cast<uint32_t*>(hot + n);
+    for (uint32_t i = 0; i < n; i++) {
+        // radius^2 is the same single f32 product the shader forms (:375)
+        hot[i] = make_float4(s[i].position[0], s[i].position[1], s[i].position[2], s[i].radius * s[i].radius);
+        mat[i] = s[i].material_index;
+    }
+    RT_HIP(ctx, hipMemcpyAsync(ctx->d_sph_hot, hot, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(ctx, hipMemcpyAsync(ctx->d_sph_mat, mat, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(ctx, hipEventRecord(ctx->staging_done, ctx->stream));
+    ctx->staging_busy = true;
+    return RT_OK;
+}
+
+int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
+    if (n == 0) return RT_OK;
+    void* p;
+    int rc = staging(ctx, (size_t)n * sizeof(RtTriangleHot), &p);
+    if (rc) return rc;
+    RtTriangleHot* hot = static_cast<RtTriangleHot*>(p);
+    for (uint32_t i = 0; i < n; i++) {
+        const rt_scene_triangle& s = t[i];
+        hot[i].a = make_float4(s.a[0], s.a[1], s.a[2], 0.f);
+        hot[i].edge_ab = make_float4(s.edge_ab[0], s.edge_ab[1], s.edge_ab[2], 0.f);
+        hot[i].edge_ac = make_float4(s.edge_ac[0], s.edge_ac[1], s.edge_ac[2], 0.f);
+        hot[i].calc_normal = make_float4(s.calc_normal[0], s.calc_normal[1], s.calc_normal[2], 0.f);
+        hot[i].face_normal = make_float4(s.face_normal[0], s.face_normal[1], s.face_normal[2], 0.f);
+    }
+    return staged_copy(ctx, ctx->d_tri, (size_t)n * sizeof(RtTriangleHot));
+}
+
+// Index ranges the kernel walks must lie inside the buffers (the reference's
+// fixed-size WGSL arrays would clamp; here they are rejected up front).
+int validate_ranges(rt_ctx* ctx) {
+    for (size_t i = 0; i < ctx->h_obj.size(); i++) {
+        const rt_object_info& o = ctx->h_obj[i];
+        if ((uint64_t)o.first_sub_object_index + o.sub_object_count > ctx->cap_sub)
+            return fail(ctx, RT_E_INVALID, "object " + std::to_string(i) + " sub-object range exceeds sub_object_count");
+    }
+    for (size_t i = 0; i < ctx->h_sub.size(); i++) {
+        const rt_sub_object_info& s = ctx->h_sub[i];
+        if (s.triangle_count != 0 && (uint64_t)s.first_triangle_index + s.triangle_count > ctx->cap_tri)
+            return fail(ctx, RT_E_INVALID, "sub-object " + std::to_string(i) + " triangle range exceeds triangle_count");
+    }
+    return RT_OK;
+}
+
+int check_params(rt_ctx* ctx, const rt_params* p) {
+    if (!p) return fail(ctx, RT_E_INVALID, "params is NULL");
+    if (p->screen_width != ctx->width)
+        return fail(ctx, RT_E_INVALID, "params.screen_width must equal the framebuffer width");
+    if (p->sphere_count > ctx->cap_sph) return fail(ctx, RT_E_INVALID, "params.sphere_count exceeds sphere buffer");
+    if (p->object_count > ctx->cap_obj) return fail(ctx, RT_E_INVALID, "params.object_count exceeds object buffer");
+    return RT_OK;
+}
+
+template <typename T>
+int dev_alloc(rt_ctx* ctx, T** p, size_t count) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 16;  // keep every binding a valid pointer
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), bytes);
+    if (e != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    e = hipMemsetAsync(*p, 0, bytes, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "hipMemsetAsync", e);
+    return RT_OK;
+}
+
+int collect_timing(rt_ctx* ctx) {
+    for (EventPair& ev : ctx->pending) {
+        RT_HIP(ctx, hipEventSynchronize(ev.stop));
+        float ms = 0.f;
+        RT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
+        ctx->total_ms += ms;
+        ctx->n_timed += 1;
+        ctx->last_ms = ms;
+        ctx->pool.push_back(ev);
+    }
+    ctx->pending.clear();
+    return RT_OK;
+}
+
+int reap_finished_timing(rt_ctx* ctx) {
+    // non-blocking: harvest only pairs whose stop event has completed
+    size_t keep = 0;
+    for (size_t i = 0; i < ctx->pending.size(); i++) {
+        EventPair ev = ctx->pending[i];
+        if (hipEventQuery(ev.stop) == hipSuccess) {
+            float ms = 0.f;
+            RT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
+            ctx->total_ms += ms;
+            ctx->n_timed += 1;
+            ctx->last_ms = ms;
+            ctx->pool.push_back(ev);
+        } else {
+            ctx->pending[keep++] = ev;
+        }
+    }
+    ctx->pending.resize(keep);
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int rt_srgb_table(float out[256]) {
+    if (!out) return RT_E_INVALID;
+    srgb_table(out);
+    return RT_OK;
+}
+
+int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
+    g_create_error.clear();
+    if (!info || !out_ctx) return fail(nullptr, RT_E_INVALID, "rt_create: NULL argument");
+    *out_ctx = nullptr;
+    if (info->width == 0 || info->height == 0) return fail(nullptr, RT_E_INVALID, "width and height must be > 0");
+    if (info->world_size == 0 || info->rank >= info->world_size)
+        return fail(nullptr, RT_E_INVALID, "rank must be < world_size (world_size >= 1)");
+    const uint64_t n_pixels = (uint64_t)info->width * info->height;
+    if (n_pixels > 0xffffffffull) return fail(nullptr, RT_E_INVALID, "pixel index must fit in u32 (:148)");
+    if (!info->camera_rays) return fail(nullptr, RT_E_INVALID, "camera_rays is NULL");
+    if ((info->material_count && !info->materials) || (info->sphere_count && !info->spheres) ||
+        (info->triangle_count && !info->triangles) || (info->object_count && !info->objects) ||
+        (info->sub_object_count && !info->sub_objects))
+        return fail(nullptr, RT_E_INVALID, "NULL scene array with a non-zero count");
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev == 0)
+        return fail(nullptr, RT_E_NODEVICE, "no HIP device available");
+    if (info->device < 0 || info->device >= n_dev) return fail(nullptr, RT_E_NODEVICE, "device ordinal out of range");
+
+    rt_ctx* ctx = new (std::nothrow) rt_ctx();
+    if (!ctx) return fail(nullptr, RT_E_NOMEM, "out of host memory");
+    auto bail = [&](int rc) {
+        g_create_error = ctx->err;
+        rt_destroy(ctx);
+        return rc;
+    };
+    ctx->device = info->device;
+    ctx->width = info->width;
+    ctx->height = info->height;
+    ctx->n_pixels = n_pixels;
+    ctx->rank = info->rank;
+    ctx->world = info->world_size;
+    ctx->tiles_x = (info->width + 7) / 8;
+    ctx->tiles_y = (info->height + 7) / 8;
+    ctx->owned_tiles = owned_tile_count(ctx->tiles_x * ctx->tiles_y, ctx->rank, ctx->world);
+    ctx->camera = info->camera;
+    ctx->cap_mat = info->material_count;
+    ctx->cap_sph = info->sphere_count;
+    ctx->cap_tri = info->triangle_count;
+    ctx->cap_obj = info->object_count;
+    ctx->cap_sub = info->sub_object_count;
+    ctx->n_mat_dev = info->material_count ? info->material_count : 1;
+    ctx->n_tri_dev = info->triangle_count ? info->triangle_count : 1;
+    ctx->n_sub_dev = info->sub_object_count ? info->sub_object_count : 1;
+    ctx->h_obj.assign(info->objects, info->objects + info->object_count);
+    ctx->h_sub.assign(info->sub_objects, info->sub_objects + info->sub_object_count);
+
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return bail(hip_fail(ctx, "hipSetDevice", e));
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
+    e = hipEventCreateWithFlags(&ctx->staging_done, hipEventDisableTiming);
+    if (e != hipSuccess) return bail(hip_fail(ctx, "hipEventCreate", e));
+
+    int rc;
+    if ((rc = check_params(ctx, &info->params))) return bail(rc);
+    if ((rc = validate_ranges(ctx))) return bail(rc);
+    ctx->params = info->params;
+    ctx->k = 1;  // src/renderer.rs:96
+
+    if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
+        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_sph_hot, info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
+        (rc = dev_alloc(ctx, &ctx->d_srgb, 256)) || (rc = dev_alloc(ctx, &ctx->d_tex, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_env, 1)))
+        return bail(rc);
+    ctx->tex_w = ctx->tex_h = ctx->tex_layers = 1;  // a black 1x1 placeholder until textures arrive
+    ctx->env_w = ctx->env_h = 1;
+
+    if ((rc = upload_raw(ctx, ctx->d_rays, info->camera_rays, n_pixels * 16)) ||
+        (rc = upload_raw(ctx, ctx->d_mat, info->materials, (size_t)info->material_count * 32)) ||
+        (rc = upload_spheres(ctx, info->spheres, info->sphere_count)) ||
+        (rc = upload_triangles(ctx, info->triangles, info->triangle_count)) ||
+        (rc = upload_raw(ctx, ctx->d_obj, info->objects, (size_t)info->object_count * 48)) ||
+        (rc = upload_raw(ctx, ctx->d_sub, info->sub_objects, (size_t)info->sub_object_count * 32)))
+        return bail(rc);
+    float lut[256];
+    srgb_table(lut);
+    if ((rc = upload_raw(ctx, ctx->d_srgb, lut, sizeof(lut)))) return bail(rc);
+    e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamSynchronize", e));
+    ctx->staging_busy = false;
+    *out_ctx = ctx;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_sph_hot, ctx->d_sph_mat,
+                    ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
+                    ctx->d_srgb};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (EventPair& ev : ctx->pending) {
+        (void)hipEventDestroy(ev.start);
+        (void)hipEventDestroy(ev.stop);
+    }
+    for (EventPair& ev : ctx->pool) {
+        (void)hipEventDestroy(ev.start);
+        (void)hipEventDestroy(ev.stop);
+    }
+    if (ctx->staging_done) (void)hipEventDestroy(ctx->staging_done);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+#define RT_ENTER(ctx)                                               \
+    do {                                                            \
+        if (!(ctx)) return RT_E_INVALID;                            \
+        (ctx)->err.clear();                                         \
+        hipError_t e0_ = hipSetDevice((ctx)->device);               \
+        if (e0_ != hipSuccess) return hip_fail(ctx, "hipSetDevice", e0_); \
+    } while (0)
+
+int rt_upload_textures(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height, uint32_t layers) {
+    RT_ENTER(ctx);
+    if (!rgba8 || width == 0 || height == 0 || layers == 0)
+        return fail(ctx, RT_E_INVALID, "textures: need non-empty RGBA8 data");
+    const size_t texels = (size_t)width * height * layers;
+    if (texels != (size_t)ctx->tex_w * ctx->tex_h * ctx->tex_layers || !ctx->d_tex) {
+        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->d_tex) RT_HIP(ctx, hipFree(ctx->d_tex));
+        ctx->d_tex = nullptr;
+        RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tex), texels * 4));
+    }
+    ctx->tex_w = width;
+    ctx->tex_h = height;
+    ctx->tex_layers = layers;
+    return upload_raw(ctx, ctx->d_tex, rgba8, texels * 4);
+}
+
+int rt_upload_env_map(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height) {
+    RT_ENTER(ctx);
+    if (!rgba8 || width == 0 || height == 0) return fail(ctx, RT_E_INVALID, "env map: need non-empty RGBA8 data");
+    const size_t texels = (size_t)width * height;
+    if (texels != (size_t)ctx->env_w * ctx->env_h || !ctx->d_env) {
+        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->d_env) RT_HIP(ctx, hipFree(ctx->d_env));
+        ctx->d_env = nullptr;
+        RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_env), texels * 4));
+    }
+    ctx->env_w = width;
+    ctx->env_h = height;
+    return upload_raw(ctx, ctx->d_env, rgba8, texels * 4);
+}
+
+int rt_update_params(rt_ctx* ctx, const rt_params* params) {
+    RT_ENTER(ctx);
+    int rc = check_params(ctx, params);
+    if (rc) return rc;
+    ctx->params = *params;
+    return RT_OK;
+}
+
+int rt_reset_accumulation(rt_ctx* ctx, const rt_params* params) {
+    RT_ENTER(ctx);
+    int rc = check_params(ctx, params);
+    if (rc) return rc;
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_accum, 0, ctx->n_pixels * 16, ctx->stream));
+    ctx->params = *params;
+    ctx->k = params->accumulation_index;
+    return RT_OK;
+}
+
+int rt_update_ray_directions(rt_ctx* ctx, const rt_ray* rays, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !rays) return fail(ctx, RT_E_INVALID, "rays is NULL");
+    if (count > ctx->n_pixels) return fail(ctx, RT_E_CAPACITY, "more rays than pixels");
+    return upload_raw(ctx, ctx->d_rays, rays, (size_t)count * 16);
+}
+
+int rt_update_camera(rt_ctx* ctx, const rt_ray_camera* camera) {
+    RT_ENTER(ctx);
+    if (!camera) return fail(ctx, RT_E_INVALID, "camera is NULL");
+    ctx->camera = *camera;  // passed by value to the next launch
+    return RT_OK;
+}
+
+int rt_update_spheres(rt_ctx* ctx, const rt_scene_sphere* spheres, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !spheres) return fail(ctx, RT_E_INVALID, "spheres is NULL");
+    if (count > ctx->cap_sph) return fail(ctx, RT_E_CAPACITY, "more spheres than the buffer holds");
+    return upload_spheres(ctx, spheres, count);
+}
+
+int rt_update_triangles(rt_ctx* ctx, const rt_scene_triangle* triangles, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !triangles) return fail(ctx, RT_E_INVALID, "triangles is NULL");
+    if (count > ctx->cap_tri) return fail(ctx, RT_E_CAPACITY, "more triangles than the buffer holds");
+    return upload_triangles(ctx, triangles, count);
+}
+
+int rt_update_object_info(rt_ctx* ctx, const rt_object_info* objects, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !objects) return fail(ctx, RT_E_INVALID, "objects is NULL");
+    if (count > ctx->cap_obj) return fail(ctx, RT_E_CAPACITY, "more objects than the buffer holds");
+    std::vector<rt_object_info> saved = ctx->h_obj;
+    std::copy(objects, objects + count, ctx->h_obj.begin());
+    int rc = validate_ranges(ctx);
+    if (rc) {
+        ctx->h_obj.swap(saved);
+        return rc;
+    }
+    return upload_raw(ctx, ctx->d_obj, objects, (size_t)count * 48);
+}
+
+int rt_update_sub_object_info(rt_ctx* ctx, const rt_sub_object_info* sub_objects, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !sub_objects) return fail(ctx, RT_E_INVALID, "sub_objects is NULL");
+    if (count > ctx->cap_sub) return fail(ctx, RT_E_CAPACITY, "more sub-objects than the buffer holds");
+    std::vector<rt_sub_object_info> saved = ctx->h_sub;
+    std::copy(sub_objects, sub_objects + count, ctx->h_sub.begin());
+    int rc = validate_ranges(ctx);
+    if (rc) {
+        ctx->h_sub.swap(saved);
+        return rc;
+    }
+    return upload_raw(ctx, ctx->d_sub, sub_objects, (size_t)count * 32);
+}
+
+int rt_update_materials(rt_ctx* ctx, const rt_scene_material* materials, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !materials) return fail(ctx, RT_E_INVALID, "materials is NULL");
+    if (count > ctx->cap_mat) return fail(ctx, RT_E_CAPACITY, "more materials than the buffer holds");
+    return upload_raw(ctx, ctx->d_mat, materials, (size_t)count * 32);
+}
+
+int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
+    RT_ENTER(ctx);
+    const rt_params& p = ctx->params;
+    KernelArgs ka{};
+    ka.camera_rays = ctx->d_rays;
+    ka.accum = ctx->d_accum;
+    ka.output = ctx->d_out;
+    ka.ray_counter = ctx->d_counter;
+    ka.sphere_hot = ctx->d_sph_hot;
+    ka.sphere_material = ctx->d_sph_mat;
+    ka.materials = ctx->d_mat;
+    ka.objects = ctx->d_obj;
+    ka.sub_objects = ctx->d_sub;
+    ka.triangles = ctx->d_tri;
+    ka.textures = ctx->d_tex;
+    ka.env = ctx->d_env;
+    ka.srgb = ctx->d_srgb;
+    ka.camera_origin[0] = ctx->camera.origin[0];
+    ka.camera_origin[1] = ctx->camera.origin[1];
+    ka.camera_origin[2] = ctx->camera.origin[2];
+    ka.width = ctx->width;
+    ka.accumulation_index = p.accumulation_index;
+    ka.accumulate = p.accumulate;
+    ka.sphere_count = p.sphere_count;
+    ka.object_count = p.object_count;
+    ka.compute_per_frame = p.compute_per_frame;
+    ka.texture_width = p.texture_width;
+    ka.texture_height = p.texture_height;
+    ka.env_map_width = p.env_map_width;
+    ka.env_map_height = p.env_map_height;
+    ka.material_count = ctx->n_mat_dev;
+    ka.sub_object_count = ctx->n_sub_dev;
+    ka.triangle_count = ctx->n_tri_dev;
+    ka.tex_w = ctx->tex_w;
+    ka.tex_h = ctx->tex_h;
+    ka.tex_layers = ctx->tex_layers;
+    ka.env_w = ctx->env_w;
+    ka.env_h = ctx->env_h;
+    ka.height = ctx->height;
+    ka.bounces = bounces;
+    ka.tiles_x = ctx->tiles_x;
+    ka.owned_tiles = ctx->owned_tiles;
+    ka.rank = ctx->rank;
+    ka.world_size = ctx->world;
+
+    // dynamic LDS carve-up: spheres | materials | objects | sphere materials | srgb
+    auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+    size_t off = al16((size_t)p.sphere_count * 16);
+    ka.lds_mat_offset = (uint32_t)off;
+    off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
+    ka.lds_obj_offset = (uint32_t)off;
+    off = al16(off + (size_t)p.object_count * sizeof(RtObject));
+    ka.lds_smat_offset = (uint32_t)off;
+    off = al16(off + (size_t)p.sphere_count * 4);
+    const bool scene_in_lds = off + 1024 <= kLdsSceneBudget;
+    size_t lds_bytes;
+    if (scene_in_lds) {
+        ka.lds_srgb_offset = (uint32_t)off;
+        lds_bytes = off + 1024;
+    } else {
+        ka.lds_srgb_offset = 0;
+        lds_bytes = 1024;
+    }
+    const uint32_t blocks = (ctx->owned_tiles + kTilesPerBlock - 1) / kTilesPerBlock;
+    if (blocks == 0 || bounces == 0) return RT_OK;
+
+    EventPair ev;
+    if (ctx->timing) {
+        int rc = reap_finished_timing(ctx);
+        if (rc) return rc;
+        if (!ctx->pool.empty()) {
+            ev = ctx->pool.back();
+            ctx->pool.pop_back();
+        } else {
+            RT_HIP(ctx, hipEventCreate(&ev.start));
+            RT_HIP(ctx, hipEventCreate(&ev.stop));
+        }
+        RT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
+    }
+    hipError_t e = rt_launch_pathtrace(ka, scene_in_lds, lds_bytes, blocks, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
+    if (ctx->timing) {
+        RT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
+        ctx->pending.push_back(ev);
+    }
+    return RT_OK;
+}
+
+int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) {
+    RT_ENTER(ctx);
+    if (ctx->params.accumulate) {  // src/renderer.rs:216-235 (`accumulate` is a bool there)
+        ctx->params.accumulation_index = ctx->k;
+        ctx->k += 1;
+    }
+    return rt_dispatch(ctx, bounces);
+}
+
+int rt_synchronize(rt_ctx* ctx) {
+    RT_ENTER(ctx);
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_read_output(rt_ctx* ctx, uint32_t* out) {
+    RT_ENTER(ctx);
+    if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_out, ctx->n_pixels * 4, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_read_accumulation(rt_ctx* ctx, float* out) {
+    RT_ENTER(ctx);
+    if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_accum, ctx->n_pixels * 16, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_ray_count(rt_ctx* ctx, uint64_t* out) {
+    RT_ENTER(ctx);
+    if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    unsigned long long v = 0;
+    RT_HIP(ctx, hipMemcpyAsync(&v, ctx->d_counter, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *out = v;
+    return RT_OK;
+}
+
+int rt_reset_ray_count(rt_ctx* ctx) {
+    RT_ENTER(ctx);
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, sizeof(unsigned long long), ctx->stream));
+    return RT_OK;
+}
+
+int rt_accumulation_index(const rt_ctx* ctx, uint32_t* out) {
+    if (!ctx || !out) return RT_E_INVALID;
+    *out = ctx->k;
+    return RT_OK;
+}
+
+int rt_set_timing(rt_ctx* ctx, int enable) {
+    RT_ENTER(ctx);
+    ctx->timing = enable != 0;
+    return RT_OK;
+}
+
+int rt_last_dispatch_ms(rt_ctx* ctx, float* out_ms) {
+    RT_ENTER(ctx);
+    if (!out_ms) return fail(ctx, RT_E_INVALID, "out is NULL");
+    int rc = collect_timing(ctx);
+    if (rc) return rc;
+    *out_ms = ctx->last_ms;
+    return RT_OK;
+}
+
+int rt_dispatch_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed) {
+    RT_ENTER(ctx);
+    if (!total_ms || !n_timed) return fail(ctx, RT_E_INVALID, "out is NULL");
+    int rc = collect_timing(ctx);
+    if (rc) return rc;
+    *total_ms = ctx->total_ms;
+    *n_timed = ctx->n_timed;
+    return RT_OK;
+}
+
+int rt_reset_timing(rt_ctx* ctx) {
+    RT_ENTER(ctx);
+    int rc = collect_timing(ctx);
+    if (rc) return rc;
+    ctx->total_ms = 0.0;
+    ctx->n_timed = 0;
+    ctx->last_ms = 0.0f;
+    return RT_OK;
+}
+
+int rt_owned_pixel_count(const rt_ctx* ctx, uint32_t rank, uint32_t world_size, uint64_t* out) {
+    if (!ctx || !out || world_size == 0 || rank >= world_size) return RT_E_INVALID;
+    *out = (uint64_t)owned_tile_count(ctx->tiles_x * ctx->tiles_y, rank, world_size) * 64u;
+    return RT_OK;
+}
+
+int rt_pack_owned_accumulation(rt_ctx* ctx, void* dst_device) {
+    RT_ENTER(ctx);
+    if (!dst_device) return fail(ctx, RT_E_INVALID, "dst is NULL");
+    if (ctx->owned_tiles == 0) return RT_OK;
+    hipError_t e = rt_launch_pack(ctx->d_accum, static_cast<float4*>(dst_device), ctx->width, ctx->height,
+                                  ctx->tiles_x, ctx->owned_tiles, ctx->rank, ctx->world, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_pack_tiles_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size,
+                           uint32_t divisor) {
+    RT_ENTER(ctx);
+    if (!src_device || world_size == 0 || src_rank >= world_size || divisor == 0)
+        return fail(ctx, RT_E_INVALID, "unpack: bad arguments");
+    const uint32_t owned = owned_tile_count(ctx->tiles_x * ctx->tiles_y, src_rank, world_size);
+    if (owned == 0) return RT_OK;
+    hipError_t e = rt_launch_unpack(static_cast<const float4*>(src_device), ctx->d_accum, ctx->d_out, ctx->width,
+                                    ctx->height, ctx->tiles_x, owned, src_rank, world_size, (float)divisor,
+                                    ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_unpack_tiles_kernel launch", e);
+    return RT_OK;
+}
+
+void* rt_stream(rt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+}  // extern "C"

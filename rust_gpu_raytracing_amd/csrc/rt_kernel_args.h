@@ -1,0 +1,109 @@
+// rt_kernel_args.h — device-side scene records and the kernel argument block.
+//
+// The records are the reference's GPU layouts (src/buffers.rs:7-129,
+// compute_shader.wgsl:43-126) except the triangle, which is repacked on upload
+// to the 80 bytes the kernel reads (the reference's 112-byte SceneTriangle
+// carries per-triangle bounds the shader never touches).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+constexpr uint32_t kBlockThreads = 256;            // 4 waves
+constexpr uint32_t kTilesPerBlock = kBlockThreads / 64;  // one 8x8 tile per wave
+
+struct RtSphere {  // src/buffers.rs:40-45, 32 B
+    float position[3];
+    float radius;
+    uint32_t material_index;
+    uint32_t _pad[3];
+};
+
+struct RtMaterial {  // src/buffers.rs:100-109, 32 B
+    uint32_t texture_index;
+    float roughness;
+    float emission_power;
+    float specular;
+    float specular_scatter;
+    float glass;
+    float refraction_index;
+    uint32_t _pad;
+};
+
+struct RtObject {  // src/buffers.rs:113-120, 48 B
+    float min_bounds[3];
+    uint32_t first_sub_object_index;
+    float max_bounds[3];
+    uint32_t sub_object_count;
+    uint32_t material_index;
+    uint32_t _pad[3];
+};
+
+struct RtSubObject {  // src/buffers.rs:124-129, 32 B
+    float min_bounds[3];
+    uint32_t first_triangle_index;
+    float max_bounds[3];
+    uint32_t triangle_count;
+};
+
+struct RtTriangleHot {  // the 80 B of SceneTriangle (src/buffers.rs:49-64) the kernel reads
+    float4 a;
+    float4 edge_ab;
+    float4 edge_ac;
+    float4 calc_normal;
+    float4 face_normal;
+};
+
+static_assert(sizeof(RtSphere) == 32, "SceneSphere layout");
+static_assert(sizeof(RtMaterial) == 32, "SceneMaterial layout");
+static_assert(sizeof(RtObject) == 48, "ObjectInfo layout");
+static_assert(sizeof(RtSubObject) == 32, "SubObjectInfo layout");
+static_assert(sizeof(RtTriangleHot) == 80, "hot triangle layout");
+
+struct KernelArgs {
+    // framebuffer (bindings 1, 2, 6)
+    const float4* __restrict__ camera_rays;
+    float4* __restrict__ accum;
+    uint32_t* __restrict__ output;
+    unsigned long long* __restrict__ ray_counter;
+    // scene (bindings 3, 4, 5, 7, 8, 10)
+    const float4* __restrict__ sphere_hot;        // centre.xyz, radius*radius (f32, computed at upload)
+    const uint32_t* __restrict__ sphere_material;
+    const RtMaterial* __restrict__ materials;
+    const RtObject* __restrict__ objects;
+    const RtSubObject* __restrict__ sub_objects;
+    const RtTriangleHot* __restrict__ triangles;
+    // textures (bindings 9, 11), RGBA8 sRGB, + decode table
+    const uint32_t* __restrict__ textures;
+    const uint32_t* __restrict__ env;
+    const float* __restrict__ srgb;
+    float camera_origin[3];
+    // Params (binding 0), passed by value at launch
+    uint32_t width;
+    uint32_t accumulation_index;
+    uint32_t accumulate;
+    uint32_t sphere_count;
+    uint32_t object_count;
+    uint32_t compute_per_frame;
+    uint32_t texture_width;
+    uint32_t texture_height;
+    uint32_t env_map_width;
+    uint32_t env_map_height;
+    // extents of what is actually allocated (Restrict-policy clamps)
+    uint32_t material_count;
+    uint32_t sub_object_count;
+    uint32_t triangle_count;
+    uint32_t tex_w, tex_h, tex_layers;
+    uint32_t env_w, env_h;
+    // launch geometry
+    uint32_t height;
+    uint32_t bounces;
+    uint32_t tiles_x;
+    uint32_t owned_tiles;
+    uint32_t rank;
+    uint32_t world_size;
+    // dynamic LDS carve-up (byte offsets)
+    uint32_t lds_mat_offset;
+    uint32_t lds_obj_offset;
+    uint32_t lds_smat_offset;
+    uint32_t lds_srgb_offset;
+};

@@ -1,0 +1,202 @@
+"""``Renderer`` — the host side of the hot path, over the C ABI.
+
+Mirrors ``Renderer`` in src/renderer.rs:28-320 (names, argument meaning and
+call order), with wgpu replaced by ``include/rt_abi.h``:
+
+===========================================  ==========================================
+reference (src/renderer.rs)                  here
+===========================================  ==========================================
+``Renderer::new`` :42-101                    ``Renderer(scene, ...)`` -> ``rt_create`` +
+                                             ``rt_upload_textures`` + ``rt_upload_env_map``
+``reset_accumulation`` :131-151              ``reset_accumulation()`` -> ``rt_reset_accumulation``
+``update_scene`` :153-199                    ``update_scene()`` -> ``rt_update_*``
+``compute_frame`` :201-252                   ``compute_frame(bounces)`` -> ``rt_compute_frame``
+``on_update`` (camera moved) :109-129        ``update_camera(camera)``
+(no readback in the reference)               ``read_output`` / ``read_accumulation``
+===========================================  ==========================================
+
+Errors raise :class:`RtError` (the reference panics via ``.expect``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from . import buffers as B
+from .scene import RenderScene
+
+REFERENCE_BOUNCES = 10  # compute_shader.wgsl:150
+
+
+class Renderer:
+    def __init__(
+        self,
+        scene: RenderScene,
+        *,
+        accumulate: bool = True,
+        compute_per_frame: int = 1,
+        device: int = 0,
+        rank: int = 0,
+        world_size: int = 1,
+        camera_rays: np.ndarray | None = None,
+    ):
+        self._lib = N.load_library()
+        self.scene = scene
+        self.accumulate = accumulate
+        self.compute_per_frame = compute_per_frame
+        self.width = scene.camera.viewport_width
+        self.height = scene.camera.viewport_height
+        self.rank, self.world_size = rank, world_size
+        self._ctx = None
+        rays = scene.camera.recalculate_ray_directions() if camera_rays is None else camera_rays
+        self.camera_rays = np.ascontiguousarray(rays, dtype=B.RAY)
+        objs, subs, tris = scene.flatten()
+        self._keep = [self.camera_rays, scene.materials, scene.spheres, tris, objs, subs]
+
+        info = N.rt_create_info()
+        info.width, info.height, info.device = self.width, self.height, device
+        info.camera.origin[:] = [float(x) for x in scene.camera.position]
+        info.camera_rays = N.ptr(self.camera_rays)
+        info.materials, info.material_count = N.ptr(scene.materials), scene.materials.shape[0]
+        info.spheres, info.sphere_count = N.ptr(scene.spheres), scene.spheres.shape[0]
+        info.triangles, info.triangle_count = N.ptr(tris), tris.shape[0]
+        info.objects, info.object_count = N.ptr(objs), objs.shape[0]
+        info.sub_objects, info.sub_object_count = N.ptr(subs), subs.shape[0]
+        info.params = N.params_struct(self._params(accumulation_index=1))
+        info.rank, info.world_size = rank, world_size
+        ctx = ctypes.c_void_p()
+        N.check(None, self._lib.rt_create(ctypes.byref(info), ctypes.byref(ctx)))
+        self._ctx = ctx
+        self._upload_textures()
+
+    # ------------------------------------------------------------------ helpers
+    def _params(self, accumulation_index: int) -> np.ndarray:
+        return self.scene.params(
+            accumulate=int(self.accumulate),
+            compute_per_frame=self.compute_per_frame,
+            accumulation_index=accumulation_index,
+        )
+
+    def _call(self, name, *args):
+        if self._ctx is None:
+            raise N.RtError(N.RT_E_INVALID, "renderer is closed")
+        N.check(self._ctx, getattr(self._lib, name)(self._ctx, *args))
+
+    def _upload_textures(self):
+        tex = np.ascontiguousarray(self.scene.textures, np.uint8)
+        layers, th, tw, _ = tex.shape
+        self._call("rt_upload_textures", N.ptr(tex), tw, th, layers)
+        env = np.ascontiguousarray(self.scene.environment_map, np.uint8)
+        eh, ew, _ = env.shape
+        self._call("rt_upload_env_map", N.ptr(env), ew, eh)
+
+    # ------------------------------------------------------------------ reference surface
+    def reset_accumulation(self) -> None:
+        """src/renderer.rs:131-151."""
+        p = N.params_struct(self._params(accumulation_index=1))
+        self._call("rt_reset_accumulation", ctypes.byref(p))
+
+    def update_scene(self) -> None:
+        """src/renderer.rs:153-199: reset, then re-upload spheres, textures, env map,
+        triangles, objects, sub-objects and materials."""
+        self.reset_accumulation()
+        s = self.scene
+        self._call("rt_update_spheres", N.ptr(s.spheres), s.spheres.shape[0])
+        self._upload_textures()
+        objs, subs, tris = s.flatten()
+        self._keep[3:6] = [tris, objs, subs]
+        self._call("rt_update_triangles", N.ptr(tris), tris.shape[0])
+        self._call("rt_update_object_info", N.ptr(objs), objs.shape[0])
+        self._call("rt_update_sub_object_info", N.ptr(subs), subs.shape[0])
+        self._call("rt_update_materials", N.ptr(s.materials), s.materials.shape[0])
+
+    def update_camera(self, camera) -> None:
+        """src/renderer.rs:109-129 after a move: reset, new origin, new ray directions."""
+        self.scene.camera = camera
+        self.reset_accumulation()
+        rc = N.rt_ray_camera()
+        rc.origin[:] = [float(x) for x in camera.position]
+        self._call("rt_update_camera", ctypes.byref(rc))
+        self.camera_rays = np.ascontiguousarray(camera.recalculate_ray_directions())
+        self._keep[0] = self.camera_rays
+        self._call("rt_update_ray_directions", N.ptr(self.camera_rays), self.camera_rays.shape[0])
+
+    def compute_frame(self, bounces: int = REFERENCE_BOUNCES) -> None:
+        """src/renderer.rs:201-252 (asynchronous)."""
+        self._call("rt_compute_frame", bounces)
+
+    # ------------------------------------------------------------------ readback & stats
+    def synchronize(self) -> None:
+        self._call("rt_synchronize")
+
+    def read_output(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width), np.uint32)
+        self._call("rt_read_output", N.ptr(out))
+        return out
+
+    def read_accumulation(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.float32)
+        self._call("rt_read_accumulation", N.ptr(out))
+        return out
+
+    def ray_count(self) -> int:
+        v = ctypes.c_uint64()
+        self._call("rt_ray_count", ctypes.byref(v))
+        return v.value
+
+    def reset_ray_count(self) -> None:
+        self._call("rt_reset_ray_count")
+
+    @property
+    def accumulation_index(self) -> int:
+        v = ctypes.c_uint32()
+        self._call("rt_accumulation_index", ctypes.byref(v))
+        return v.value
+
+    def set_timing(self, enable: bool) -> None:
+        self._call("rt_set_timing", int(enable))
+
+    def dispatch_time_total(self):
+        """(total milliseconds of timed launches, number timed) — HIP events on the ctx stream."""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        self._call("rt_dispatch_time_total", ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
+    def reset_timing(self) -> None:
+        self._call("rt_reset_timing")
+
+    def owned_pixel_count(self, rank: int | None = None, world_size: int | None = None) -> int:
+        v = ctypes.c_uint64()
+        r = self.rank if rank is None else rank
+        w = self.world_size if world_size is None else world_size
+        N.check(self._ctx, self._lib.rt_owned_pixel_count(self._ctx, r, w, ctypes.byref(v)))
+        return v.value
+
+    def pack_owned_accumulation(self, dst_device_ptr: int) -> None:
+        self._call("rt_pack_owned_accumulation", ctypes.c_void_p(dst_device_ptr))
+
+    def unpack_accumulation(self, src_device_ptr: int, src_rank: int, world_size: int, divisor: int) -> None:
+        self._call("rt_unpack_accumulation", ctypes.c_void_p(src_device_ptr), src_rank, world_size, divisor)
+
+    @property
+    def stream_handle(self) -> int:
+        return self._lib.rt_stream(self._ctx) or 0
+
+    def close(self) -> None:
+        if self._ctx is not None:
+            self._lib.rt_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

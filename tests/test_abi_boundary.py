@@ -1,0 +1,100 @@
+"""The C-ABI library: builds, loads, exports exactly what include/rt_abi.h declares.
+
+No kernel launches here (no GPU in the CPU suite); host-only entry points only.
+"""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from rust_gpu_raytracing_amd import _native as N
+from rust_gpu_raytracing_amd import buffers as B
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "rt_abi.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^RT_API\s+[\w\s\*]+?\b(rt_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for must in ("rt_create", "rt_destroy", "rt_compute_frame", "rt_dispatch", "rt_update_spheres",
+                 "rt_update_triangles", "rt_reset_accumulation", "rt_read_accumulation", "rt_ray_count"):
+        assert must in fns
+    assert set(fns) == set(N.SIGNATURES), set(fns) ^ set(N.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol(native_lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(N.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (rt_\w+)", out))
+    assert set(declared_functions()) <= exported
+    # internal launch helpers stay hidden (-fvisibility=hidden)
+    assert not any(s.startswith("rt_launch") for s in exported)
+    for name in declared_functions():
+        assert hasattr(native_lib, name)
+
+
+def test_abi_version(native_lib):
+    assert native_lib.rt_abi_version() == 1
+
+
+def test_ctypes_layouts_match_header():
+    assert ctypes.sizeof(N.rt_params) == B.PARAMS.itemsize == 48
+    # rt_create_info: 4 u32, camera 16 B, rays pointer, then 5 (pointer, u32 count + pad) pairs
+    assert N.rt_create_info.camera.offset == 16
+    assert N.rt_create_info.camera_rays.offset == 32
+    assert N.rt_create_info.materials.offset == 40
+    assert N.rt_create_info.sub_objects.offset == 40 + 4 * 16
+
+
+def test_create_info_layout_against_compiled_header(tmp_path):
+    # compile a tiny C program against the real header and compare offsets
+    src = tmp_path / "off.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "rt_abi.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu\\n\", sizeof(rt_create_info),"
+        " offsetof(rt_create_info, camera_rays), offsetof(rt_create_info, params),"
+        " offsetof(rt_create_info, rank), sizeof(rt_scene_triangle)); return 0;}\n"
+    )
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
+    size, rays, params, rank, tri = map(int, subprocess.run([str(exe)], capture_output=True, text=True,
+                                                             check=True).stdout.split())
+    assert size == ctypes.sizeof(N.rt_create_info)
+    assert rays == N.rt_create_info.camera_rays.offset
+    assert params == N.rt_create_info.params.offset
+    assert rank == N.rt_create_info.rank.offset
+    assert tri == 112
+
+
+def test_srgb_table_matches_oracle(native_lib, oracle_lib):
+    prod = N.srgb_table()
+    ref = np.zeros(256, np.float32)
+    oracle_lib.lib().oracle_srgb_table(ref.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    assert np.array_equal(prod.view(np.uint32), ref.view(np.uint32))
+
+
+def test_invalid_create_is_rejected_without_device(native_lib):
+    info = N.rt_create_info()  # width = height = 0
+    ctx = ctypes.c_void_p()
+    rc = native_lib.rt_create(ctypes.byref(info), ctypes.byref(ctx))
+    assert rc == N.RT_E_INVALID and not ctx.value
+    assert b"width" in native_lib.rt_last_error(None)
+
+
+def test_null_context_calls_fail_cleanly(native_lib):
+    assert native_lib.rt_compute_frame(None, 8) == N.RT_E_INVALID
+    assert native_lib.rt_synchronize(None) == N.RT_E_INVALID
+    native_lib.rt_destroy(None)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(N.NativeLibraryError):
+        N.load_library(tmp_path / "nope.so")
