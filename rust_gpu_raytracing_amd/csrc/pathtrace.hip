@@ -5,8 +5,9 @@
 // a6-a18); the numeric contract that makes it bit-exact against the CPU
 // oracle is in rt_device_math.h. What is MI355X-specific:
 //
-//  * Work unit = one 8x8 pixel tile per wave64 (the reference's workgroup,
-//    :146), four tiles per 256-thread workgroup. Tiles are dealt to ranks
+//  * Work unit = one 8x8 pixel tile (the reference's workgroup, :146),
+//    claimed by persistent wave64s from a device-wide queue; finished lanes
+//    are refilled with the tile's next pixels (ballot/mbcnt compaction). Tiles are dealt to ranks
 //    round-robin (tile t -> rank t % world) so a multi-GPU split is a launch
 //    argument, not a different kernel; seeds depend only on the global pixel
 //    index (:217), so any split is bitwise identical to one GPU.
@@ -64,25 +65,50 @@ __device__ __forceinline__ f4 decode_texel(uint32_t texel, const float* srgb) {
 }
 
 // check_spheres, compute_shader.wgsl:355-404. Returns the closest index or -1.
+// The sweep is wave-uniform (every lane tests every sphere). Spheres are taken
+// four at a time: the four discriminants are formed branch-free and the
+// exec-masked root/compare path runs only if some lane has disc >= 0 for one
+// of them, in index order so the reference's first-wins tie rule (:391) holds.
+__device__ __forceinline__ void sphere_candidate(float disc, float b, float two_a, int idx, float& closest,
+                                                 int& closest_i) {
+    if (disc >= 0.0f) {
+        const float t = (-b - sqrt_rn(disc)) / two_a;
+        if (t > 0.0f && t < closest) {
+            closest = t;
+            closest_i = idx;
+        }
+    }
+}
+
 __device__ __forceinline__ int closest_sphere(const SceneView& sv, uint32_t count, f3 o, f3 d, float& t_out) {
     float closest = kF32Max;
     int closest_i = -1;
     const float a = dot(d, d);
     const float four_a = 4.0f * a;
     const float two_a = 2.0f * a;
-    for (uint32_t i = 0; i < count; ++i) {
+    uint32_t i = 0;
+    for (; i + 4u <= count; i += 4u) {
+        float b[4], disc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 s = sv.sph[i + k];
+            const f3 oc = o - ld3(s);
+            b[k] = 2.0f * dot(d, oc);
+            const float c = dot(oc, oc) - s.w;
+            disc[k] = b[k] * b[k] - four_a * c;
+        }
+        const bool any = (disc[0] >= 0.0f) | (disc[1] >= 0.0f) | (disc[2] >= 0.0f) | (disc[3] >= 0.0f);
+        if (any) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sphere_candidate(disc[k], b[k], two_a, (int)(i + k), closest, closest_i);
+        }
+    }
+    for (; i < count; ++i) {
         const float4 s = sv.sph[i];
         const f3 oc = o - ld3(s);
         const float b = 2.0f * dot(d, oc);
         const float c = dot(oc, oc) - s.w;
-        const float disc = b * b - four_a * c;
-        if (disc >= 0.0f) {
-            const float t = (-b - sqrt_rn(disc)) / two_a;
-            if (t > 0.0f && t < closest) {
-                closest = t;
-                closest_i = (int)i;
-            }
-        }
+        sphere_candidate(b * b - four_a * c, b, two_a, (int)i, closest, closest_i);
     }
     t_out = closest;
     return closest_i;
@@ -193,88 +219,99 @@ __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb
     return decode_texel(ka.env[(size_t)y * ka.env_w + (size_t)x], srgb);
 }
 
-// per_pixel, compute_shader.wgsl:210-314.
-__device__ __forceinline__ f4 per_pixel(const SceneView& sv, const KernelArgs& ka, uint32_t index,
-                                        uint32_t random_index, uint32_t& rays) {
-    f3 o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
+// State of one path of per_pixel (compute_shader.wgsl:210-314) between bounces.
+struct Path {
+    f3 o, d;
+    f4 light, contrib;
+    uint32_t seed;
+    uint32_t bounce;
+};
+
+// per_pixel prologue, :212-222.
+__device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t index, uint32_t random_index, Path& p) {
+    p.o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
     const float4 cr = ka.camera_rays[index];
-    f3 d = mk(cr.x, cr.y, cr.z);
-    uint32_t seed = index * random_index * 326624u;
-    {
-        const float rx = random01(seed), ry = random01(seed), rz = random01(seed);
-        const f3 jit = mk(rx * 2.0f - 1.0f, ry * 2.0f - 1.0f, rz * 2.0f - 1.0f);
-        d = d + jit * 0.0005f;  // not renormalised (:219)
+    p.d = mk(cr.x, cr.y, cr.z);
+    p.seed = index * random_index * 326624u;
+    const float rx = random01(p.seed), ry = random01(p.seed), rz = random01(p.seed);
+    const f3 jit = mk(rx * 2.0f - 1.0f, ry * 2.0f - 1.0f, rz * 2.0f - 1.0f);
+    p.d = p.d + jit * 0.0005f;  // not renormalised (:219)
+    p.contrib = f4{1.0f, 1.0f, 1.0f, 1.0f};
+    p.light = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    p.bounce = 0;
+}
+
+// One iteration of the bounce loop, :226-311. Returns true when the path is
+// finished (escaped to the environment, or the bounce limit is reached).
+__device__ __forceinline__ bool path_step(const SceneView& sv, const KernelArgs& ka, Path& p, uint32_t& rays) {
+    if (p.bounce >= ka.bounces) return true;
+    const Hit h = trace_ray(sv, ka, p.o, p.d);
+    ++rays;
+    if (h.t == kF32Max) {
+        const f4 c = sample_env(ka, sv.srgb, p.d);
+        p.light.x = p.light.x + c.x * p.contrib.x;
+        p.light.y = p.light.y + c.y * p.contrib.y;
+        p.light.z = p.light.z + c.z * p.contrib.z;
+        p.light.w = p.light.w + c.w * p.contrib.w;
+        return true;
     }
-    f4 contrib{1.0f, 1.0f, 1.0f, 1.0f};
-    f4 light{0.0f, 0.0f, 0.0f, 0.0f};
-    for (uint32_t i = 0; i < ka.bounces; ++i) {
-        const Hit h = trace_ray(sv, ka, o, d);
-        ++rays;
-        if (h.t == kF32Max) {
-            const f4 c = sample_env(ka, sv.srgb, d);
-            light.x = light.x + c.x * contrib.x;
-            light.y = light.y + c.y * contrib.y;
-            light.z = light.z + c.z * contrib.z;
-            light.w = light.w + c.w * contrib.w;
-            break;
-        }
-        const RtMaterial m = sv.mat[min(h.material_index, ka.material_count - 1u)];
-        const float gx = normal01(seed);
-        const float gy = normal01(seed);
-        const float gz = normal01(seed);
-        const f3 diffuse = normalize(h.n + mk(gx, gy, gz));
-        const f3 specular = d - h.n * (2.0f * dot(h.n, d));  // reflect(d, n)
-        const f4 color = sample_texture(ka, sv.srgb, m.texture_index, h.u, h.v);
-        const float e = m.emission_power;
-        light.x = light.x + (color.x * e) * contrib.x;
-        light.y = light.y + (color.y * e) * contrib.y;
-        light.z = light.z + (color.z * e) * contrib.z;
-        light.w = light.w + (color.w * e) * contrib.w;
-        const bool is_glass = m.glass > random01(seed);
-        bool tint;
-        if (is_glass) {
-            float ior = m.refraction_index;
-            if (h.front_face) ior = 1.0f / ior;
-            const float cos_t = fmin_nn(dot(-d, h.n), 1.0f);
-            const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
-            const bool reflects = ior * sin_t > 1.0f;
-            float r0 = (1.0f - ior) / (1.0f + ior);  // specular_percentage, :328-334
-            r0 = r0 * r0;
-            const float sp = r0 + (1.0f - r0) * pow5(1.0f - cos_t);
-            const bool is_spec = (m.specular * sp) > random01(seed);
-            if (reflects || is_spec) {
-                d = lerp(specular, diffuse, m.specular_scatter);
-                o = h.p + h.n * 0.0001f;
-                tint = false;
-            } else {
-                // refract, :316-325
-                const f3 perp = (d + h.n * cos_t) * ior;
-                const float len = sqrt_rn(dot(perp, perp));
-                const float len_sq = len * len;
-                const f3 refr = perp + h.n * (-sqrt_rn(__builtin_fabsf(1.0f - len_sq)));
-                d = lerp(refr, diffuse, m.roughness / 10.0f);
-                o = h.p - h.n * 0.0001f;
-                tint = true;
-            }
+    const RtMaterial m = sv.mat[min(h.material_index, ka.material_count - 1u)];
+    const float gx = normal01(p.seed);
+    const float gy = normal01(p.seed);
+    const float gz = normal01(p.seed);
+    const f3 diffuse = normalize(h.n + mk(gx, gy, gz));
+    const f3 specular = p.d - h.n * (2.0f * dot(h.n, p.d));  // reflect(d, n)
+    const f4 color = sample_texture(ka, sv.srgb, m.texture_index, h.u, h.v);
+    const float e = m.emission_power;
+    p.light.x = p.light.x + (color.x * e) * p.contrib.x;
+    p.light.y = p.light.y + (color.y * e) * p.contrib.y;
+    p.light.z = p.light.z + (color.z * e) * p.contrib.z;
+    p.light.w = p.light.w + (color.w * e) * p.contrib.w;
+    const bool is_glass = m.glass > random01(p.seed);
+    bool tint;
+    if (is_glass) {
+        float ior = m.refraction_index;
+        if (h.front_face) ior = 1.0f / ior;
+        const float cos_t = fmin_nn(dot(-p.d, h.n), 1.0f);
+        const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
+        const bool reflects = ior * sin_t > 1.0f;
+        float r0 = (1.0f - ior) / (1.0f + ior);  // specular_percentage, :328-334
+        r0 = r0 * r0;
+        const float sp = r0 + (1.0f - r0) * pow5(1.0f - cos_t);
+        const bool is_spec = (m.specular * sp) > random01(p.seed);
+        if (reflects || is_spec) {
+            p.d = lerp(specular, diffuse, m.specular_scatter);
+            p.o = h.p + h.n * 0.0001f;
+            tint = false;
         } else {
-            const bool is_spec = m.specular > random01(seed);
-            if (is_spec) {
-                d = lerp(specular, diffuse, m.specular_scatter);
-                tint = false;
-            } else {
-                d = lerp(specular, diffuse, m.roughness);
-                tint = true;
-            }
-            o = h.p + h.n * 0.0001f;
+            // refract, :316-325
+            const f3 perp = (p.d + h.n * cos_t) * ior;
+            const float len = sqrt_rn(dot(perp, perp));
+            const float len_sq = len * len;
+            const f3 refr = perp + h.n * (-sqrt_rn(__builtin_fabsf(1.0f - len_sq)));
+            p.d = lerp(refr, diffuse, m.roughness / 10.0f);
+            p.o = h.p - h.n * 0.0001f;
+            tint = true;
         }
-        if (tint) {
-            contrib.x = contrib.x * color.x;
-            contrib.y = contrib.y * color.y;
-            contrib.z = contrib.z * color.z;
-            contrib.w = contrib.w * color.w;
+    } else {
+        const bool is_spec = m.specular > random01(p.seed);
+        if (is_spec) {
+            p.d = lerp(specular, diffuse, m.specular_scatter);
+            tint = false;
+        } else {
+            p.d = lerp(specular, diffuse, m.roughness);
+            tint = true;
         }
+        p.o = h.p + h.n * 0.0001f;
     }
-    return light;
+    if (tint) {
+        p.contrib.x = p.contrib.x * color.x;
+        p.contrib.y = p.contrib.y * color.y;
+        p.contrib.z = p.contrib.z * color.z;
+        p.contrib.w = p.contrib.w * color.w;
+    }
+    p.bounce += 1;
+    return p.bounce >= ka.bounces;
 }
 
 __device__ __forceinline__ float clamp01(float x) { return fmin_nn(fmax_nn(x, 0.0f), 1.0f); }
@@ -290,6 +327,21 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 
 }  // namespace
 
+// Claim the next local tile for this wave: one atomic per 64 pixels on a
+// monotonically increasing 64-bit counter (ka.tile_base is its value at launch
+// start, so no per-frame reset is needed: a launch performs exactly
+// owned_tiles + waves increments, one failing claim per wave).
+__device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
+    const uint64_t live = __ballot(1);
+    const uint32_t leader = (uint32_t)__ffsll((long long)live) - 1u;
+    unsigned long long v = 0;
+    if ((threadIdx.x & 63u) == leader) v = atomicAdd(ka.tile_counter, 1ull);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, leader);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), leader);
+    const uint64_t rel = ((uint64_t)hi << 32 | lo) - ka.tile_base;
+    return rel > 0xffffffffull ? 0xffffffffu : (uint32_t)rel;
+}
+
 // Dynamic LDS image, in this order (all 16-byte aligned):
 //   float4   spheres[sphere_count]   centre.xyz, radius^2
 //   RtMaterial materials[material_count]
@@ -298,6 +350,14 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 //   float    srgb[256]
 // kSceneInLds = false keeps spheres/materials/objects in global memory (for
 // scenes beyond the LDS budget); the sRGB table is always staged.
+//
+// Persistent waves with in-wave path regeneration (the "ray compaction across
+// bounces"): each wave claims 8x8 tiles from a device-wide queue and keeps all
+// 64 lanes busy — whenever lanes' paths finish, __ballot + mbcnt (a wave-wide
+// prefix sum) hand those lanes the next pixels of the current tile, so a
+// wave never idles behind one long path while work remains. A pixel's samples
+// (compute_per_frame) run back to back on one lane, so the accumulation is
+// summed in the reference's order (:160-163) and results are bit-identical.
 template <bool kSceneInLds>
 __global__ void __launch_bounds__(kBlockThreads) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -330,43 +390,78 @@ __global__ void __launch_bounds__(kBlockThreads) rt_pathtrace_kernel(KernelArgs 
     __syncthreads();
 
     const SceneView sv{sph, smat, mat, obj, l_srgb};
+    const bool accumulate = ka.accumulate == 1u;
+    const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;  // :158-175
 
-    const uint32_t wave = tid >> 6;
-    const uint32_t lane = tid & 63u;
-    const uint32_t local_tile = blockIdx.x * kTilesPerBlock + wave;
     uint32_t rays = 0;
-    if (local_tile < ka.owned_tiles) {
-        const uint32_t tile = local_tile * ka.world_size + ka.rank;
-        const uint32_t x = (tile % ka.tiles_x) * 8u + (lane & 7u);
-        const uint32_t y = (tile / ka.tiles_x) * 8u + (lane >> 3);
-        if (x < ka.width && y < ka.height) {
-            const uint32_t index = y * ka.width + x;
-            float r, g, b, a;
-            if (ka.accumulate == 1u) {
-                float4 px = ka.accum[index];
-                uint32_t random_index = ka.accumulation_index;
-                for (uint32_t i = 0; i < ka.compute_per_frame; ++i) {
-                    const f4 l = per_pixel(sv, ka, index, random_index, rays);
-                    px.x = px.x + l.x;
-                    px.y = px.y + l.y;
-                    px.z = px.z + l.z;
-                    px.w = px.w + l.w;
-                    random_index = random_index + 1u;
+    bool active = false;
+    uint32_t index = 0, sample = 0;
+    float4 pix = make_float4(0.f, 0.f, 0.f, 0.f);
+    Path p;
+    p.o = p.d = mk(0.f, 0.f, 0.f);
+    p.light = p.contrib = f4{0.f, 0.f, 0.f, 0.f};
+    p.seed = p.bounce = 0;
+
+    uint32_t tile = claim_tile(ka);  // wave-uniform
+    uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
+    while (true) {
+        // Refill: idle lanes take the next pixels, in slot order.
+        while (true) {
+            const uint64_t need = __ballot(!active);
+            if (need == 0 || tile >= ka.owned_tiles) break;
+            const uint32_t avail = 64u - next;
+            if (!active) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                if (rank < avail) {
+                    const uint32_t slot = next + rank;
+                    const uint32_t gt = tile * ka.world_size + ka.rank;
+                    const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);
+                    const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
+                    if (x < ka.width && y < ka.height) {
+                        index = y * ka.width + x;  // :148
+                        sample = 0;
+                        active = true;
+                        if (accumulate) pix = ka.accum[index];  // :156
+                        start_sample(ka, index, ka.accumulation_index, p);
+                    }
                 }
-                ka.accum[index] = px;
-                const float div = (float)(ka.accumulation_index * ka.compute_per_frame);
-                r = clamp01(px.x / div);
-                g = clamp01(px.y / div);
-                b = clamp01(px.z / div);
-                a = clamp01(px.w / div);
-            } else {
-                const f4 l = per_pixel(sv, ka, index, ka.accumulation_index, rays);
-                r = clamp01(l.x);
-                g = clamp01(l.y);
-                b = clamp01(l.z);
-                a = clamp01(l.w);
             }
-            ka.output[index] = pack_rgba8(r, g, b, a);
+            next += min((uint32_t)__popcll(need), avail);
+            if (next == 64u) {
+                tile = claim_tile(ka);
+                next = 0;
+            }
+        }
+        if (__ballot(active) == 0) break;
+        if (active && path_step(sv, ka, p, rays)) {
+            sample += 1;
+            if (accumulate) {  // pixel_color += per_pixel(...), :161
+                pix.x = pix.x + p.light.x;
+                pix.y = pix.y + p.light.y;
+                pix.z = pix.z + p.light.z;
+                pix.w = pix.w + p.light.w;
+            }
+            if (sample < samples) {
+                start_sample(ka, index, ka.accumulation_index + sample, p);  // random_index += 1, :162
+            } else {
+                float r, g, b, a;
+                if (accumulate) {
+                    ka.accum[index] = pix;  // :164
+                    const float div = (float)(ka.accumulation_index * ka.compute_per_frame);
+                    r = clamp01(pix.x / div);
+                    g = clamp01(pix.y / div);
+                    b = clamp01(pix.z / div);
+                    a = clamp01(pix.w / div);
+                } else {
+                    r = clamp01(p.light.x);
+                    g = clamp01(p.light.y);
+                    b = clamp01(p.light.z);
+                    a = clamp01(p.light.w);
+                }
+                ka.output[index] = pack_rgba8(r, g, b, a);  // :178
+                active = false;
+            }
         }
     }
     atomicAdd(&block_rays, rays);
@@ -382,6 +477,14 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t l
         hipLaunchKernelGGL(rt_pathtrace_kernel<false>, dim3(blocks), dim3(kBlockThreads), lds_bytes, stream, ka);
     }
     return hipGetLastError();
+}
+
+hipError_t rt_pathtrace_occupancy(bool scene_in_lds, size_t lds_bytes, int* blocks_per_cu) {
+    if (scene_in_lds)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_pathtrace_kernel<true>, kBlockThreads,
+                                                            lds_bytes);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_pathtrace_kernel<false>, kBlockThreads,
+                                                        lds_bytes);
 }
 
 // Gather support: pack the accumulation of this rank's tiles, in

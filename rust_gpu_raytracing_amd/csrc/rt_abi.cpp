@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -21,6 +22,7 @@
 
 hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t lds_bytes, uint32_t blocks,
                                hipStream_t stream);
+hipError_t rt_pathtrace_occupancy(bool scene_in_lds, size_t lds_bytes, int* blocks_per_cu);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
@@ -71,6 +73,13 @@ struct rt_ctx {
     float4* d_accum = nullptr;
     uint32_t* d_out = nullptr;
     unsigned long long* d_counter = nullptr;
+    unsigned long long* d_tile_counter = nullptr;
+    unsigned long long tile_base = 0;  // value of *d_tile_counter when the next launch starts
+    int n_cu = 0;
+    bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
+    size_t occ_lds_bytes = 0;
+    bool occ_lds_scene = false;
+    int occ_blocks_per_cu = 0;
     float4* d_sph_hot = nullptr;
     uint32_t* d_sph_mat = nullptr;
     RtMaterial* d_mat = nullptr;
@@ -341,6 +350,14 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
 
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipSetDevice", e));
+    {
+        int n_cu = 0;
+        e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        if (e != hipSuccess) return bail(hip_fail(ctx, "hipDeviceGetAttribute", e));
+        ctx->n_cu = n_cu;
+        const char* env = std::getenv("RT_SCENE_IN_LDS");
+        ctx->force_global_scene = env && env[0] == '0';
+    }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
     e = hipEventCreateWithFlags(&ctx->staging_done, hipEventDisableTiming);
@@ -354,6 +371,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
 
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
         (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_tile_counter, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_hot, info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
@@ -385,7 +403,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_sph_hot, ctx->d_sph_mat,
+    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_tile_counter, ctx->d_sph_hot, ctx->d_sph_mat,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb};
     for (void* b : bufs)
@@ -533,6 +551,8 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.accum = ctx->d_accum;
     ka.output = ctx->d_out;
     ka.ray_counter = ctx->d_counter;
+    ka.tile_counter = ctx->d_tile_counter;
+    ka.tile_base = ctx->tile_base;
     ka.sphere_hot = ctx->d_sph_hot;
     ka.sphere_material = ctx->d_sph_mat;
     ka.materials = ctx->d_mat;
@@ -579,7 +599,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     off = al16(off + (size_t)p.object_count * sizeof(RtObject));
     ka.lds_smat_offset = (uint32_t)off;
     off = al16(off + (size_t)p.sphere_count * 4);
-    const bool scene_in_lds = off + 1024 <= kLdsSceneBudget;
+    const bool scene_in_lds = off + 1024 <= kLdsSceneBudget && !ctx->force_global_scene;
     size_t lds_bytes;
     if (scene_in_lds) {
         ka.lds_srgb_offset = (uint32_t)off;
@@ -588,8 +608,20 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
         ka.lds_srgb_offset = 0;
         lds_bytes = 1024;
     }
-    const uint32_t blocks = (ctx->owned_tiles + kTilesPerBlock - 1) / kTilesPerBlock;
-    if (blocks == 0 || bounces == 0) return RT_OK;
+    // Persistent grid: as many workgroups as can be resident (never more than
+    // one wave per tile); waves then pull tiles from the queue.
+    if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_lds_scene != scene_in_lds) {
+        int per_cu = 0;
+        hipError_t oe = rt_pathtrace_occupancy(scene_in_lds, lds_bytes, &per_cu);
+        if (oe != hipSuccess) return hip_fail(ctx, "hipOccupancyMaxActiveBlocksPerMultiprocessor", oe);
+        ctx->occ_blocks_per_cu = per_cu > 0 ? per_cu : 1;
+        ctx->occ_lds_bytes = lds_bytes;
+        ctx->occ_lds_scene = scene_in_lds;
+    }
+    const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
+    const uint64_t wanted = (ctx->owned_tiles + kTilesPerBlock - 1) / kTilesPerBlock;
+    const uint32_t blocks = (uint32_t)(wanted < resident ? wanted : resident);
+    if (blocks == 0) return RT_OK;
 
     EventPair ev;
     if (ctx->timing) {
@@ -606,6 +638,8 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     }
     hipError_t e = rt_launch_pathtrace(ka, scene_in_lds, lds_bytes, blocks, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
+    // every tile is claimed once and every wave makes one final failing claim
+    ctx->tile_base += (unsigned long long)ctx->owned_tiles + (unsigned long long)blocks * kTilesPerBlock;
     if (ctx->timing) {
         RT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
         ctx->pending.push_back(ev);

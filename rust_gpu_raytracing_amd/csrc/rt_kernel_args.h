@@ -65,6 +65,8 @@ struct KernelArgs {
     float4* __restrict__ accum;
     uint32_t* __restrict__ output;
     unsigned long long* __restrict__ ray_counter;
+    unsigned long long* __restrict__ tile_counter;  // monotonically increasing tile queue head
+    unsigned long long tile_base;                   // its value at launch start
     // scene (bindings 3, 4, 5, 7, 8, 10)
     const float4* __restrict__ sphere_hot;        // centre.xyz, radius*radius (f32, computed at upload)
     const uint32_t* __restrict__ sphere_material;
