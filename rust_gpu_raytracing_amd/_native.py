@@ -123,32 +123,40 @@ _lib = None
 
 
 def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
-    """Load (once) and return the HIP extension; raise if it is unavailable."""
+    """Load and return the HIP extension; raise if it is unavailable.
+
+    With no argument: the in-tree build (cached), or the build named by the
+    RT_LIB environment variable (experiment builds for A/B runs; it must exist
+    too — there is no fallback). With a path: that build, uncached."""
     global _lib
-    if _lib is not None and path is None:
+    if path is None:
+        if _lib is not None:
+            return _lib
+        _lib = _open(Path(os.environ.get("RT_LIB") or LIB_PATH))
         return _lib
-    p = Path(path) if path is not None else LIB_PATH
+    return _open(Path(path))
+
+
+def _open(p: Path) -> ctypes.CDLL:
     if not p.exists():
         raise NativeLibraryError(
             f"{p} not found: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')"
         )
     try:
-        lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+        lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_LOCAL)
     except OSError as exc:  # pragma: no cover - depends on the box
         raise NativeLibraryError(f"could not load {p}: {exc}") from exc
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if path is None:
-        _lib = lib
     return lib
 
 
-def check(ctx, rc: int) -> None:
+def check(ctx, rc: int, lib=None) -> None:
     if rc != RT_OK:
-        msg = load_library().rt_last_error(ctx)
+        msg = (lib or load_library()).rt_last_error(ctx)
         raise RtError(rc, msg.decode() if msg else "")
 
 

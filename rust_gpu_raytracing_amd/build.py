@@ -16,8 +16,8 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 OUT = PKG / "librt_pathtrace.so"
-SOURCES = [CSRC / "pathtrace.hip", CSRC / "rt_abi.cpp"]
-HEADERS = [CSRC / "rt_device_math.h", CSRC / "rt_kernel_args.h", INCLUDE / "rt_abi.h"]
+SOURCES = [CSRC / "pathtrace.hip", CSRC / "rt_abi.cpp", CSRC / "sphere_bvh.cpp"]
+HEADERS = [CSRC / "rt_device_math.h", CSRC / "rt_kernel_args.h", CSRC / "sphere_bvh.h", INCLUDE / "rt_abi.h"]
 
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -28,6 +28,10 @@ NUMERIC_FLAGS = [
     "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-fno-gpu-flush-denormals-to-zero",
 ]
+# gfx950 runs v_pk_{mul,add}_f32 at about a third of the scalar wave-instruction
+# rate (tools/microbench/valu_rate.hip), so the SLP vectorizer's packed f32
+# code is slower than scalar code here: measured -21% kernel time without it.
+PERF_FLAGS = ["-fno-slp-vectorize"]
 
 
 def hipcc_command(out: Path = OUT, extra: list[str] | None = None) -> list[str]:
@@ -37,6 +41,7 @@ def hipcc_command(out: Path = OUT, extra: list[str] | None = None) -> list[str]:
         "-O3",
         "-std=c++17",
         *NUMERIC_FLAGS,
+        *PERF_FLAGS,
         "-fPIC",
         "-shared",
         "-fvisibility=hidden",

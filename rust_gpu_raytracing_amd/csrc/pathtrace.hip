@@ -42,8 +42,10 @@ struct Hit {
 };
 
 struct SceneView {
-    const float4* sph;        // LDS or global: centre.xyz, radius^2
-    const uint32_t* sph_mat;  // material index per sphere
+    const float4* sph;        // per slot: centre.xyz, radius^2 (brute-force set, then BVH leaf order)
+    const uint32_t* orig;     // per slot: original sphere index
+    const uint32_t* sph_mat;  // per original index: material index
+    const float4* nodes;      // sphere BVH, 2 float4 per node (sphere_bvh.h)
     const RtMaterial* mat;    // LDS
     const RtObject* obj;      // LDS
     const float* srgb;        // LDS, 256 entries
@@ -64,54 +66,100 @@ __device__ __forceinline__ f4 decode_texel(uint32_t texel, const float* srgb) {
               (float)(texel >> 24) / 255.0f};
 }
 
-// check_spheres, compute_shader.wgsl:355-404. Returns the closest index or -1.
-// The sweep is wave-uniform (every lane tests every sphere). Spheres are taken
-// four at a time: the four discriminants are formed branch-free and the
-// exec-masked root/compare path runs only if some lane has disc >= 0 for one
-// of them, in index order so the reference's first-wins tie rule (:391) holds.
-__device__ __forceinline__ void sphere_candidate(float disc, float b, float two_a, int idx, float& closest,
-                                                 int& closest_i) {
+// check_spheres, compute_shader.wgsl:355-404.
+//
+// The reference sweeps spheres in index order keeping the first of equal
+// distances (strict `<`, :391), i.e. it returns the lexicographic minimum of
+// (t, index) over spheres with disc >= 0 and t > 0. Here spheres are visited
+// in slot order (brute-force set, then BVH leaves), so acceptance compares
+// (t, original index) lexicographically, which yields the same sphere in any
+// visiting order. `c_orig` starts at 0 so that t == F32_MAX is never taken.
+struct SphereHit {
+    float t;
+    uint32_t orig;
+    uint32_t slot;
+};
+
+__device__ __forceinline__ void sphere_candidate(float disc, float b, float two_a, uint32_t orig, uint32_t slot,
+                                                 SphereHit& best) {
     if (disc >= 0.0f) {
         const float t = (-b - sqrt_rn(disc)) / two_a;
-        if (t > 0.0f && t < closest) {
-            closest = t;
-            closest_i = idx;
+        if (t > 0.0f && (t < best.t || (t == best.t && orig < best.orig))) {
+            best.t = t;
+            best.orig = orig;
+            best.slot = slot;
         }
     }
 }
 
-__device__ __forceinline__ int closest_sphere(const SceneView& sv, uint32_t count, f3 o, f3 d, float& t_out) {
-    float closest = kF32Max;
-    int closest_i = -1;
+// The reference's per-sphere arithmetic (:372-379), unchanged.
+__device__ __forceinline__ float sphere_disc(const float4 s, f3 o, f3 d, float four_a, float& b) {
+    const f3 oc = o - ld3(s);
+    b = 2.0f * dot(d, oc);
+    const float c = dot(oc, oc) - s.w;
+    return b * b - four_a * c;
+}
+
+// Box inflation per unit of (|o| + extent): covers both the f32 rounding of the
+// discriminant (a float disc >= 0 implies the ray line passes within
+// sqrt(r^2 + 32u|o-C|^2) of the centre, u = 2^-24) and of the near root
+// (|t_f - t| <= ~1.4e-3 |o-C| / |d|), with slack for the slab test's own
+// rounding. DESIGN.md §5.2 has the derivation.
+constexpr float kBvhMarginScale = 4.0e-3f;
+
+__device__ __forceinline__ SphereHit closest_sphere(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d) {
+    SphereHit best{kF32Max, 0u, 0u};
     const float a = dot(d, d);
     const float four_a = 4.0f * a;
     const float two_a = 2.0f * a;
+    // brute-force set: wave-uniform sweep, 4 at a time, one exec-masked branch per group
+    const uint32_t n_always = ka.sphere_always;
     uint32_t i = 0;
-    for (; i + 4u <= count; i += 4u) {
+    for (; i + 4u <= n_always; i += 4u) {
         float b[4], disc[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float4 s = sv.sph[i + k];
-            const f3 oc = o - ld3(s);
-            b[k] = 2.0f * dot(d, oc);
-            const float c = dot(oc, oc) - s.w;
-            disc[k] = b[k] * b[k] - four_a * c;
-        }
-        const bool any = (disc[0] >= 0.0f) | (disc[1] >= 0.0f) | (disc[2] >= 0.0f) | (disc[3] >= 0.0f);
-        if (any) {
+        for (int k = 0; k < 4; ++k) disc[k] = sphere_disc(sv.sph[i + k], o, d, four_a, b[k]);
+        // any(disc[k] >= 0): max of the four (NaN operands ignored, as `NaN >= 0` is false)
+        if (fmax_nn(fmax_nn(disc[0], disc[1]), fmax_nn(disc[2], disc[3])) >= 0.0f) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) sphere_candidate(disc[k], b[k], two_a, (int)(i + k), closest, closest_i);
+            for (int k = 0; k < 4; ++k) sphere_candidate(disc[k], b[k], two_a, sv.orig[i + k], i + k, best);
         }
     }
-    for (; i < count; ++i) {
-        const float4 s = sv.sph[i];
-        const f3 oc = o - ld3(s);
-        const float b = 2.0f * dot(d, oc);
-        const float c = dot(oc, oc) - s.w;
-        sphere_candidate(b * b - four_a * c, b, two_a, (int)i, closest, closest_i);
+    for (; i < n_always; ++i) {
+        float b;
+        const float disc = sphere_disc(sv.sph[i], o, d, four_a, b);
+        sphere_candidate(disc, b, two_a, sv.orig[i], i, best);
     }
-    t_out = closest;
-    return closest_i;
+    // BVH set: per-lane stackless traversal over depth-first nodes with skip links
+    const uint32_t n_nodes = ka.sphere_nodes;
+    if (n_nodes != 0) {
+        const float m = kBvhMarginScale * (sqrt_rn(dot(o, o)) + ka.sphere_extent) + 1.0e-6f;
+        const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        uint32_t node = 0;
+        while (node < n_nodes) {
+            const float4 lo = sv.nodes[2u * node];
+            const float4 hi = sv.nodes[2u * node + 1u];
+            const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
+            const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
+            const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
+            const float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
+            const float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
+            // enters the inflated box, not wholly behind the origin, not beyond the best hit
+            const bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= best.t * 1.00001f;
+            const uint32_t leaf = __float_as_uint(hi.w);
+            if (hit && leaf != 0xffffffffu) {
+                const uint32_t first = leaf & 0xffffffu;
+                const uint32_t cnt = leaf >> 24;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    float b;
+                    const float disc = sphere_disc(sv.sph[first + k], o, d, four_a, b);
+                    sphere_candidate(disc, b, two_a, sv.orig[first + k], first + k, best);
+                }
+            }
+            node = (hit && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
+        }
+    }
+    return best;
 }
 
 // ray_in_bounds, compute_shader.wgsl:407-419.
@@ -181,11 +229,11 @@ __device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& 
     h.u = 0.f;
     h.v = 0.f;
     if (ka.object_count != 0) closest_triangle(sv, ka, o, d, h);
-    float ts;
-    const int si = closest_sphere(sv, ka.sphere_count, o, d, ts);
-    if (si >= 0 && ts < h.t) {
+    const SphereHit sh = closest_sphere(sv, ka, o, d);
+    if (sh.t < h.t) {  // sphere wins only if strictly closer (:347); no sphere -> F32_MAX
         // sphere_hit, :530-555, and sphere_texture_coords, :557-566
-        const float4 s = sv.sph[si];
+        const float4 s = sv.sph[sh.slot];
+        const float ts = sh.t;
         const f3 p = o + d * ts;
         const f3 outward = normalize(p - ld3(s));
         const float theta = acosf_c(-outward.y);
@@ -196,7 +244,7 @@ __device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& 
         h.v = theta / kWgslPi;
         h.front_face = dot(d, outward) < 0.0f;
         h.n = h.front_face ? outward : -outward;
-        h.material_index = sv.sph_mat[si];
+        h.material_index = sv.sph_mat[sh.orig];
     }
     return h;
 }
@@ -343,13 +391,15 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
 }
 
 // Dynamic LDS image, in this order (all 16-byte aligned):
-//   float4   spheres[sphere_count]   centre.xyz, radius^2
+//   float4   sphere slots[sphere_count]   centre.xyz, radius^2
 //   RtMaterial materials[material_count]
 //   RtObject objects[object_count]
-//   uint32   sphere_material[sphere_count]
+//   uint32   slot -> original index[sphere_count]
+//   uint32   sphere material[sphere_count] (by original index)
+//   float4x2 sphere BVH nodes[sphere_nodes]
 //   float    srgb[256]
-// kSceneInLds = false keeps spheres/materials/objects in global memory (for
-// scenes beyond the LDS budget); the sRGB table is always staged.
+// kSceneInLds = false keeps the scene in global memory (for scenes beyond the
+// LDS budget); the sRGB table is always staged.
 //
 // Persistent waves with in-wave path regeneration (the "ray compaction across
 // bounces"): each wave claims 8x8 tiles from a device-wide queue and keeps all
@@ -358,38 +408,39 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
 // wave never idles behind one long path while work remains. A pixel's samples
 // (compute_per_frame) run back to back on one lane, so the accumulation is
 // summed in the reference's order (:160-163) and results are bit-identical.
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 1
+#endif
 template <bool kSceneInLds>
-__global__ void __launch_bounds__(kBlockThreads) rt_pathtrace_kernel(KernelArgs ka) {
+__global__ void __launch_bounds__(kBlockThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
 
     const uint32_t tid = threadIdx.x;
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
-    const float4* sph = ka.sphere_hot;
-    const uint32_t* smat = ka.sphere_material;
-    const RtMaterial* mat = ka.materials;
-    const RtObject* obj = ka.objects;
+    SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, ka.objects,
+                 l_srgb};
     if (tid == 0) block_rays = 0;
     if constexpr (kSceneInLds) {
         float4* l_sph = reinterpret_cast<float4*>(lds);
         RtMaterial* l_mat = reinterpret_cast<RtMaterial*>(lds + ka.lds_mat_offset);
         RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
+        uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
         uint32_t* l_smat = reinterpret_cast<uint32_t*>(lds + ka.lds_smat_offset);
+        float4* l_nodes = reinterpret_cast<float4*>(lds + ka.lds_nodes_offset);
         for (uint32_t i = tid; i < ka.sphere_count; i += kBlockThreads) {
-            l_sph[i] = ka.sphere_hot[i];
+            l_sph[i] = ka.sphere_slots[i];
+            l_orig[i] = ka.sphere_orig[i];
             l_smat[i] = ka.sphere_material[i];
         }
+        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kBlockThreads) l_nodes[i] = ka.sphere_bvh[i];
         for (uint32_t i = tid; i < ka.material_count; i += kBlockThreads) l_mat[i] = ka.materials[i];
         for (uint32_t i = tid; i < ka.object_count; i += kBlockThreads) l_obj[i] = ka.objects[i];
-        sph = l_sph;
-        smat = l_smat;
-        mat = l_mat;
-        obj = l_obj;
+        sv = SceneView{l_sph, l_orig, l_smat, l_nodes, l_mat, l_obj, l_srgb};
     }
     for (uint32_t i = tid; i < 256u; i += kBlockThreads) l_srgb[i] = ka.srgb[i];
     __syncthreads();
 
-    const SceneView sv{sph, smat, mat, obj, l_srgb};
     const bool accumulate = ka.accumulate == 1u;
     const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;  // :158-175
 

@@ -19,6 +19,7 @@
 
 #include "rt_abi.h"
 #include "rt_kernel_args.h"
+#include "sphere_bvh.h"
 
 hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t lds_bytes, uint32_t blocks,
                                hipStream_t stream);
@@ -80,8 +81,16 @@ struct rt_ctx {
     size_t occ_lds_bytes = 0;
     bool occ_lds_scene = false;
     int occ_blocks_per_cu = 0;
-    float4* d_sph_hot = nullptr;
-    uint32_t* d_sph_mat = nullptr;
+    float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
+    uint32_t* d_slot_orig = nullptr;
+    uint32_t* d_sph_mat = nullptr;       // by original index
+    SphereBvhNode* d_bvh = nullptr;
+    std::vector<rt_scene_sphere> h_sph;  // host copy: the BVH is rebuilt from it
+    bool slots_dirty = true;
+    uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
+    bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
+    uint32_t n_always = 0, n_nodes = 0;
+    float sphere_extent = 0.0f;
     RtMaterial* d_mat = nullptr;
     RtObject* d_obj = nullptr;
     RtSubObject* d_sub = nullptr;
@@ -183,20 +192,30 @@ int upload_raw(rt_ctx* ctx, void* dst, const void* src, size_t bytes) {
 
 int upload_spheres(rt_ctx* ctx, const rt_scene_sphere* s, uint32_t n) {
     if (n == 0) return RT_OK;
-    void* p;
-    int rc = staging(ctx, (size_t)n * 20, &p);
-    if (rc) return rc;
-    float4* hot = static_cast<float4*>(p);
-    uint32_t* mat = reinterpret_cast<uint32_t*>(hot + n);
-    for (uint32_t i = 0; i < n; i++) {
-        // radius^2 is the same single f32 product the shader forms (:375)
-        hot[i] = make_float4(s[i].position[0], s[i].position[1], s[i].position[2], s[i].radius * s[i].radius);
-        mat[i] = s[i].material_index;
-    }
-    RT_HIP(ctx, hipMemcpyAsync(ctx->d_sph_hot, hot, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
-    RT_HIP(ctx, hipMemcpyAsync(ctx->d_sph_mat, mat, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
-    RT_HIP(ctx, hipEventRecord(ctx->staging_done, ctx->stream));
-    ctx->staging_busy = true;
+    std::copy(s, s + n, ctx->h_sph.begin());
+    ctx->slots_dirty = true;  // slots + BVH are rebuilt at the next dispatch
+    return RT_OK;
+}
+
+// Rebuild the kernel's sphere slots (brute-force set + BVH) for the first
+// `count` spheres and upload them, stream-ordered before the next launch.
+int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
+    if (!ctx->slots_dirty && ctx->slots_count == count) return RT_OK;
+    SphereSlots sl;
+    build_sphere_slots(ctx->h_sph.data(), count, ctx->use_bvh, &sl);
+    std::vector<uint32_t> mat(count);
+    for (uint32_t i = 0; i < count; i++) mat[i] = ctx->h_sph[i].material_index;
+    int rc;
+    if ((rc = upload_raw(ctx, ctx->d_slot_sph, sl.slot_sph.data(), sl.slot_sph.size() * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_slot_orig, sl.slot_orig.data(), sl.slot_orig.size() * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_sph_mat, mat.data(), mat.size() * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_bvh, sl.nodes.data(), sl.nodes.size() * sizeof(SphereBvhNode))))
+        return rc;
+    ctx->n_always = sl.n_always;
+    ctx->n_nodes = (uint32_t)sl.nodes.size();
+    ctx->sphere_extent = sl.extent;
+    ctx->slots_dirty = false;
+    ctx->slots_count = count;
     return RT_OK;
 }
 
@@ -346,6 +365,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
     ctx->n_tri_dev = info->triangle_count ? info->triangle_count : 1;
     ctx->n_sub_dev = info->sub_object_count ? info->sub_object_count : 1;
     ctx->h_obj.assign(info->objects, info->objects + info->object_count);
+    ctx->h_sph.resize(info->sphere_count);
     ctx->h_sub.assign(info->sub_objects, info->sub_objects + info->sub_object_count);
 
     hipError_t e = hipSetDevice(ctx->device);
@@ -357,6 +377,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->n_cu = n_cu;
         const char* env = std::getenv("RT_SCENE_IN_LDS");
         ctx->force_global_scene = env && env[0] == '0';
+        env = std::getenv("RT_SPHERE_BVH");
+        ctx->use_bvh = !(env && env[0] == '0');
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
@@ -372,8 +394,10 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
         (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_tile_counter, 1)) ||
-        (rc = dev_alloc(ctx, &ctx->d_sph_hot, info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_slot_sph, info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_slot_orig, info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_bvh, 2 * (size_t)info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
         (rc = dev_alloc(ctx, &ctx->d_srgb, 256)) || (rc = dev_alloc(ctx, &ctx->d_tex, 1)) ||
@@ -403,7 +427,8 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_tile_counter, ctx->d_sph_hot, ctx->d_sph_mat,
+    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_tile_counter, ctx->d_slot_sph,
+                    ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb};
     for (void* b : bufs)
@@ -546,6 +571,10 @@ int rt_update_materials(rt_ctx* ctx, const rt_scene_material* materials, uint32_
 int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     RT_ENTER(ctx);
     const rt_params& p = ctx->params;
+    {
+        int rc = refresh_sphere_slots(ctx, p.sphere_count);
+        if (rc) return rc;
+    }
     KernelArgs ka{};
     ka.camera_rays = ctx->d_rays;
     ka.accum = ctx->d_accum;
@@ -553,8 +582,13 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.ray_counter = ctx->d_counter;
     ka.tile_counter = ctx->d_tile_counter;
     ka.tile_base = ctx->tile_base;
-    ka.sphere_hot = ctx->d_sph_hot;
+    ka.sphere_slots = ctx->d_slot_sph;
+    ka.sphere_orig = ctx->d_slot_orig;
     ka.sphere_material = ctx->d_sph_mat;
+    ka.sphere_bvh = reinterpret_cast<const float4*>(ctx->d_bvh);
+    ka.sphere_always = ctx->n_always;
+    ka.sphere_nodes = ctx->n_nodes;
+    ka.sphere_extent = ctx->sphere_extent;
     ka.materials = ctx->d_mat;
     ka.objects = ctx->d_obj;
     ka.sub_objects = ctx->d_sub;
@@ -590,15 +624,19 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.rank = ctx->rank;
     ka.world_size = ctx->world;
 
-    // dynamic LDS carve-up: spheres | materials | objects | sphere materials | srgb
+    // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
     size_t off = al16((size_t)p.sphere_count * 16);
     ka.lds_mat_offset = (uint32_t)off;
     off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
     ka.lds_obj_offset = (uint32_t)off;
     off = al16(off + (size_t)p.object_count * sizeof(RtObject));
+    ka.lds_orig_offset = (uint32_t)off;
+    off = al16(off + (size_t)p.sphere_count * 4);
     ka.lds_smat_offset = (uint32_t)off;
     off = al16(off + (size_t)p.sphere_count * 4);
+    ka.lds_nodes_offset = (uint32_t)off;
+    off = al16(off + (size_t)ctx->n_nodes * sizeof(SphereBvhNode));
     const bool scene_in_lds = off + 1024 <= kLdsSceneBudget && !ctx->force_global_scene;
     size_t lds_bytes;
     if (scene_in_lds) {

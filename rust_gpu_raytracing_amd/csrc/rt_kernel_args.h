@@ -8,7 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-constexpr uint32_t kBlockThreads = 256;            // 4 waves
+constexpr uint32_t kBlockThreads = 512;            // 8 waves share one LDS copy of the scene
 constexpr uint32_t kTilesPerBlock = kBlockThreads / 64;  // one 8x8 tile per wave
 
 struct RtSphere {  // src/buffers.rs:40-45, 32 B
@@ -68,8 +68,10 @@ struct KernelArgs {
     unsigned long long* __restrict__ tile_counter;  // monotonically increasing tile queue head
     unsigned long long tile_base;                   // its value at launch start
     // scene (bindings 3, 4, 5, 7, 8, 10)
-    const float4* __restrict__ sphere_hot;        // centre.xyz, radius*radius (f32, computed at upload)
-    const uint32_t* __restrict__ sphere_material;
+    const float4* __restrict__ sphere_slots;      // centre.xyz, radius*radius (f32), kernel order (sphere_bvh.h)
+    const uint32_t* __restrict__ sphere_orig;     // slot -> original sphere index
+    const uint32_t* __restrict__ sphere_material; // original index -> material index
+    const float4* __restrict__ sphere_bvh;        // SphereBvhNode[sphere_nodes] as float4 pairs
     const RtMaterial* __restrict__ materials;
     const RtObject* __restrict__ objects;
     const RtSubObject* __restrict__ sub_objects;
@@ -85,6 +87,9 @@ struct KernelArgs {
     uint32_t accumulate;
     uint32_t sphere_count;
     uint32_t object_count;
+    uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
+    uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
+    float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
     uint32_t compute_per_frame;
     uint32_t texture_width;
     uint32_t texture_height;
@@ -106,6 +111,8 @@ struct KernelArgs {
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;
     uint32_t lds_obj_offset;
+    uint32_t lds_orig_offset;
     uint32_t lds_smat_offset;
+    uint32_t lds_nodes_offset;
     uint32_t lds_srgb_offset;
 };

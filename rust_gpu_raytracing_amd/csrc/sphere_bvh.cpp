@@ -1,0 +1,180 @@
+// sphere_bvh.cpp — binned-SAH BVH over spheres, flattened depth-first with
+// skip links for stackless traversal on the GPU.
+#include "sphere_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+namespace {
+
+struct Box {
+    double lo[3] = {INFINITY, INFINITY, INFINITY};
+    double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const double* a, const double* b) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], a[k]);
+            hi[k] = std::max(hi[k], b[k]);
+        }
+    }
+    void grow(const Box& o) { grow(o.lo, o.hi); }
+    double area() const {
+        if (lo[0] > hi[0]) return 0.0;
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct Prim {
+    Box box;
+    double c[3];
+    uint32_t orig;
+};
+
+struct Builder {
+    std::vector<Prim>& prims;
+    std::vector<SphereBvhNode>& nodes;
+    std::vector<uint32_t> leaf_order;
+
+    // Builds the subtree over prims[begin, end) at node index `at` (pre-order).
+    void build(uint32_t begin, uint32_t end) {
+        const uint32_t at = (uint32_t)nodes.size();
+        nodes.push_back(SphereBvhNode{});
+        Box box, cbox;
+        for (uint32_t i = begin; i < end; i++) {
+            box.grow(prims[i].box);
+            cbox.grow(prims[i].c, prims[i].c);
+        }
+        for (int k = 0; k < 3; k++) {  // round outward to f32
+            nodes[at].bmin[k] = std::nextafter((float)box.lo[k], -INFINITY);
+            nodes[at].bmax[k] = std::nextafter((float)box.hi[k], INFINITY);
+        }
+        const uint32_t n = end - begin;
+        if (n <= kSphereBvhLeafMax) {
+            nodes[at].leaf = (uint32_t)leaf_order.size() | (n << 24);
+            for (uint32_t i = begin; i < end; i++) leaf_order.push_back(prims[i].orig);
+            nodes[at].skip = (uint32_t)nodes.size();
+            return;
+        }
+        // binned SAH along the widest centroid axis
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (cbox.hi[k] - cbox.lo[k] > cbox.hi[axis] - cbox.lo[axis]) axis = k;
+        const double span = cbox.hi[axis] - cbox.lo[axis];
+        uint32_t mid = begin + n / 2;
+        if (span > 0.0) {
+            constexpr int kBins = 16;
+            Box bins[kBins];
+            uint32_t cnt[kBins] = {};
+            auto bin_of = [&](const Prim& p) {
+                int b = (int)((p.c[axis] - cbox.lo[axis]) / span * kBins);
+                return std::min(std::max(b, 0), kBins - 1);
+            };
+            for (uint32_t i = begin; i < end; i++) {
+                const int b = bin_of(prims[i]);
+                bins[b].grow(prims[i].box);
+                cnt[b]++;
+            }
+            double best = INFINITY;
+            int best_split = -1;
+            for (int s = 1; s < kBins; s++) {
+                Box l, r;
+                uint32_t nl = 0, nr = 0;
+                for (int b = 0; b < s; b++) {
+                    if (cnt[b]) l.grow(bins[b]);
+                    nl += cnt[b];
+                }
+                for (int b = s; b < kBins; b++) {
+                    if (cnt[b]) r.grow(bins[b]);
+                    nr += cnt[b];
+                }
+                if (nl == 0 || nr == 0) continue;
+                const double cost = l.area() * nl + r.area() * nr;
+                if (cost < best) {
+                    best = cost;
+                    best_split = s;
+                }
+            }
+            if (best_split > 0) {
+                auto it = std::stable_partition(prims.begin() + begin, prims.begin() + end,
+                                                [&](const Prim& p) { return bin_of(p) < best_split; });
+                mid = (uint32_t)(it - prims.begin());
+            } else {
+                std::stable_sort(prims.begin() + begin, prims.begin() + end,
+                                 [&](const Prim& a, const Prim& b) { return a.c[axis] < b.c[axis]; });
+            }
+        }
+        if (mid == begin || mid == end) mid = begin + n / 2;
+        nodes[at].leaf = kSphereBvhInternal;
+        build(begin, mid);
+        build(mid, end);
+        nodes[at].skip = (uint32_t)nodes.size();
+    }
+};
+
+}  // namespace
+
+void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, SphereSlots* out) {
+    out->n_always = 0;
+    out->slot_sph.clear();
+    out->slot_orig.clear();
+    out->nodes.clear();
+    out->extent = 0.0f;
+
+    auto push_slot = [&](uint32_t i) {
+        const rt_scene_sphere& sp = s[i];
+        out->slot_sph.insert(out->slot_sph.end(),
+                             {sp.position[0], sp.position[1], sp.position[2], sp.radius * sp.radius});
+        out->slot_orig.push_back(i);
+    };
+
+    // Extent of each sphere from the origin; the handful of huge/far spheres
+    // (a ground sphere of radius 1000) stay in the brute-force set so that the
+    // per-ray BVH margin, proportional to the BVH spheres' extent, stays small.
+    std::vector<double> ext(count);
+    for (uint32_t i = 0; i < count; i++) {
+        const rt_scene_sphere& sp = s[i];
+        ext[i] = std::sqrt((double)sp.position[0] * sp.position[0] + (double)sp.position[1] * sp.position[1] +
+                           (double)sp.position[2] * sp.position[2]) +
+                 std::fabs((double)sp.radius);
+    }
+    std::vector<bool> in_bvh(count, false);
+    if (use_bvh && count >= 16) {
+        std::vector<double> sorted(ext);
+        std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
+        const double cap = 8.0 * std::max(sorted[count / 2], 1e-30);
+        for (uint32_t i = 0; i < count; i++) in_bvh[i] = std::isfinite(ext[i]) && ext[i] <= cap;
+    }
+    for (uint32_t i = 0; i < count; i++)
+        if (!in_bvh[i]) push_slot(i);
+    out->n_always = (uint32_t)out->slot_orig.size();
+
+    std::vector<Prim> prims;
+    double extent = 0.0;
+    for (uint32_t i = 0; i < count; i++) {
+        if (!in_bvh[i]) continue;
+        const rt_scene_sphere& sp = s[i];
+        Prim p;
+        const double r = std::fabs((double)sp.radius);
+        for (int k = 0; k < 3; k++) {
+            p.c[k] = sp.position[k];
+            p.box.lo[k] = p.c[k] - r;
+            p.box.hi[k] = p.c[k] + r;
+        }
+        p.orig = i;
+        prims.push_back(p);
+        extent = std::max(extent, ext[i]);
+    }
+    if (prims.size() < 2) {  // nothing worth a tree: brute-force everything
+        for (const Prim& p : prims) push_slot(p.orig);
+        out->n_always = (uint32_t)out->slot_orig.size();
+        return;
+    }
+    Builder b{prims, out->nodes, {}};
+    b.build(0, (uint32_t)prims.size());
+    for (uint32_t orig : b.leaf_order) push_slot(orig);
+    // leaf fields index the BVH part of the slot array; shift by the brute-force prefix
+    for (SphereBvhNode& nd : out->nodes)
+        if (nd.leaf != kSphereBvhInternal) nd.leaf += out->n_always;
+    out->extent = std::nextafter((float)extent, INFINITY);
+}

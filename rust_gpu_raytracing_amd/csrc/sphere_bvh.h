@@ -1,0 +1,42 @@
+// sphere_bvh.h — host-built bounding-volume hierarchy over the scene spheres.
+//
+// The reference tests every sphere for every ray (check_spheres,
+// compute_shader.wgsl:355-404). The kernel instead walks this BVH and tests
+// only the spheres in boxes the ray can reach, with boxes inflated by a per-ray
+// margin that provably covers the f32 rounding of the reference's formula
+// (DESIGN.md §5.2), so the closest sphere — and with the (t, index)
+// lexicographic minimum, the tie winner — is exactly the one the brute-force
+// sweep finds.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "rt_abi.h"
+
+// 32-byte node, depth-first order. Internal: left child = this + 1, right child
+// follows the left subtree. `skip` = first node after this subtree.
+struct SphereBvhNode {
+    float bmin[3];
+    uint32_t skip;
+    float bmax[3];
+    uint32_t leaf;  // kSphereBvhInternal, or first_slot | (count << 24)
+};
+static_assert(sizeof(SphereBvhNode) == 32, "node layout");
+
+constexpr uint32_t kSphereBvhInternal = 0xffffffffu;
+constexpr uint32_t kSphereBvhLeafMax = 4;
+
+struct SphereSlots {
+    // Spheres in kernel order: the brute-force ("always") set first, in
+    // original index order, then the BVH leaves' spheres in leaf order.
+    uint32_t n_always = 0;
+    std::vector<float> slot_sph;        // 4 per slot: centre.xyz, radius*radius
+    std::vector<uint32_t> slot_orig;    // original sphere index of each slot
+    std::vector<SphereBvhNode> nodes;   // empty when every sphere is brute-forced
+    float extent = 0.0f;                // max over BVH spheres of |centre| + radius (rounded up)
+};
+
+// Build the slot layout for the first `count` spheres. With `use_bvh` false (or
+// too few spheres to pay off) every sphere is in the brute-force set.
+void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use_bvh, SphereSlots* out);

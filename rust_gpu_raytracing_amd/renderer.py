@@ -41,8 +41,9 @@ class Renderer:
         rank: int = 0,
         world_size: int = 1,
         camera_rays: np.ndarray | None = None,
+        lib=None,
     ):
-        self._lib = N.load_library()
+        self._lib = N.load_library() if lib is None else lib
         self.scene = scene
         self.accumulate = accumulate
         self.compute_per_frame = compute_per_frame
@@ -67,7 +68,7 @@ class Renderer:
         info.params = N.params_struct(self._params(accumulation_index=1))
         info.rank, info.world_size = rank, world_size
         ctx = ctypes.c_void_p()
-        N.check(None, self._lib.rt_create(ctypes.byref(info), ctypes.byref(ctx)))
+        N.check(None, self._lib.rt_create(ctypes.byref(info), ctypes.byref(ctx)), self._lib)
         self._ctx = ctx
         self._upload_textures()
 
@@ -82,7 +83,7 @@ class Renderer:
     def _call(self, name, *args):
         if self._ctx is None:
             raise N.RtError(N.RT_E_INVALID, "renderer is closed")
-        N.check(self._ctx, getattr(self._lib, name)(self._ctx, *args))
+        N.check(self._ctx, getattr(self._lib, name)(self._ctx, *args), self._lib)
 
     def _upload_textures(self):
         tex = np.ascontiguousarray(self.scene.textures, np.uint8)
@@ -171,7 +172,7 @@ class Renderer:
         v = ctypes.c_uint64()
         r = self.rank if rank is None else rank
         w = self.world_size if world_size is None else world_size
-        N.check(self._ctx, self._lib.rt_owned_pixel_count(self._ctx, r, w, ctypes.byref(v)))
+        N.check(self._ctx, self._lib.rt_owned_pixel_count(self._ctx, r, w, ctypes.byref(v)), self._lib)
         return v.value
 
     def pack_owned_accumulation(self, dst_device_ptr: int) -> None:

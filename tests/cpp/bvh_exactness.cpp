@@ -1,0 +1,152 @@
+// CPU check of the sphere-BVH culling used by rt_pathtrace_kernel: for many
+// rays, the kernel's traversal logic (restated here in the same f32 operation
+// order, compiled with -ffp-contract=off) must return exactly the sphere and
+// t of the reference's brute-force scan (compute_shader.wgsl:355-404).
+// usage: bvh_exactness <n_rays> <seed>   -> prints "ok <rays> <hits> <avg_tests>" or the first mismatch
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "sphere_bvh.h"
+
+static const float F32_MAX_ = 3.4028235e+38f;
+struct V { float x, y, z; };
+static V sub(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static float dot(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static float fmin_nn(float a, float b) { return std::fmin(a, b); }
+static float fmax_nn(float a, float b) { return std::fmax(a, b); }
+
+struct Res { float t; int idx; };
+
+static Res brute(const std::vector<rt_scene_sphere>& s, V o, V d) {
+    float closest = F32_MAX_;
+    int ci = -1;
+    float a = dot(d, d);
+    for (size_t i = 0; i < s.size(); i++) {
+        V oc = sub(o, V{s[i].position[0], s[i].position[1], s[i].position[2]});
+        float b = 2.0f * dot(d, oc);
+        float c = dot(oc, oc) - s[i].radius * s[i].radius;
+        float disc = b * b - 4.0f * a * c;
+        if (disc < 0.0f) continue;
+        float t = (-b - std::sqrt(disc)) / (2.0f * a);
+        if (t > 0.0f && t < closest) { closest = t; ci = (int)i; }
+    }
+    return {closest, ci};
+}
+
+static long g_tests = 0;
+
+static void cand(const SphereSlots& sl, uint32_t slot, V o, V d, float four_a, float two_a, float& bt, uint32_t& bo, bool& found) {
+    const float* q = &sl.slot_sph[4 * slot];
+    V oc = sub(o, V{q[0], q[1], q[2]});
+    float b = 2.0f * dot(d, oc);
+    float c = dot(oc, oc) - q[3];
+    float disc = b * b - four_a * c;
+    g_tests++;
+    if (disc >= 0.0f) {
+        float t = (-b - std::sqrt(disc)) / two_a;
+        uint32_t orig = sl.slot_orig[slot];
+        if (t > 0.0f && (t < bt || (t == bt && orig < bo))) { bt = t; bo = orig; found = true; }
+    }
+}
+
+static Res kernel_like(const SphereSlots& sl, V o, V d) {
+    float bt = F32_MAX_;
+    uint32_t bo = 0;
+    bool found = false;
+    float a = dot(d, d), four_a = 4.0f * a, two_a = 2.0f * a;
+    for (uint32_t i = 0; i < sl.n_always; i++) cand(sl, i, o, d, four_a, two_a, bt, bo, found);
+    const uint32_t n = (uint32_t)sl.nodes.size();
+    if (n) {
+        const float m = (getenv("MARGIN") ? (float)atof(getenv("MARGIN")) : 4.0e-3f) * (std::sqrt(dot(o, o)) + sl.extent) + (getenv("MARGIN") ? 0.0f : 1.0e-6f);
+        V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        uint32_t node = 0;
+        while (node < n) {
+            const SphereBvhNode& nd = sl.nodes[node];
+            float tx0 = (nd.bmin[0] - m - o.x) * inv.x, tx1 = (nd.bmax[0] + m - o.x) * inv.x;
+            float ty0 = (nd.bmin[1] - m - o.y) * inv.y, ty1 = (nd.bmax[1] + m - o.y) * inv.y;
+            float tz0 = (nd.bmin[2] - m - o.z) * inv.z, tz1 = (nd.bmax[2] + m - o.z) * inv.z;
+            float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
+            float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
+            bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= bt * 1.00001f;
+            if (hit && nd.leaf != kSphereBvhInternal) {
+                uint32_t first = nd.leaf & 0xffffffu, cnt = nd.leaf >> 24;
+                for (uint32_t k = 0; k < cnt; k++) cand(sl, first + k, o, d, four_a, two_a, bt, bo, found);
+            }
+            node = (hit && nd.leaf == kSphereBvhInternal) ? node + 1 : nd.skip;
+        }
+    }
+    return {bt, found ? (int)bo : -1};
+}
+
+int main(int argc, char** argv) {
+    long n_rays = argc > 1 ? atol(argv[1]) : 200000;
+    unsigned seed = argc > 2 ? (unsigned)atoi(argv[2]) : 1;
+    std::mt19937 rng(seed);
+    std::uniform_real_distribution<float> U(0.0f, 1.0f);
+    // RTIOW-like field + ground + a few big spheres + duplicates (ties) + touching spheres
+    std::vector<rt_scene_sphere> s;
+    auto add = [&](float x, float y, float z, float r) {
+        rt_scene_sphere sp{}; sp.position[0] = x; sp.position[1] = y; sp.position[2] = z; sp.radius = r;
+        sp.material_index = (uint32_t)s.size(); s.push_back(sp);
+    };
+    add(0, 1000, 0, 1000);
+    for (int a = -11; a < 11; a++)
+        for (int b = -11; b < 11; b++) add(a + 0.9f * U(rng), -0.2f, b + 0.9f * U(rng), 0.2f);
+    add(0, -1, 0, 1); add(-4, -1, 0, 1); add(4, -1, 0, 1);
+    add(4, -1, 0, 1);           // exact duplicate: tie must go to the lower index
+    add(4.5f, -1.2f, 0.3f, 0.7f);  // overlapping
+    add(0.0f, -3.0f, 0.0f, 0.001f); // tiny
+    SphereSlots sl;
+    build_sphere_slots(s.data(), (uint32_t)s.size(), true, &sl);
+    if (sl.nodes.empty()) { printf("no bvh built\n"); return 2; }
+    // structural checks
+    std::vector<int> seen(s.size(), 0);
+    for (uint32_t i = 0; i < sl.slot_orig.size(); i++) seen[sl.slot_orig[i]]++;
+    for (size_t i = 0; i < s.size(); i++) if (seen[i] != 1) { printf("slot coverage broken at %zu\n", i); return 1; }
+    long hits = 0;
+    for (long r = 0; r < n_rays; r++) {
+        V o, d;
+        int kind = r % 5;
+        if (kind == 0) {  // camera-like
+            o = {13.0f + U(rng), -2.0f - U(rng), 3.0f + U(rng)};
+            d = {-13.0f + 6 * (U(rng) - 0.5f), 2.0f + 2 * (U(rng) - 0.5f), -3.0f + 6 * (U(rng) - 0.5f)};
+        } else if (kind <= 2) {  // secondary from a sphere surface, offset like the shader (+-n*1e-4)
+            const rt_scene_sphere& sp = s[1 + (rng() % (s.size() - 1))];
+            V n{U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f};
+            float inv = 1.0f / std::sqrt(dot(n, n));
+            n = {n.x * inv, n.y * inv, n.z * inv};
+            float off = (kind == 1 ? 1.0f : -1.0f) * 0.0001f;
+            o = {sp.position[0] + n.x * sp.radius + n.x * off, sp.position[1] + n.y * sp.radius + n.y * off,
+                 sp.position[2] + n.z * sp.radius + n.z * off};
+            d = {U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f};
+            if (r % 7 == 0) d = {n.z, 0.0f, -n.x};  // tangent
+        } else if (kind == 3) {  // from the ground, far out
+            o = {200 * (U(rng) - 0.5f), -0.0001f, 200 * (U(rng) - 0.5f)};
+            d = {U(rng) - 0.5f, -U(rng), U(rng) - 0.5f};
+        } else {  // axis-parallel and tiny components, aimed at sphere centres
+            const rt_scene_sphere& sp = s[rng() % s.size()];
+            o = {sp.position[0] + 5 * (U(rng) - 0.5f), sp.position[1] - 3, sp.position[2]};
+            d = {0.0f, 1.0f, (r % 3 == 0) ? 1e-30f : 0.0f};
+            if (r % 2) d = {sp.position[0] - o.x, sp.position[1] - o.y + sp.radius * (U(rng) - 0.5f) * 2, sp.position[2] - o.z};
+        }
+        float scale = 0.5f + 2.0f * U(rng);  // non-unit directions (jitter breaks unit length, :219)
+        d = {d.x * scale, d.y * scale, d.z * scale};
+        Res a = brute(s, o, d), b = kernel_like(sl, o, d);
+        uint32_t ta, tb;
+        memcpy(&ta, &a.t, 4);
+        memcpy(&tb, &b.t, 4);
+        if (a.idx != b.idx || ta != tb) {
+            printf("MISMATCH ray %ld kind %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) brute=(%d %.9g) bvh=(%d %.9g)\n", r,
+                   kind, o.x, o.y, o.z, d.x, d.y, d.z, a.idx, a.t, b.idx, b.t);
+            return 1;
+        }
+        hits += a.idx >= 0;
+    }
+    printf("ok %ld %ld %.1f %zu\n", n_rays, hits, (double)g_tests / n_rays, s.size());
+    return 0;
+}

@@ -1,0 +1,68 @@
+"""Interleaved A/B timing of several builds of librt_pathtrace.so in ONE process.
+
+usage: python tools/ab_bench.py lib_a.so lib_b.so ... [--config c2_rtiow] [--rounds 5] [--frames 10]
+Each round times `frames` frames of every build (HIP events around each launch)
+in turn; prints per-build median/min kernel ms and Mray/s, and checks that all
+builds produce bit-identical accumulations.
+"""
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from rust_gpu_raytracing_amd import Renderer, _native as N  # noqa: E402
+from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--config", default="c2_rtiow")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--env", nargs="*", default=[])
+    args = ap.parse_args()
+    scene, bounces = build_config(args.config, width=args.width, height=args.height)
+    rays_dirs = scene.camera.recalculate_ray_directions()
+    rs = []
+    for p in args.libs:
+        lib = N.load_library(Path(p).resolve())
+        rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib))
+    for r in rs:  # warmup
+        r.compute_frame(bounces)
+        r.synchronize()
+    times = {p: [] for p in args.libs}
+    rays = {}
+    for _ in range(args.rounds):
+        for p, r in zip(args.libs, rs):
+            r.reset_timing()
+            r.reset_ray_count()
+            r.set_timing(True)
+            for _ in range(args.frames):
+                r.compute_frame(bounces)
+            r.synchronize()
+            r.set_timing(False)
+            ms, n = r.dispatch_time_total()
+            times[p].append(ms / n)
+            rays[p] = r.ray_count() / args.frames
+    ref = rs[0].read_accumulation().view(np.uint32)
+    same = [bool(np.array_equal(r.read_accumulation().view(np.uint32), ref)) for r in rs]
+    out = []
+    for (p, t), s in zip(times.items(), same):
+        med = statistics.median(t)
+        out.append({"lib": Path(p).name, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+                    "mray_s": round(rays[p] / med / 1e3, 1), "bit_identical_to_first": s})
+    print(json.dumps({"config": args.config, "bounces": bounces, "results": out}, indent=1))
+    for r in rs:
+        r.close()
+
+
+if __name__ == "__main__":
+    main()
