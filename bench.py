@@ -145,6 +145,7 @@ def main() -> int:
     barrier_sync()
     elapsed = time.perf_counter() - t0
     r.set_timing(False)
+    launch = r.launch_config()
     rays = r.ray_count()
     kern_ms, n_timed = r.dispatch_time_total()
 
@@ -206,6 +207,7 @@ def main() -> int:
                 "traffic": None,
                 "kernel": "rt_pathtrace_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
+                "launch": launch,
                 "bytes_per_launch": b_launch,
                 "note": "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction",
             },

@@ -254,6 +254,12 @@ RT_API int rt_pack_owned_accumulation(rt_ctx* ctx, void* dst_device);
 RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size,
                            uint32_t divisor);
 
+/* Launch geometry of the last rt_dispatch (diagnostics): workgroup size in
+ * threads, workgroups launched, dynamic LDS bytes per workgroup, and whether
+ * the scene was staged in LDS (1) or read from global memory (0). */
+RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
+                            uint32_t* scene_in_lds);
+
 /* The context's HIP stream (hipStream_t), for callers that want to order
  * their own device work (e.g. an RCCL collective) after a frame. */
 RT_API void* rt_stream(rt_ctx* ctx);

@@ -80,6 +80,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_render_pixels.argtypes = [ctypes.POINTER(OScene), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_set_trace_log.restype = None
+        L.oracle_set_trace_log.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_trace_log_count.restype = ctypes.c_uint64
         _lib = L
     return _lib
 

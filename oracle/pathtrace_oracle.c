@@ -400,7 +400,25 @@ static OHit check_triangles(const OScene* s, const OParams* pr, v3 o, v3 d) {   
     return best;
 }
 
+/* Optional trace log (test/analysis only): records (o, d) of every trace_ray
+ * call, for replaying real ray distributions through traversal experiments.
+ * Only meaningful with one thread. */
+static float* g_trace_log = 0;
+static uint64_t g_trace_cap = 0, g_trace_n = 0;
+
+void oracle_set_trace_log(float* buf, uint64_t cap) {
+    g_trace_log = buf;
+    g_trace_cap = cap;
+    g_trace_n = 0;
+}
+
+uint64_t oracle_trace_log_count(void) { return g_trace_n; }
+
 static inline OHit trace_ray(const OScene* s, const OParams* pr, v3 o, v3 d) {   /* :342-353 */
+    if (g_trace_log && g_trace_n < g_trace_cap) {
+        float* q = g_trace_log + 6 * g_trace_n++;
+        q[0] = o.x; q[1] = o.y; q[2] = o.z; q[3] = d.x; q[4] = d.y; q[5] = d.z;
+    }
     OHit hs = check_spheres(s, pr, o, d);
     OHit ht = check_triangles(s, pr, o, d);
     return hs.t < ht.t ? hs : ht;

@@ -115,6 +115,7 @@ SIGNATURES = {
     "rt_owned_pixel_count": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_pack_owned_accumulation": (ctypes.c_int, [_P, _P]),
     "rt_unpack_accumulation": (ctypes.c_int, [_P, _P, _U32, _U32, _U32]),
+    "rt_launch_config": (ctypes.c_int, [_P] + [ctypes.POINTER(ctypes.c_uint32)] * 4),
     "rt_stream": (_P, [_P]),
     "rt_srgb_table": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
 }
@@ -134,10 +135,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
             return _lib
         _lib = _open(Path(os.environ.get("RT_LIB") or LIB_PATH))
         return _lib
-    return _open(Path(path))
+    return _open(Path(path), strict=False)
 
 
-def _open(p: Path) -> ctypes.CDLL:
+def _open(p: Path, strict: bool = True) -> ctypes.CDLL:
     if not p.exists():
         raise NativeLibraryError(
             f"{p} not found: build the HIP extension first "
@@ -148,6 +149,8 @@ def _open(p: Path) -> ctypes.CDLL:
     except OSError as exc:  # pragma: no cover - depends on the box
         raise NativeLibraryError(f"could not load {p}: {exc}") from exc
     for name, (res, args) in SIGNATURES.items():
+        if not strict and not hasattr(lib, name):  # older experiment builds may predate an entry point
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

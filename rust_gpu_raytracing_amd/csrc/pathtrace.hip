@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "rt_device_math.h"
 #include "rt_kernel_args.h"
 
@@ -411,8 +413,8 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
-template <bool kSceneInLds>
-__global__ void __launch_bounds__(kBlockThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
+template <bool kSceneInLds, uint32_t kThreads>
+__global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
 
@@ -428,17 +430,17 @@ __global__ void __launch_bounds__(kBlockThreads, RT_WAVES_PER_EU) rt_pathtrace_k
         uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
         uint32_t* l_smat = reinterpret_cast<uint32_t*>(lds + ka.lds_smat_offset);
         float4* l_nodes = reinterpret_cast<float4*>(lds + ka.lds_nodes_offset);
-        for (uint32_t i = tid; i < ka.sphere_count; i += kBlockThreads) {
+        for (uint32_t i = tid; i < ka.sphere_count; i += kThreads) {
             l_sph[i] = ka.sphere_slots[i];
             l_orig[i] = ka.sphere_orig[i];
             l_smat[i] = ka.sphere_material[i];
         }
-        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kBlockThreads) l_nodes[i] = ka.sphere_bvh[i];
-        for (uint32_t i = tid; i < ka.material_count; i += kBlockThreads) l_mat[i] = ka.materials[i];
-        for (uint32_t i = tid; i < ka.object_count; i += kBlockThreads) l_obj[i] = ka.objects[i];
+        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
+        for (uint32_t i = tid; i < ka.material_count; i += kThreads) l_mat[i] = ka.materials[i];
+        for (uint32_t i = tid; i < ka.object_count; i += kThreads) l_obj[i] = ka.objects[i];
         sv = SceneView{l_sph, l_orig, l_smat, l_nodes, l_mat, l_obj, l_srgb};
     }
-    for (uint32_t i = tid; i < 256u; i += kBlockThreads) l_srgb[i] = ka.srgb[i];
+    for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];
     __syncthreads();
 
     const bool accumulate = ka.accumulate == 1u;
@@ -520,22 +522,54 @@ __global__ void __launch_bounds__(kBlockThreads, RT_WAVES_PER_EU) rt_pathtrace_k
     if (tid == 0 && block_rays != 0) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
 }
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t lds_bytes, uint32_t blocks,
-                               hipStream_t stream) {
-    if (scene_in_lds) {
-        hipLaunchKernelGGL(rt_pathtrace_kernel<true>, dim3(blocks), dim3(kBlockThreads), lds_bytes, stream, ka);
-    } else {
-        hipLaunchKernelGGL(rt_pathtrace_kernel<false>, dim3(blocks), dim3(kBlockThreads), lds_bytes, stream, ka);
+// Workgroup sizes the kernel is instantiated for. All waves of a workgroup
+// share one LDS copy of the scene, so the best size depends on the scene's
+// LDS footprint against the VGPR-limited waves per SIMD; the host picks the
+// size with the most resident waves (rt_pathtrace_pick_config).
+#define RT_FOR_EACH_BLOCK(X) X(256) X(320) X(384) X(512) X(640)
+
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, uint32_t threads, size_t lds_bytes,
+                               uint32_t blocks, hipStream_t stream) {
+#define RT_LAUNCH(T)                                                                                       \
+    if (threads == T) {                                                                                    \
+        if (scene_in_lds)                                                                                  \
+            hipLaunchKernelGGL((rt_pathtrace_kernel<true, T>), dim3(blocks), dim3(T), lds_bytes, stream, ka);  \
+        else                                                                                               \
+            hipLaunchKernelGGL((rt_pathtrace_kernel<false, T>), dim3(blocks), dim3(T), lds_bytes, stream, ka); \
+        return hipGetLastError();                                                                          \
     }
-    return hipGetLastError();
+    RT_FOR_EACH_BLOCK(RT_LAUNCH)
+#undef RT_LAUNCH
+    return hipErrorInvalidValue;
 }
 
-hipError_t rt_pathtrace_occupancy(bool scene_in_lds, size_t lds_bytes, int* blocks_per_cu) {
-    if (scene_in_lds)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_pathtrace_kernel<true>, kBlockThreads,
-                                                            lds_bytes);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_pathtrace_kernel<false>, kBlockThreads,
-                                                        lds_bytes);
+// Picks the workgroup size for this LDS footprint: the most resident waves
+// per CU up to kTargetWavesPerCu (measured on C2: 16 waves/CU beat 18 and 20 —
+// the per-lane BVH traversal is LDS-latency bound and more waves only add
+// contention), ties to the smaller workgroup.
+constexpr int kTargetWavesPerCu = 16;
+
+hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t* threads,
+                                    int* blocks_per_cu) {
+    int best_waves = -1;
+#define RT_OCC(T)                                                                                         \
+    {                                                                                                     \
+        int n = 0;                                                                                        \
+        hipError_t e = scene_in_lds                                                                       \
+                           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<true, T>, T, lds_bytes) \
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<false, T>, T, lds_bytes); \
+        if (e != hipSuccess) return e;                                                                    \
+        const int waves = std::min(n * (int)(T / 64), kTargetWavesPerCu);                                  \
+        if (n > 0 && (force_threads ? force_threads == T : waves > best_waves)) {                                                               \
+            best_waves = waves;                                                                           \
+            *threads = T;                                                                                 \
+            *blocks_per_cu = force_threads ? n : std::max(1, std::min(n, kTargetWavesPerCu / (int)(T / 64))); \
+        }                                                                                                 \
+    }
+    RT_FOR_EACH_BLOCK(RT_OCC)
+#undef RT_OCC
+    if (best_waves <= 0) return hipErrorInvalidConfiguration;
+    return hipSuccess;
 }
 
 // Gather support: pack the accumulation of this rank's tiles, in

@@ -21,9 +21,10 @@
 #include "rt_kernel_args.h"
 #include "sphere_bvh.h"
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, size_t lds_bytes, uint32_t blocks,
-                               hipStream_t stream);
-hipError_t rt_pathtrace_occupancy(bool scene_in_lds, size_t lds_bytes, int* blocks_per_cu);
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, uint32_t threads, size_t lds_bytes,
+                               uint32_t blocks, hipStream_t stream);
+hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t* threads,
+                                    int* blocks_per_cu);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
@@ -81,6 +82,9 @@ struct rt_ctx {
     size_t occ_lds_bytes = 0;
     bool occ_lds_scene = false;
     int occ_blocks_per_cu = 0;
+    uint32_t occ_threads = 0;
+    uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
+    uint32_t last_blocks = 0, last_lds = 0;
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
     uint32_t* d_sph_mat = nullptr;       // by original index
@@ -377,6 +381,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->n_cu = n_cu;
         const char* env = std::getenv("RT_SCENE_IN_LDS");
         ctx->force_global_scene = env && env[0] == '0';
+        env = std::getenv("RT_BLOCK_THREADS");
+        ctx->force_threads = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
         ctx->use_bvh = !(env && env[0] == '0');
     }
@@ -650,14 +656,17 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     // one wave per tile); waves then pull tiles from the queue.
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_lds_scene != scene_in_lds) {
         int per_cu = 0;
-        hipError_t oe = rt_pathtrace_occupancy(scene_in_lds, lds_bytes, &per_cu);
-        if (oe != hipSuccess) return hip_fail(ctx, "hipOccupancyMaxActiveBlocksPerMultiprocessor", oe);
-        ctx->occ_blocks_per_cu = per_cu > 0 ? per_cu : 1;
+        uint32_t threads = 0;
+        hipError_t oe = rt_pathtrace_pick_config(scene_in_lds, lds_bytes, ctx->force_threads, &threads, &per_cu);
+        if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
+        ctx->occ_blocks_per_cu = per_cu;
+        ctx->occ_threads = threads;
         ctx->occ_lds_bytes = lds_bytes;
         ctx->occ_lds_scene = scene_in_lds;
     }
+    const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
-    const uint64_t wanted = (ctx->owned_tiles + kTilesPerBlock - 1) / kTilesPerBlock;
+    const uint64_t wanted = (ctx->owned_tiles + waves_per_block - 1) / waves_per_block;
     const uint32_t blocks = (uint32_t)(wanted < resident ? wanted : resident);
     if (blocks == 0) return RT_OK;
 
@@ -674,10 +683,12 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
         }
         RT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
     }
-    hipError_t e = rt_launch_pathtrace(ka, scene_in_lds, lds_bytes, blocks, ctx->stream);
+    hipError_t e = rt_launch_pathtrace(ka, scene_in_lds, ctx->occ_threads, lds_bytes, blocks, ctx->stream);
+    ctx->last_blocks = blocks;
+    ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
     // every tile is claimed once and every wave makes one final failing claim
-    ctx->tile_base += (unsigned long long)ctx->owned_tiles + (unsigned long long)blocks * kTilesPerBlock;
+    ctx->tile_base += (unsigned long long)ctx->owned_tiles + (unsigned long long)blocks * waves_per_block;
     if (ctx->timing) {
         RT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
         ctx->pending.push_back(ev);
@@ -800,6 +811,16 @@ int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_ran
                                     ctx->height, ctx->tiles_x, owned, src_rank, world_size, (float)divisor,
                                     ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_unpack_tiles_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
+                     uint32_t* scene_in_lds) {
+    if (!ctx || !threads || !blocks || !lds_bytes || !scene_in_lds) return RT_E_INVALID;
+    *threads = ctx->occ_threads;
+    *blocks = ctx->last_blocks;
+    *lds_bytes = ctx->last_lds;
+    *scene_in_lds = ctx->occ_lds_scene ? 1u : 0u;
     return RT_OK;
 }
 

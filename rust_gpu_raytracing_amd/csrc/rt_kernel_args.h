@@ -8,8 +8,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-constexpr uint32_t kBlockThreads = 512;            // 8 waves share one LDS copy of the scene
-constexpr uint32_t kTilesPerBlock = kBlockThreads / 64;  // one 8x8 tile per wave
 
 struct RtSphere {  // src/buffers.rs:40-45, 32 B
     float position[3];

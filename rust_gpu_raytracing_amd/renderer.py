@@ -181,6 +181,12 @@ class Renderer:
     def unpack_accumulation(self, src_device_ptr: int, src_rank: int, world_size: int, divisor: int) -> None:
         self._call("rt_unpack_accumulation", ctypes.c_void_p(src_device_ptr), src_rank, world_size, divisor)
 
+    def launch_config(self) -> dict:
+        """Geometry of the last launch: workgroup threads, workgroups, LDS bytes, scene staged in LDS."""
+        v = [ctypes.c_uint32() for _ in range(4)]
+        N.check(self._ctx, self._lib.rt_launch_config(self._ctx, *[ctypes.byref(x) for x in v]), self._lib)
+        return dict(zip(("threads", "blocks", "lds_bytes", "scene_in_lds"), (x.value for x in v)))
+
     @property
     def stream_handle(self) -> int:
         return self._lib.rt_stream(self._ctx) or 0

@@ -39,6 +39,7 @@ static Res brute(const std::vector<rt_scene_sphere>& s, V o, V d) {
 }
 
 static long g_tests = 0;
+static long g_nodes = 0;
 
 static void cand(const SphereSlots& sl, uint32_t slot, V o, V d, float four_a, float two_a, float& bt, uint32_t& bo, bool& found) {
     const float* q = &sl.slot_sph[4 * slot];
@@ -66,6 +67,7 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
         V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
         uint32_t node = 0;
         while (node < n) {
+            g_nodes++;
             const SphereBvhNode& nd = sl.nodes[node];
             float tx0 = (nd.bmin[0] - m - o.x) * inv.x, tx1 = (nd.bmax[0] + m - o.x) * inv.x;
             float ty0 = (nd.bmin[1] - m - o.y) * inv.y, ty1 = (nd.bmax[1] + m - o.y) * inv.y;
@@ -83,7 +85,35 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
     return {bt, found ? (int)bo : -1};
 }
 
+static int replay(const char* rays_path, const char* sph_path) {
+    FILE* f = fopen(sph_path, "rb");
+    std::vector<rt_scene_sphere> s;
+    rt_scene_sphere sp;
+    while (fread(&sp, sizeof(sp), 1, f) == 1) s.push_back(sp);
+    fclose(f);
+    SphereSlots sl;
+    build_sphere_slots(s.data(), (uint32_t)s.size(), true, &sl);
+    f = fopen(rays_path, "rb");
+    float q[6];
+    long n = 0, bad = 0;
+    g_tests = 0;
+    while (fread(q, sizeof(q), 1, f) == 1) {
+        V o{q[0], q[1], q[2]}, d{q[3], q[4], q[5]};
+        Res a = brute(s, o, d), b = kernel_like(sl, o, d);
+        uint32_t ta, tb;
+        memcpy(&ta, &a.t, 4);
+        memcpy(&tb, &b.t, 4);
+        bad += (a.idx != b.idx || ta != tb);
+        n++;
+    }
+    fclose(f);
+    printf("replay rays %ld mismatches %ld spheres %zu always %u nodes %zu | per ray: node visits %.2f sphere tests %.2f\n",
+           n, bad, s.size(), sl.n_always, sl.nodes.size(), (double)g_nodes / n, (double)g_tests / n);
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 3 && strcmp(argv[1], "--replay") == 0) return replay(argv[2], argv[3]);
     long n_rays = argc > 1 ? atol(argv[1]) : 200000;
     unsigned seed = argc > 2 ? (unsigned)atoi(argv[2]) : 1;
     std::mt19937 rng(seed);

@@ -34,9 +34,8 @@ def test_library_exports_every_declared_symbol(native_lib):
     out = subprocess.run(["nm", "-D", "--defined-only", str(N.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
     exported = set(re.findall(r"\bT (rt_\w+)", out))
-    assert set(declared_functions()) <= exported
-    # internal launch helpers stay hidden (-fvisibility=hidden)
-    assert not any(s.startswith("rt_launch") for s in exported)
+    # exactly the declared surface: internal helpers stay hidden (-fvisibility=hidden)
+    assert set(declared_functions()) == exported
     for name in declared_functions():
         assert hasattr(native_lib, name)
 

@@ -19,6 +19,13 @@ from rust_gpu_raytracing_amd import Renderer, _native as N  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
 
+def launch_of(r):
+    try:
+        return r.launch_config()
+    except AttributeError:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
@@ -58,7 +65,8 @@ def main():
     for (p, t), s in zip(times.items(), same):
         med = statistics.median(t)
         out.append({"lib": Path(p).name, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
-                    "mray_s": round(rays[p] / med / 1e3, 1), "bit_identical_to_first": s})
+                    "mray_s": round(rays[p] / med / 1e3, 1), "bit_identical_to_first": s,
+                    "launch": launch_of(rs[list(times).index(p)])})
     print(json.dumps({"config": args.config, "bounces": bounces, "results": out}, indent=1))
     for r in rs:
         r.close()

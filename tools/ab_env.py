@@ -1,0 +1,71 @@
+"""Interleaved A/B of ONE build under different per-context environment settings.
+
+usage: python tools/ab_env.py "RT_BLOCK_THREADS=256" "RT_BLOCK_THREADS=512" ... [--config ...]
+Each spec is a space-separated list of VAR=VALUE applied while that variant's
+context is created (the runtime reads its switches at rt_create).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from rust_gpu_raytracing_amd import Renderer  # noqa: E402
+from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("specs", nargs="+")
+    ap.add_argument("--config", default="c2_rtiow")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=10)
+    args = ap.parse_args()
+    scene, bounces = build_config(args.config, width=args.width, height=args.height)
+    dirs = scene.camera.recalculate_ray_directions()
+    rs = []
+    for spec in args.specs:
+        saved = dict(os.environ)
+        for kv in spec.split():
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
+        rs.append(Renderer(scene, camera_rays=dirs))
+        os.environ.clear()
+        os.environ.update(saved)
+    for r in rs:
+        r.compute_frame(bounces)
+        r.synchronize()
+    times = {s: [] for s in args.specs}
+    rays = {}
+    for _ in range(args.rounds):
+        for s, r in zip(args.specs, rs):
+            r.reset_timing()
+            r.reset_ray_count()
+            r.set_timing(True)
+            for _ in range(args.frames):
+                r.compute_frame(bounces)
+            r.synchronize()
+            r.set_timing(False)
+            ms, n = r.dispatch_time_total()
+            times[s].append(ms / n)
+            rays[s] = r.ray_count() / args.frames
+    ref = rs[0].read_accumulation().view(np.uint32)
+    for (s, t), r in zip(times.items(), rs):
+        med = statistics.median(t)
+        print(json.dumps({"spec": s, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+                          "mray_s": round(rays[s] / med / 1e3, 1),
+                          "bit_identical_to_first": bool(np.array_equal(r.read_accumulation().view(np.uint32), ref)),
+                          "launch": r.launch_config()}))
+    for r in rs:
+        r.close()
+
+
+if __name__ == "__main__":
+    main()

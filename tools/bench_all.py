@@ -1,0 +1,81 @@
+"""Measure every BASELINE.json configuration on one GPU (+ the CPU oracle on a sample).
+
+usage: python tools/bench_all.py [--frames 10] [--configs c1_four_spheres c2_rtiow ...] [--cpu-seconds 8]
+Prints one JSON object per config: GPU Mray/s (HIP-event kernel time and wall),
+rays per frame, algorithmic HBM bytes per launch and fraction of 8 TB/s, and the
+CPU oracle's Mray/s on a tile sample of the same frame.
+C4 is the 8-GPU configuration; here it runs whole on one GPU (the per-GPU share is
+1/8 of it).
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import bench  # noqa: E402
+from rust_gpu_raytracing_amd import Renderer  # noqa: E402
+from rust_gpu_raytracing_amd.scene import CONFIGS, build_config  # noqa: E402
+
+SIZES = {  # BASELINE.json configs
+    "c1_four_spheres": (800, 600),
+    "c2_rtiow": (1920, 1080),
+    "c3_chess": (1920, 1080),
+    "c4_mixed": (3840, 2160),
+    "c5_heightfield": (1920, 1080),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", nargs="*", default=list(CONFIGS))
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    ap.add_argument("--cpu-sample-world", type=int, default=64)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    for name in args.configs:
+        w, h = SIZES[name]
+        t0 = time.perf_counter()
+        scene, bounces = build_config(name, width=w, height=h)
+        t_build = time.perf_counter() - t0
+        with Renderer(scene) as r:
+            for _ in range(args.warmup):
+                r.compute_frame(bounces)
+            r.synchronize()
+            r.reset_ray_count()
+            r.reset_timing()
+            r.set_timing(True)
+            t0 = time.perf_counter()
+            for _ in range(args.frames):
+                r.compute_frame(bounces)
+            r.synchronize()
+            wall = time.perf_counter() - t0
+            r.set_timing(False)
+            ms, n = r.dispatch_time_total()
+            rays = r.ray_count()
+            launch = r.launch_config()
+        kern_s = ms / n / 1e3
+        rpf = rays / args.frames
+        b = bench.algorithmic_bytes(w * h, rpf, bench.scene_bytes(scene))
+        res = {
+            "config": name, "width": w, "height": h, "bounces": bounces,
+            "spheres": int(scene.spheres.shape[0]), "triangles": int(scene.flatten()[2].shape[0]),
+            "gpu_mray_s": rpf / kern_s / 1e6, "gpu_mray_s_wall": rays / wall / 1e6,
+            "kernel_ms": kern_s * 1e3, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
+            "hbm_bytes_per_launch": b, "hbm_frac": b / kern_s / 8e12, "launch": launch,
+            "scene_build_s": round(t_build, 2),
+        }
+        if not args.no_cpu:
+            res["cpu"] = bench.cpu_baseline(scene, bounces, args.cpu_seconds, args.cpu_sample_world)
+            res["gpu_over_cpu"] = res["gpu_mray_s"] / res["cpu"]["value"]
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
