@@ -109,7 +109,8 @@ __device__ __forceinline__ float sphere_disc(const float4 s, f3 o, f3 d, float f
 // rounding. DESIGN.md §5.2 has the derivation.
 constexpr float kBvhMarginScale = 4.0e-3f;
 
-__device__ __forceinline__ SphereHit closest_sphere(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d) {
+__device__ __forceinline__ SphereHit closest_sphere(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d,
+                                                    float limit) {
     SphereHit best{kF32Max, 0u, 0u};
     const float a = dot(d, d);
     const float four_a = 4.0f * a;
@@ -146,8 +147,9 @@ __device__ __forceinline__ SphereHit closest_sphere(const SceneView& sv, const K
             const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
             const float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
             const float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
-            // enters the inflated box, not wholly behind the origin, not beyond the best hit
-            const bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= best.t * 1.00001f;
+            // enters the inflated box, not wholly behind the origin, not beyond the best
+            // sphere or the triangle hit (a sphere wins only when strictly closer, :347)
+            const bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= fmin_nn(best.t, limit) * 1.00001f;
             const uint32_t leaf = __float_as_uint(hi.w);
             if (hit && leaf != 0xffffffffu) {
                 const uint32_t first = leaf & 0xffffffu;
@@ -220,6 +222,93 @@ __device__ __forceinline__ void closest_triangle(const SceneView& sv, const Kern
     }
 }
 
+// Accelerated check_triangles: same candidates, same winner.
+// A BVH over the (object, sub-object) pairs of the reference's sweep culls
+// pairs whose sub-object box the ray cannot reach (boxes inflated by a per-ray
+// margin that covers the f32 rounding of the reference's slab test, :407-419);
+// each reached pair then runs the reference's own object and sub-object
+// ray_in_bounds tests and triangle tests. Among accepted triangles the winner
+// is the lexicographic minimum of (distance, position in the reference's
+// object -> sub-object -> triangle order), which is the sweep's first-wins
+// result. A NaN distance (ray lying exactly in a triangle's plane) makes the
+// sweep accept later candidates unconditionally (:457); if one is met, the lane
+// reruns the reference sweep itself.
+constexpr float kTriMarginScale = 1.0e-5f;
+
+__device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, Hit& h) {
+    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float m = kTriMarginScale * (sqrt_rn(dot(o, o)) + ka.tri_extent) + 1.0e-30f;
+    float best = kF32Max;
+    uint32_t best_seq = 0, best_tri = 0, best_obj = 0;
+    bool best_front = false, nan_hit = false;
+    const uint32_t n_nodes = ka.tri_nodes;
+    uint32_t node = 0;
+    while (node < n_nodes) {
+        const float4 lo = ka.tri_bvh[2u * node];
+        const float4 hi = ka.tri_bvh[2u * node + 1u];
+        const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
+        const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
+        const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
+        const float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
+        const float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
+        const bool hit = near_t <= far_t && far_t >= 0.0f;
+        const uint32_t leaf = __float_as_uint(hi.w);
+        if (hit && leaf != 0xffffffffu) {
+            const uint4 pr = ka.tri_prims[leaf & 0xffffffu];  // object, sub, seq_base
+            const RtObject& ob = sv.obj[pr.x];
+            const RtSubObject sub = ka.sub_objects[pr.y];
+            if (ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds) &&
+                ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) {
+                for (uint32_t j = 0; j < sub.triangle_count; ++j) {
+                    const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
+                    const uint32_t seq = pr.z + j;
+                    const RtTriangleHot& tr = ka.triangles[ti];
+                    const f3 cn = ld3(tr.calc_normal);
+                    const float det = -dot(d, cn);
+                    const float inv_det = 1.0f / det;
+                    const f3 ao = o - ld3(tr.a);
+                    const float dist = dot(ao, cn) * inv_det;
+                    const bool nan_dist = dist != dist;
+                    if (dist < 0.0f) continue;
+                    if (!nan_dist && !(dist < best || (dist == best && seq < best_seq))) continue;
+                    const f3 dao = cross(ao, d);
+                    const float v = -dot(ld3(tr.edge_ab), dao) * inv_det;
+                    if (v < 0.0f) continue;
+                    const float u = dot(ld3(tr.edge_ac), dao) * inv_det;
+                    if (u < 0.0f) continue;
+                    const float w = 1.0f - u - v;
+                    if (w < 0.0f) continue;
+                    if (nan_dist) {
+                        nan_hit = true;
+                        continue;
+                    }
+                    best = dist;
+                    best_seq = seq;
+                    best_tri = ti;
+                    best_obj = pr.x;
+                    best_front = det > 0.0f;
+                }
+            }
+        }
+        node = (hit && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
+    }
+    if (nan_hit) {  // measure-zero case: the sweep's own semantics decide
+        closest_triangle(sv, ka, o, d, h);
+        return;
+    }
+    if (best < kF32Max) {
+        const RtObject& ob = sv.obj[best_obj];
+        const f3 fn = ld3(ka.triangles[best_tri].face_normal);
+        h.front_face = best_front;
+        h.n = best_front ? fn : -fn;
+        h.t = best;
+        h.p = o + d * best;
+        h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
+        h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
+        h.material_index = ob.material_index;
+    }
+}
+
 // trace_ray, compute_shader.wgsl:342-353: sphere wins only if strictly closer.
 __device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d) {
     Hit h;
@@ -230,8 +319,14 @@ __device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& 
     h.front_face = false;
     h.u = 0.f;
     h.v = 0.f;
-    if (ka.object_count != 0) closest_triangle(sv, ka, o, d, h);
-    const SphereHit sh = closest_sphere(sv, ka, o, d);
+    if (ka.object_count != 0) {
+        if (ka.tri_accel)
+            closest_triangle_bvh(sv, ka, o, d, h);
+        else
+            closest_triangle(sv, ka, o, d, h);
+    }
+    // a sphere must be strictly closer than the triangle hit to win: prune with it
+    const SphereHit sh = closest_sphere(sv, ka, o, d, h.t);
     if (sh.t < h.t) {  // sphere wins only if strictly closer (:347); no sphere -> F32_MAX
         // sphere_hit, :530-555, and sphere_texture_coords, :557-566
         const float4 s = sv.sph[sh.slot];

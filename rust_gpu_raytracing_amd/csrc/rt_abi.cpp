@@ -95,6 +95,15 @@ struct rt_ctx {
     bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
     uint32_t n_always = 0, n_nodes = 0;
     float sphere_extent = 0.0f;
+    // triangle accelerator over (object, sub-object) pairs (sphere_bvh.h)
+    SphereBvhNode* d_tri_bvh = nullptr;
+    SubObjectPrim* d_tri_prims = nullptr;
+    size_t tri_bvh_cap = 0, tri_prims_cap = 0;
+    bool tri_dirty = true;
+    uint32_t tri_count_built = 0xffffffffu;
+    bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
+    uint32_t tri_nodes = 0;
+    float tri_extent = 0.0f;
     RtMaterial* d_mat = nullptr;
     RtObject* d_obj = nullptr;
     RtSubObject* d_sub = nullptr;
@@ -220,6 +229,38 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     ctx->sphere_extent = sl.extent;
     ctx->slots_dirty = false;
     ctx->slots_count = count;
+    return RT_OK;
+}
+
+// Rebuild the triangle accelerator for the first `object_count` objects when
+// objects or sub-objects changed (the boxes it culls with are theirs).
+int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
+    if (!ctx->use_tri_bvh || object_count == 0) return RT_OK;
+    if (!ctx->tri_dirty && ctx->tri_count_built == object_count) return RT_OK;
+    TriangleAccel acc;
+    build_triangle_accel(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(), &acc);
+    auto ensure = [&](void** p, size_t* cap, size_t bytes) -> int {
+        if (bytes <= *cap && *p) return RT_OK;
+        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (*p) RT_HIP(ctx, hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+        const size_t alloc = bytes < 256 ? 256 : bytes;
+        RT_HIP(ctx, hipMalloc(p, alloc));
+        *cap = alloc;
+        return RT_OK;
+    };
+    int rc;
+    const size_t nb = acc.nodes.size() * sizeof(SphereBvhNode), pb = acc.prims.size() * sizeof(SubObjectPrim);
+    if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_bvh), &ctx->tri_bvh_cap, nb)) ||
+        (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_prims), &ctx->tri_prims_cap, pb)) ||
+        (rc = upload_raw(ctx, ctx->d_tri_bvh, acc.nodes.data(), nb)) ||
+        (rc = upload_raw(ctx, ctx->d_tri_prims, acc.prims.data(), pb)))
+        return rc;
+    ctx->tri_nodes = (uint32_t)acc.nodes.size();
+    ctx->tri_extent = acc.extent;
+    ctx->tri_dirty = false;
+    ctx->tri_count_built = object_count;
     return RT_OK;
 }
 
@@ -383,6 +424,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->force_global_scene = env && env[0] == '0';
         env = std::getenv("RT_BLOCK_THREADS");
         ctx->force_threads = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
+        env = std::getenv("RT_TRI_BVH");
+        ctx->use_tri_bvh = !(env && env[0] == '0');
         env = std::getenv("RT_SPHERE_BVH");
         ctx->use_bvh = !(env && env[0] == '0');
     }
@@ -434,7 +477,7 @@ void rt_destroy(rt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_tile_counter, ctx->d_slot_sph,
-                    ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat,
+                    ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb};
     for (void* b : bufs)
@@ -550,6 +593,7 @@ int rt_update_object_info(rt_ctx* ctx, const rt_object_info* objects, uint32_t c
         ctx->h_obj.swap(saved);
         return rc;
     }
+    ctx->tri_dirty = true;
     return upload_raw(ctx, ctx->d_obj, objects, (size_t)count * 48);
 }
 
@@ -564,6 +608,7 @@ int rt_update_sub_object_info(rt_ctx* ctx, const rt_sub_object_info* sub_objects
         ctx->h_sub.swap(saved);
         return rc;
     }
+    ctx->tri_dirty = true;
     return upload_raw(ctx, ctx->d_sub, sub_objects, (size_t)count * 32);
 }
 
@@ -580,6 +625,8 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     {
         int rc = refresh_sphere_slots(ctx, p.sphere_count);
         if (rc) return rc;
+        rc = refresh_tri_accel(ctx, p.object_count);
+        if (rc) return rc;
     }
     KernelArgs ka{};
     ka.camera_rays = ctx->d_rays;
@@ -595,6 +642,11 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.sphere_always = ctx->n_always;
     ka.sphere_nodes = ctx->n_nodes;
     ka.sphere_extent = ctx->sphere_extent;
+    ka.tri_accel = (ctx->use_tri_bvh && p.object_count != 0) ? 1u : 0u;
+    ka.tri_nodes = ka.tri_accel ? ctx->tri_nodes : 0u;
+    ka.tri_extent = ctx->tri_extent;
+    ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
+    ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);
     ka.materials = ctx->d_mat;
     ka.objects = ctx->d_obj;
     ka.sub_objects = ctx->d_sub;

@@ -74,6 +74,8 @@ struct KernelArgs {
     const RtObject* __restrict__ objects;
     const RtSubObject* __restrict__ sub_objects;
     const RtTriangleHot* __restrict__ triangles;
+    const float4* __restrict__ tri_bvh;           // BVH over (object, sub-object) pairs, float4 pairs per node
+    const uint4* __restrict__ tri_prims;          // per leaf: object, sub-object, sweep position of its first triangle
     // textures (bindings 9, 11), RGBA8 sRGB, + decode table
     const uint32_t* __restrict__ textures;
     const uint32_t* __restrict__ env;
@@ -88,6 +90,9 @@ struct KernelArgs {
     uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
+    uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)
+    uint32_t tri_accel;       // 1: use the triangle BVH, 0: the reference's sweep
+    float tri_extent;         // max |coordinate| over sub-object boxes (margin scale)
     uint32_t compute_per_frame;
     uint32_t texture_width;
     uint32_t texture_height;

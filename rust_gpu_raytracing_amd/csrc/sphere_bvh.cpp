@@ -35,6 +35,7 @@ struct Builder {
     std::vector<Prim>& prims;
     std::vector<SphereBvhNode>& nodes;
     std::vector<uint32_t> leaf_order;
+    uint32_t leaf_max = kSphereBvhLeafMax;
 
     // Builds the subtree over prims[begin, end) at node index `at` (pre-order).
     void build(uint32_t begin, uint32_t end) {
@@ -50,7 +51,7 @@ struct Builder {
             nodes[at].bmax[k] = std::nextafter((float)box.hi[k], INFINITY);
         }
         const uint32_t n = end - begin;
-        if (n <= kSphereBvhLeafMax) {
+        if (n <= leaf_max) {
             nodes[at].leaf = (uint32_t)leaf_order.size() | (n << 24);
             for (uint32_t i = begin; i < end; i++) leaf_order.push_back(prims[i].orig);
             nodes[at].skip = (uint32_t)nodes.size();
@@ -114,6 +115,65 @@ struct Builder {
 
 }  // namespace
 
+void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, uint32_t leaf_max,
+                   std::vector<SphereBvhNode>* nodes, std::vector<uint32_t>* leaf_order) {
+    const size_t n = lo.size() / 3;
+    std::vector<Prim> prims(n);
+    for (size_t i = 0; i < n; i++) {
+        for (int k = 0; k < 3; k++) {
+            prims[i].box.lo[k] = lo[3 * i + k];
+            prims[i].box.hi[k] = hi[3 * i + k];
+            prims[i].c[k] = 0.5 * ((double)lo[3 * i + k] + (double)hi[3 * i + k]);
+        }
+        prims[i].orig = (uint32_t)i;
+    }
+    nodes->clear();
+    leaf_order->clear();
+    if (n == 0) return;
+    Builder b{prims, *nodes, {}, leaf_max};
+    b.build(0, (uint32_t)n);
+    *leaf_order = std::move(b.leaf_order);
+}
+
+void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, const rt_sub_object_info* subs,
+                          uint32_t sub_count, TriangleAccel* out) {
+    out->prims.clear();
+    out->nodes.clear();
+    out->extent = 0.0f;
+    std::vector<SubObjectPrim> prims;
+    std::vector<float> lo, hi;
+    double extent = 0.0;
+    uint32_t seq = 0;
+    for (uint32_t o = 0; o < object_count; o++) {
+        for (uint32_t i = 0; i < objects[o].sub_object_count; i++) {
+            const uint32_t si = objects[o].first_sub_object_index + i;
+            if (si >= sub_count) break;  // validated on the host; never taken
+            const rt_sub_object_info& s = subs[si];
+            const uint32_t base = seq;
+            seq += s.triangle_count;
+            if (s.triangle_count == 0) continue;
+            bool finite = true;
+            for (int k = 0; k < 3; k++) finite = finite && std::isfinite(s.min_bounds[k]) && std::isfinite(s.max_bounds[k]);
+            prims.push_back(SubObjectPrim{o, si, base, 0});
+            for (int k = 0; k < 3; k++) {
+                // the reference's slab test is symmetric in min/max (:414-415); a
+                // non-finite box can still pass it on its other axes (NaN operands
+                // are ignored), so it gets a box that every ray enters
+                const float a = finite ? std::min(s.min_bounds[k], s.max_bounds[k]) : -3.0e38f;
+                const float b = finite ? std::max(s.min_bounds[k], s.max_bounds[k]) : 3.0e38f;
+                lo.push_back(a);
+                hi.push_back(b);
+                if (finite) extent = std::max(extent, std::max(std::fabs((double)a), std::fabs((double)b)));
+            }
+        }
+    }
+    std::vector<uint32_t> order;
+    build_box_bvh(lo, hi, 1, &out->nodes, &order);
+    out->prims.reserve(order.size());
+    for (uint32_t p : order) out->prims.push_back(prims[p]);
+    out->extent = std::nextafter((float)extent, INFINITY);
+}
+
 void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, SphereSlots* out) {
     out->n_always = 0;
     out->slot_sph.clear();
@@ -170,7 +230,7 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
         out->n_always = (uint32_t)out->slot_orig.size();
         return;
     }
-    Builder b{prims, out->nodes, {}};
+    Builder b{prims, out->nodes, {}, kSphereBvhLeafMax};
     b.build(0, (uint32_t)prims.size());
     for (uint32_t orig : b.leaf_order) push_slot(orig);
     // leaf fields index the BVH part of the slot array; shift by the brute-force prefix

@@ -40,3 +40,32 @@ struct SphereSlots {
 // Build the slot layout for the first `count` spheres. With `use_bvh` false (or
 // too few spheres to pay off) every sphere is in the brute-force set.
 void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use_bvh, SphereSlots* out);
+
+// Generic builder: binned-SAH BVH over axis-aligned boxes (lo/hi, 3 floats each
+// per primitive), leaves of at most `leaf_max` primitives. Returns depth-first
+// nodes (same layout as SphereBvhNode; leaf = first | count << 24 indexing
+// `leaf_order`) and the primitive order of the leaves.
+void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, uint32_t leaf_max,
+                   std::vector<SphereBvhNode>* nodes, std::vector<uint32_t>* leaf_order);
+
+// Triangle side (check_triangles, compute_shader.wgsl:422-517). One primitive
+// per (object, sub-object) pair the reference's sweep visits, in sweep order.
+struct SubObjectPrim {
+    uint32_t object;    // object index (ray_in_bounds on its box, :431)
+    uint32_t sub;       // sub-object index (ray_in_bounds on its box, :441)
+    uint32_t seq_base;  // position of the sub-object's first triangle in the reference's sweep order
+    uint32_t _pad;
+};
+static_assert(sizeof(SubObjectPrim) == 16, "prim layout");
+
+struct TriangleAccel {
+    std::vector<SubObjectPrim> prims;  // in BVH leaf order (one prim per leaf)
+    std::vector<SphereBvhNode> nodes;
+    float extent = 0.0f;  // max |coordinate| over sub-object boxes (rounded up)
+};
+
+// Build over the first `object_count` objects. Sub-objects with no triangles
+// are left out (they can never produce a hit); non-finite boxes are kept with
+// an all-enclosing box.
+void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, const rt_sub_object_info* subs,
+                          uint32_t sub_count, TriangleAccel* out);

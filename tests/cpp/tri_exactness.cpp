@@ -1,0 +1,161 @@
+// CPU check of the triangle accelerator used by rt_pathtrace_kernel: the
+// kernel's BVH traversal logic (same f32 operation order, -ffp-contract=off)
+// must return exactly the triangle, object and distance of the reference's
+// sequential sweep (check_triangles, compute_shader.wgsl:422-517).
+// usage: tri_exactness <objects.bin> <subs.bin> <tris.bin> <rays.f32> [margin_scale]
+//   -> "ok <rays> <hits> <avg_tri_tests> <avg_nodes> <nan_fallbacks>" or the first mismatch
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "sphere_bvh.h"
+
+static const float F32_MAX_ = 3.4028235e+38f;
+struct V { float x, y, z; };
+static V sub(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static float dot(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static V cross(V a, V b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+static V ld(const float* p) { return {p[0], p[1], p[2]}; }
+
+template <typename T>
+static std::vector<T> load(const char* path) {
+    std::vector<T> v;
+    FILE* f = fopen(path, "rb");
+    if (!f) { perror(path); exit(2); }
+    T x;
+    while (fread(&x, sizeof(T), 1, f) == 1) v.push_back(x);
+    fclose(f);
+    return v;
+}
+
+static bool rib(V o, V inv, const float* mn, const float* mx) {
+    float a0 = (mn[0] - o.x) * inv.x, a1 = (mx[0] - o.x) * inv.x;
+    float b0 = (mn[1] - o.y) * inv.y, b1 = (mx[1] - o.y) * inv.y;
+    float c0 = (mn[2] - o.z) * inv.z, c1 = (mx[2] - o.z) * inv.z;
+    float n = std::fmax(std::fmax(std::fmin(a0, a1), std::fmin(b0, b1)), std::fmin(c0, c1));
+    float f = std::fmin(std::fmin(std::fmax(a0, a1), std::fmax(b0, b1)), std::fmax(c0, c1));
+    return n <= f && f >= 0.0f;
+}
+
+struct Res { float t; int tri; int obj; int front; };
+
+static long g_tests = 0, g_nodes = 0, g_nan = 0;
+
+static Res sweep(const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
+                 const std::vector<rt_scene_triangle>& tr, V o, V d) {
+    float closest = F32_MAX_;
+    Res r{F32_MAX_, -1, -1, 0};
+    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    for (size_t oi = 0; oi < ob.size(); oi++) {
+        if (!rib(o, inv, ob[oi].min_bounds, ob[oi].max_bounds)) continue;
+        for (uint32_t i = 0; i < ob[oi].sub_object_count; i++) {
+            const rt_sub_object_info& s = sb[ob[oi].first_sub_object_index + i];
+            if (!rib(o, inv, s.min_bounds, s.max_bounds)) continue;
+            for (uint32_t j = 0; j < s.triangle_count; j++) {
+                const rt_scene_triangle& t = tr[s.first_triangle_index + j];
+                V cn = ld(t.calc_normal);
+                float det = -dot(d, cn), inv_det = 1.0f / det;
+                V ao = sub(o, ld(t.a));
+                float dist = dot(ao, cn) * inv_det;
+                if (dist < 0.0f || dist >= closest) continue;
+                V dao = cross(ao, d);
+                float v = -dot(ld(t.edge_ab), dao) * inv_det;
+                if (v < 0.0f) continue;
+                float u = dot(ld(t.edge_ac), dao) * inv_det;
+                if (u < 0.0f) continue;
+                float w = 1.0f - u - v;
+                if (w < 0.0f) continue;
+                closest = dist;
+                r = {dist, (int)(s.first_triangle_index + j), (int)oi, det > 0.0f};
+            }
+        }
+    }
+    return r;
+}
+
+static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
+                 const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
+    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    float m = scale * (std::sqrt(dot(o, o)) + A.extent) + 1.0e-30f;
+    float best = F32_MAX_;
+    uint32_t best_seq = 0;
+    Res r{F32_MAX_, -1, -1, 0};
+    bool nan_hit = false;
+    uint32_t node = 0, n = (uint32_t)A.nodes.size();
+    while (node < n) {
+        g_nodes++;
+        const SphereBvhNode& nd = A.nodes[node];
+        float tx0 = (nd.bmin[0] - m - o.x) * inv.x, tx1 = (nd.bmax[0] + m - o.x) * inv.x;
+        float ty0 = (nd.bmin[1] - m - o.y) * inv.y, ty1 = (nd.bmax[1] + m - o.y) * inv.y;
+        float tz0 = (nd.bmin[2] - m - o.z) * inv.z, tz1 = (nd.bmax[2] + m - o.z) * inv.z;
+        float nt = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmin(tz0, tz1));
+        float ft = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmax(tz0, tz1));
+        bool hit = nt <= ft && ft >= 0.0f;
+        if (hit && nd.leaf != kSphereBvhInternal) {
+            const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
+            const rt_object_info& OB = ob[p.object];
+            const rt_sub_object_info& s = sb[p.sub];
+            if (rib(o, inv, OB.min_bounds, OB.max_bounds) && rib(o, inv, s.min_bounds, s.max_bounds)) {
+                for (uint32_t j = 0; j < s.triangle_count; j++) {
+                    g_tests++;
+                    uint32_t ti = s.first_triangle_index + j, seq = p.seq_base + j;
+                    const rt_scene_triangle& t = tr[ti];
+                    V cn = ld(t.calc_normal);
+                    float det = -dot(d, cn), inv_det = 1.0f / det;
+                    V ao = sub(o, ld(t.a));
+                    float dist = dot(ao, cn) * inv_det;
+                    bool nan_dist = dist != dist;
+                    if (dist < 0.0f) continue;
+                    if (!nan_dist && !(dist < best || (dist == best && seq < best_seq))) continue;
+                    V dao = cross(ao, d);
+                    float v = -dot(ld(t.edge_ab), dao) * inv_det;
+                    if (v < 0.0f) continue;
+                    float u = dot(ld(t.edge_ac), dao) * inv_det;
+                    if (u < 0.0f) continue;
+                    float w = 1.0f - u - v;
+                    if (w < 0.0f) continue;
+                    if (nan_dist) { nan_hit = true; continue; }
+                    best = dist;
+                    best_seq = seq;
+                    r = {dist, (int)ti, (int)p.object, det > 0.0f};
+                }
+            }
+        }
+        node = (hit && nd.leaf == kSphereBvhInternal) ? node + 1 : nd.skip;
+    }
+    if (nan_hit) {
+        g_nan++;
+        return sweep(ob, sb, tr, o, d);
+    }
+    return r;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 5) return 2;
+    auto ob = load<rt_object_info>(argv[1]);
+    auto sb = load<rt_sub_object_info>(argv[2]);
+    auto tr = load<rt_scene_triangle>(argv[3]);
+    auto rays = load<float>(argv[4]);
+    float scale = argc > 5 ? (float)atof(argv[5]) : 1.0e-5f;
+    TriangleAccel A;
+    build_triangle_accel(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), &A);
+    long n = (long)rays.size() / 6, hits = 0;
+    for (long i = 0; i < n; i++) {
+        V o = ld(&rays[6 * i]), d = ld(&rays[6 * i + 3]);
+        Res a = sweep(ob, sb, tr, o, d), b = accel(A, ob, sb, tr, o, d, scale);
+        uint32_t ta, tb;
+        memcpy(&ta, &a.t, 4);
+        memcpy(&tb, &b.t, 4);
+        if (ta != tb || a.tri != b.tri || a.obj != b.obj || a.front != b.front) {
+            printf("MISMATCH ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n", i, o.x,
+                   o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, b.obj, b.tri, b.t);
+            return 1;
+        }
+        hits += a.tri >= 0;
+    }
+    printf("ok %ld %ld %.2f %.2f %ld\n", n, hits, (double)g_tests / n, (double)g_nodes / n, g_nan);
+    return 0;
+}

@@ -51,6 +51,8 @@ def test_gpu_matches_golden(gpu, name):
     ("c1_four_spheres", 200, 152, 4, {}),
     ("c2_rtiow", 320, 180, 2, {}),
     ("c3_chess", 320, 184, 2, dict(env_size=(2048, 1024))),
+    ("c4_mixed", 256, 144, 2, dict(env_size=(1024, 512))),
+    ("c5_heightfield", 192, 112, 2, dict(nx=160, nz=80)),
 ])
 def test_gpu_matches_oracle_full_frame(gpu, oracle_lib, config, w, h, frames, kw):
     scene, bounces = build_config(config, width=w, height=h, **kw)
@@ -59,7 +61,7 @@ def test_gpu_matches_oracle_full_frame(gpu, oracle_lib, config, w, h, frames, kw
     assert_same(acc, out, rays, acc_o, out_o, rays_o)
 
 
-@pytest.mark.parametrize("config", ["c2_rtiow", "c3_chess"])
+@pytest.mark.parametrize("config", ["c2_rtiow", "c3_chess", "c5_heightfield"])
 def test_gpu_full_size_sampled(gpu, oracle_lib, config):
     """BASELINE size (1920x1080, 8 bounces): every GPU pixel of 2 frames is checked on a
     random sample of 3000 pixels against the oracle (the oracle is too slow for the whole frame)."""
@@ -68,7 +70,7 @@ def test_gpu_full_size_sampled(gpu, oracle_lib, config):
     acc, out, _ = gpu_render(scene, bounces, 2, rays=rays)
     o = oracle_lib.Oracle(scene, camera_rays=rays)
     rng = np.random.default_rng(11)
-    pix = rng.choice(1920 * 1080, 3000, replace=False).astype(np.uint32)
+    pix = rng.choice(1920 * 1080, 300 if config == "c5_heightfield" else 3000, replace=False).astype(np.uint32)
     a = None
     for k in (1, 2):
         a, o_out, _ = o.render_pixels(scene.params(accumulation_index=k), bounces, pix, accum_in=a)
