@@ -260,6 +260,12 @@ RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t 
 RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
                             uint32_t* scene_in_lds);
 
+/* Diagnostic counters (filled only by builds compiled with -DRT_DIAG, zeros
+ * otherwise): out[0..n) receives up to 8 u64 — [0] wave-cycles in the frame
+ * loop, [1] in triangle traversal, [2] in sphere traversal, [3] loop
+ * iterations — summed over all waves since the last rt_reset_ray_count. */
+RT_API int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
+
 /* The context's HIP stream (hipStream_t), for callers that want to order
  * their own device work (e.g. an RCCL collective) after a frame. */
 RT_API void* rt_stream(rt_ctx* ctx);

@@ -309,8 +309,26 @@ __device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const 
     }
 }
 
+#ifdef RT_DIAG
+// Diagnostic build only: wave-level cycle stamps (s_memtime) accumulated per
+// wave and added to ka.diag at exit. Never compiled into the product build.
+struct DiagAcc {
+    unsigned long long tri = 0, sph = 0;
+};
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define RT_DIAG_ARG , DiagAcc& dg
+#define RT_DIAG_PASS , dg
+#else
+#define RT_DIAG_ARG
+#define RT_DIAG_PASS
+#endif
+
 // trace_ray, compute_shader.wgsl:342-353: sphere wins only if strictly closer.
-__device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d) {
+__device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d RT_DIAG_ARG) {
     Hit h;
     h.t = kF32Max;
     h.p = mk(0.f, 0.f, 0.f);
@@ -319,14 +337,25 @@ __device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& 
     h.front_face = false;
     h.u = 0.f;
     h.v = 0.f;
+#ifdef RT_DIAG
+    const unsigned long long t0 = stamp();
+#endif
     if (ka.object_count != 0) {
         if (ka.tri_accel)
             closest_triangle_bvh(sv, ka, o, d, h);
         else
             closest_triangle(sv, ka, o, d, h);
     }
+#ifdef RT_DIAG
+    const unsigned long long t1 = stamp();
+#endif
     // a sphere must be strictly closer than the triangle hit to win: prune with it
     const SphereHit sh = closest_sphere(sv, ka, o, d, h.t);
+#ifdef RT_DIAG
+    const unsigned long long t2 = stamp();
+    dg.tri += t1 - t0;
+    dg.sph += t2 - t1;
+#endif
     if (sh.t < h.t) {  // sphere wins only if strictly closer (:347); no sphere -> F32_MAX
         // sphere_hit, :530-555, and sphere_texture_coords, :557-566
         const float4 s = sv.sph[sh.slot];
@@ -388,9 +417,10 @@ __device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t inde
 
 // One iteration of the bounce loop, :226-311. Returns true when the path is
 // finished (escaped to the environment, or the bounce limit is reached).
-__device__ __forceinline__ bool path_step(const SceneView& sv, const KernelArgs& ka, Path& p, uint32_t& rays) {
+__device__ __forceinline__ bool path_step(const SceneView& sv, const KernelArgs& ka, Path& p,
+                                          uint32_t& rays RT_DIAG_ARG) {
     if (p.bounce >= ka.bounces) return true;
-    const Hit h = trace_ray(sv, ka, p.o, p.d);
+    const Hit h = trace_ray(sv, ka, p.o, p.d RT_DIAG_PASS);
     ++rays;
     if (h.t == kF32Max) {
         const f4 c = sample_env(ka, sv.srgb, p.d);
@@ -552,7 +582,15 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 
     uint32_t tile = claim_tile(ka);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
+#ifdef RT_DIAG
+    DiagAcc dg;
+    unsigned long long iters = 0;
+    const unsigned long long t_start = stamp();
+#endif
     while (true) {
+#ifdef RT_DIAG
+        ++iters;
+#endif
         // Refill: idle lanes take the next pixels, in slot order.
         while (true) {
             const uint64_t need = __ballot(!active);
@@ -582,7 +620,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             }
         }
         if (__ballot(active) == 0) break;
-        if (active && path_step(sv, ka, p, rays)) {
+        if (active && path_step(sv, ka, p, rays RT_DIAG_PASS)) {
             sample += 1;
             if (accumulate) {  // pixel_color += per_pixel(...), :161
                 pix.x = pix.x + p.light.x;
@@ -612,6 +650,14 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             }
         }
     }
+#ifdef RT_DIAG
+    if ((threadIdx.x & 63u) == 0) {
+        atomicAdd(ka.diag + 0, stamp() - t_start);
+        atomicAdd(ka.diag + 1, dg.tri);
+        atomicAdd(ka.diag + 2, dg.sph);
+        atomicAdd(ka.diag + 3, iters);
+    }
+#endif
     atomicAdd(&block_rays, rays);
     __syncthreads();
     if (tid == 0 && block_rays != 0) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
@@ -642,10 +688,11 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, uint32_t
 // per CU up to kTargetWavesPerCu (measured on C2: 16 waves/CU beat 18 and 20 —
 // the per-lane BVH traversal is LDS-latency bound and more waves only add
 // contention), ties to the smaller workgroup.
-constexpr int kTargetWavesPerCu = 16;
+constexpr int kDefaultWavesPerCu = 16;
 
-hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t* threads,
-                                    int* blocks_per_cu) {
+hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
+                                    uint32_t* threads, int* blocks_per_cu) {
+    const int kTargetWavesPerCu = waves_cap ? (int)waves_cap : kDefaultWavesPerCu;
     int best_waves = -1;
 #define RT_OCC(T)                                                                                         \
     {                                                                                                     \

@@ -23,8 +23,8 @@
 
 hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, uint32_t threads, size_t lds_bytes,
                                uint32_t blocks, hipStream_t stream);
-hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t* threads,
-                                    int* blocks_per_cu);
+hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
+                                    uint32_t* threads, int* blocks_per_cu);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
@@ -84,6 +84,7 @@ struct rt_ctx {
     int occ_blocks_per_cu = 0;
     uint32_t occ_threads = 0;
     uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
+    uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
     uint32_t last_blocks = 0, last_lds = 0;
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
@@ -424,6 +425,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->force_global_scene = env && env[0] == '0';
         env = std::getenv("RT_BLOCK_THREADS");
         ctx->force_threads = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
+        env = std::getenv("RT_WAVES_PER_CU");
+        ctx->waves_cap = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_TRI_BVH");
         ctx->use_tri_bvh = !(env && env[0] == '0');
         env = std::getenv("RT_SPHERE_BVH");
@@ -441,7 +444,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
     ctx->k = 1;  // src/renderer.rs:96
 
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
-        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9)) ||
         (rc = dev_alloc(ctx, &ctx->d_tile_counter, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_slot_sph, info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, info->sphere_count)) ||
@@ -633,6 +636,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.accum = ctx->d_accum;
     ka.output = ctx->d_out;
     ka.ray_counter = ctx->d_counter;
+    ka.diag = ctx->d_counter + 1;
     ka.tile_counter = ctx->d_tile_counter;
     ka.tile_base = ctx->tile_base;
     ka.sphere_slots = ctx->d_slot_sph;
@@ -709,7 +713,8 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_lds_scene != scene_in_lds) {
         int per_cu = 0;
         uint32_t threads = 0;
-        hipError_t oe = rt_pathtrace_pick_config(scene_in_lds, lds_bytes, ctx->force_threads, &threads, &per_cu);
+        hipError_t oe =
+            rt_pathtrace_pick_config(scene_in_lds, lds_bytes, ctx->force_threads, ctx->waves_cap, &threads, &per_cu);
         if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
         ctx->occ_blocks_per_cu = per_cu;
         ctx->occ_threads = threads;
@@ -791,7 +796,7 @@ int rt_ray_count(rt_ctx* ctx, uint64_t* out) {
 
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, sizeof(unsigned long long), ctx->stream));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, 9 * sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }
 
@@ -863,6 +868,16 @@ int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_ran
                                     ctx->height, ctx->tiles_x, owned, src_rank, world_size, (float)divisor,
                                     ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_unpack_tiles_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n) {
+    RT_ENTER(ctx);
+    if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    unsigned long long v[8] = {};
+    RT_HIP(ctx, hipMemcpyAsync(v, ctx->d_counter + 1, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t i = 0; i < n && i < 8; i++) out[i] = v[i];
     return RT_OK;
 }
 

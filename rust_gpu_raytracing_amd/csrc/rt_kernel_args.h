@@ -63,6 +63,7 @@ struct KernelArgs {
     float4* __restrict__ accum;
     uint32_t* __restrict__ output;
     unsigned long long* __restrict__ ray_counter;
+    unsigned long long* __restrict__ diag;          // 8 diagnostic counters (RT_DIAG builds)
     unsigned long long* __restrict__ tile_counter;  // monotonically increasing tile queue head
     unsigned long long tile_base;                   // its value at launch start
     // scene (bindings 3, 4, 5, 7, 8, 10)

@@ -181,6 +181,12 @@ class Renderer:
     def unpack_accumulation(self, src_device_ptr: int, src_rank: int, world_size: int, divisor: int) -> None:
         self._call("rt_unpack_accumulation", ctypes.c_void_p(src_device_ptr), src_rank, world_size, divisor)
 
+    def debug_counters(self) -> list:
+        """RT_DIAG builds only: [frame-loop, triangle, sphere wave-cycles, loop iterations]."""
+        v = (ctypes.c_uint64 * 8)()
+        N.check(self._ctx, self._lib.rt_debug_counters(self._ctx, v, 8), self._lib)
+        return list(v)
+
     def launch_config(self) -> dict:
         """Geometry of the last launch: workgroup threads, workgroups, LDS bytes, scene staged in LDS."""
         v = [ctypes.c_uint32() for _ in range(4)]

@@ -38,11 +38,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--cpu-sample-world", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kw", default="{}", help="JSON builder kwargs applied to every config, e.g. '{\"env_size\": [1024, 512]}'")
+    ap.add_argument("--size", default=None, help="WxH override")
     args = ap.parse_args()
     for name in args.configs:
-        w, h = SIZES[name]
+        w, h = SIZES[name] if args.size is None else map(int, args.size.split("x"))
         t0 = time.perf_counter()
-        scene, bounces = build_config(name, width=w, height=h)
+        scene, bounces = build_config(name, width=w, height=h, **json.loads(args.kw))
         t_build = time.perf_counter() - t0
         with Renderer(scene) as r:
             for _ in range(args.warmup):

@@ -1,0 +1,34 @@
+"""Time split of the frame loop from an RT_DIAG build (in-kernel s_memtime stamps).
+
+usage: RT_LIB=build/ab/lib_diag.so python tools/diag_split.py [config ...]
+Reports, summed over waves, the share of wave-cycles spent in triangle and
+sphere traversal; the rest is shading, RNG, refill and framebuffer I/O.
+Stamps serialise the wave around each trace: read shares, not absolute times.
+"""
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from rust_gpu_raytracing_amd import Renderer  # noqa: E402
+from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
+
+SIZES = {"c1_four_spheres": (800, 600), "c2_rtiow": (1920, 1080), "c3_chess": (1920, 1080),
+         "c4_mixed": (1920, 1080), "c5_heightfield": (1920, 1080)}
+
+for name in sys.argv[1:] or list(SIZES):
+    w, h = SIZES[name]
+    scene, bounces = build_config(name, width=w, height=h)
+    with Renderer(scene) as r:
+        r.compute_frame(bounces)
+        r.synchronize()
+        r.reset_ray_count()
+        for _ in range(3):
+            r.compute_frame(bounces)
+        c = r.debug_counters()
+        rays = r.ray_count()
+    total, tri, sph, it = c[:4]
+    print(json.dumps({"config": name, "tri_share": tri / total, "sphere_share": sph / total,
+                      "other_share": 1 - (tri + sph) / total, "cycles_per_ray": total / rays,
+                      "loop_iters_per_ray": it / rays}))
