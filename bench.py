@@ -105,10 +105,18 @@ def main() -> int:
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     assert torch.cuda.is_available(), "bench.py needs a HIP device"
-    torch.cuda.set_device(local_rank)
+    # RT_BENCH_ONE_DEVICE=1 + RT_DIST_BACKEND=gloo: rehearse the N-rank path with
+    # every rank on GPU 0 (single-GPU test boxes); the real run is one rank per GPU
+    # over RCCL (backend "nccl").
+    device = 0 if os.environ.get("RT_BENCH_ONE_DEVICE") == "1" else local_rank
+    backend = os.environ.get("RT_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     from rust_gpu_raytracing_amd import Renderer
     from rust_gpu_raytracing_amd import build as native_build
@@ -121,7 +129,7 @@ def main() -> int:
 
     scene, default_bounces = build_config(args.config, width=args.width, height=args.height)
     bounces = args.bounces or default_bounces
-    r = Renderer(scene, device=local_rank, rank=rank, world_size=world)
+    r = Renderer(scene, device=device, rank=rank, world_size=world)
     owned_px = r.owned_pixel_count()
 
     def barrier_sync():
@@ -149,7 +157,8 @@ def main() -> int:
     rays = r.ray_count()
     kern_ms, n_timed = r.dispatch_time_total()
 
-    stats = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
+    stats = torch.tensor([elapsed, float(rays)], dtype=torch.float64,
+                         device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         t_max = stats[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -168,6 +177,16 @@ def main() -> int:
         gather_accumulation(r, dst=0)
         barrier_sync()
         gather_ms = (time.perf_counter() - g0) * 1e3
+        if os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
+            # the assembled tile-split image must equal a 1-GPU render of the same frames
+            with Renderer(scene, device=device) as ref:
+                for _ in range(args.warmup + args.steps):
+                    ref.compute_frame(bounces)
+                same = np.array_equal(ref.read_accumulation().view(np.uint32), r.read_accumulation().view(np.uint32))
+                same = same and np.array_equal(ref.read_output(), r.read_output())
+            log(f"gather verify: assembled image {'==' if same else '!='} 1-GPU render")
+            if not same:
+                return 3
 
     if rank == 0:
         avg_kernel_s = kern_ms / max(n_timed, 1) / 1e3

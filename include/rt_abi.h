@@ -255,8 +255,9 @@ RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t 
                            uint32_t divisor);
 
 /* Launch geometry of the last rt_dispatch (diagnostics): workgroup size in
- * threads, workgroups launched, dynamic LDS bytes per workgroup, and whether
- * the scene was staged in LDS (1) or read from global memory (0). */
+ * threads, workgroups launched, dynamic LDS bytes per workgroup, and the LDS
+ * staging mode (0: scene in global memory, 1: spheres/materials/objects/sphere
+ * BVH staged in LDS, 2: also the triangle accelerator). */
 RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
                             uint32_t* scene_in_lds);
 

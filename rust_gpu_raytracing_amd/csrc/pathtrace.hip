@@ -51,6 +51,8 @@ struct SceneView {
     const RtMaterial* mat;    // LDS
     const RtObject* obj;      // LDS
     const float* srgb;        // LDS, 256 entries
+    const float4* tri_nodes;  // triangle accelerator nodes (LDS in mode 2, else global)
+    const uint4* tri_prims;   // triangle accelerator leaves: object, sub-object, sweep position
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -244,8 +246,8 @@ __device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const 
     const uint32_t n_nodes = ka.tri_nodes;
     uint32_t node = 0;
     while (node < n_nodes) {
-        const float4 lo = ka.tri_bvh[2u * node];
-        const float4 hi = ka.tri_bvh[2u * node + 1u];
+        const float4 lo = sv.tri_nodes[2u * node];
+        const float4 hi = sv.tri_nodes[2u * node + 1u];
         const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
         const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
         const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
@@ -254,7 +256,7 @@ __device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const 
         const bool hit = near_t <= far_t && far_t >= 0.0f;
         const uint32_t leaf = __float_as_uint(hi.w);
         if (hit && leaf != 0xffffffffu) {
-            const uint4 pr = ka.tri_prims[leaf & 0xffffffu];  // object, sub, seq_base
+            const uint4 pr = sv.tri_prims[leaf & 0xffffffu];  // object, sub, seq_base
             const RtObject& ob = sv.obj[pr.x];
             const RtSubObject sub = ka.sub_objects[pr.y];
             if (ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds) &&
@@ -381,7 +383,11 @@ __device__ __forceinline__ f4 sample_texture(const KernelArgs& ka, const float* 
     const int y = texel_coord(v * (float)(int32_t)ka.texture_height, ka.tex_h);
     const uint32_t l = min(layer, ka.tex_layers - 1u);
     const size_t off = ((size_t)l * ka.tex_h + (size_t)y) * ka.tex_w + (size_t)x;
+#ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
+    return decode_texel(0xff8040c0u ^ (uint32_t)off, srgb);
+#else
     return decode_texel(ka.textures[off], srgb);
+#endif
 }
 
 __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb, f3 d) {
@@ -390,7 +396,11 @@ __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb
     const float v = 0.5f + asinf_c(d.y) / kWgslPi;
     const int x = texel_coord(u * (float)(int32_t)ka.env_map_width, ka.env_w);
     const int y = texel_coord(v * (float)(int32_t)ka.env_map_height, ka.env_h);
+#ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
+    return decode_texel(0xffc0a080u ^ (uint32_t)(y * ka.env_w + x), srgb);
+#else
     return decode_texel(ka.env[(size_t)y * ka.env_w + (size_t)x], srgb);
+#endif
 }
 
 // State of one path of per_pixel (compute_shader.wgsl:210-314) between bounces.
@@ -404,7 +414,12 @@ struct Path {
 // per_pixel prologue, :212-222.
 __device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t index, uint32_t random_index, Path& p) {
     p.o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
+#ifdef RT_EXP_NO_FB  // timing experiment only: results are wrong
+    const float4 cr = make_float4(ka.camera_origin[0] * 0.0f + 0.1f * (float)(index & 255u) / 255.0f - 0.05f,
+                                  (float)(index % ka.width) * 1e-4f - 0.02f, -1.0f, 0.0f);
+#else
     const float4 cr = ka.camera_rays[index];
+#endif
     p.d = mk(cr.x, cr.y, cr.z);
     p.seed = index * random_index * 326624u;
     const float rx = random01(p.seed), ry = random01(p.seed), rz = random01(p.seed);
@@ -524,9 +539,12 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
 //   uint32   slot -> original index[sphere_count]
 //   uint32   sphere material[sphere_count] (by original index)
 //   float4x2 sphere BVH nodes[sphere_nodes]
+//   float4x2 triangle accelerator nodes[tri_nodes]      (mode 2)
+//   uint4    triangle accelerator leaves[tri_prims]     (mode 2)
 //   float    srgb[256]
-// kSceneInLds = false keeps the scene in global memory (for scenes beyond the
-// LDS budget); the sRGB table is always staged.
+// kMode 0 keeps the scene in global memory (scenes beyond the LDS budget),
+// 1 stages spheres/materials/objects/sphere BVH, 2 also the triangle
+// accelerator; the sRGB table is always staged.
 //
 // Persistent waves with in-wave path regeneration (the "ray compaction across
 // bounces"): each wave claims 8x8 tiles from a device-wide queue and keeps all
@@ -538,7 +556,7 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
-template <bool kSceneInLds, uint32_t kThreads>
+template <int kMode, uint32_t kThreads>
 __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
@@ -546,9 +564,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     const uint32_t tid = threadIdx.x;
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, ka.objects,
-                 l_srgb};
+                 l_srgb,          ka.tri_bvh,     ka.tri_prims};
     if (tid == 0) block_rays = 0;
-    if constexpr (kSceneInLds) {
+    if constexpr (kMode >= 1) {
         float4* l_sph = reinterpret_cast<float4*>(lds);
         RtMaterial* l_mat = reinterpret_cast<RtMaterial*>(lds + ka.lds_mat_offset);
         RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
@@ -563,7 +581,20 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
         for (uint32_t i = tid; i < ka.material_count; i += kThreads) l_mat[i] = ka.materials[i];
         for (uint32_t i = tid; i < ka.object_count; i += kThreads) l_obj[i] = ka.objects[i];
-        sv = SceneView{l_sph, l_orig, l_smat, l_nodes, l_mat, l_obj, l_srgb};
+        sv.sph = l_sph;
+        sv.orig = l_orig;
+        sv.sph_mat = l_smat;
+        sv.nodes = l_nodes;
+        sv.mat = l_mat;
+        sv.obj = l_obj;
+    }
+    if constexpr (kMode == 2) {
+        float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
+        uint4* l_tp = reinterpret_cast<uint4*>(lds + ka.lds_tri_prims_offset);
+        for (uint32_t i = tid; i < 2u * ka.tri_nodes; i += kThreads) l_tn[i] = ka.tri_bvh[i];
+        for (uint32_t i = tid; i < ka.tri_prim_count; i += kThreads) l_tp[i] = ka.tri_prims[i];
+        sv.tri_nodes = l_tn;
+        sv.tri_prims = l_tp;
     }
     for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];
     __syncthreads();
@@ -608,7 +639,11 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                         index = y * ka.width + x;  // :148
                         sample = 0;
                         active = true;
+#ifndef RT_EXP_NO_FB
                         if (accumulate) pix = ka.accum[index];  // :156
+#else
+                        pix = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
                         start_sample(ka, index, ka.accumulation_index, p);
                     }
                 }
@@ -663,52 +698,62 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     if (tid == 0 && block_rays != 0) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
 }
 
-// Workgroup sizes the kernel is instantiated for. All waves of a workgroup
-// share one LDS copy of the scene, so the best size depends on the scene's
-// LDS footprint against the VGPR-limited waves per SIMD; the host picks the
-// size with the most resident waves (rt_pathtrace_pick_config).
-#define RT_FOR_EACH_BLOCK(X) X(256) X(320) X(384) X(512) X(640)
+// Instantiations: LDS mode x workgroup size. All waves of a workgroup share
+// one LDS copy of the scene, so the best size depends on the scene's LDS
+// footprint against the VGPR-limited waves per SIMD; the host picks the size
+// with the most resident waves up to a cap (rt_pathtrace_pick_config).
+#define RT_FOR_EACH_CONFIG(X) \
+    X(0, 256) X(0, 512) X(0, 1024) X(1, 256) X(1, 512) X(1, 1024) X(2, 256) X(2, 512) X(2, 1024)
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, uint32_t threads, size_t lds_bytes,
-                               uint32_t blocks, hipStream_t stream) {
-#define RT_LAUNCH(T)                                                                                       \
-    if (threads == T) {                                                                                    \
-        if (scene_in_lds)                                                                                  \
-            hipLaunchKernelGGL((rt_pathtrace_kernel<true, T>), dim3(blocks), dim3(T), lds_bytes, stream, ka);  \
-        else                                                                                               \
-            hipLaunchKernelGGL((rt_pathtrace_kernel<false, T>), dim3(blocks), dim3(T), lds_bytes, stream, ka); \
-        return hipGetLastError();                                                                          \
+namespace {
+// Dynamic LDS above 64 KiB must be opted into per kernel.
+hipError_t allow_big_lds(const void* fn) {
+    int dev = 0, max_optin = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&max_optin, hipDeviceAttributeSharedMemPerBlockOptin, dev);
+    if (e != hipSuccess || max_optin <= 0) return hipSuccess;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, max_optin - 256);
+}
+}  // namespace
+
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, uint32_t threads, size_t lds_bytes, uint32_t blocks,
+                               hipStream_t stream) {
+#define RT_LAUNCH(M, T)                                                                                    \
+    if (mode == M && threads == T) {                                                                      \
+        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T>), dim3(blocks), dim3(T), lds_bytes, stream, ka);    \
+        return hipGetLastError();                                                                         \
     }
-    RT_FOR_EACH_BLOCK(RT_LAUNCH)
+    RT_FOR_EACH_CONFIG(RT_LAUNCH)
 #undef RT_LAUNCH
     return hipErrorInvalidValue;
 }
 
-// Picks the workgroup size for this LDS footprint: the most resident waves
-// per CU up to kTargetWavesPerCu (measured on C2: 16 waves/CU beat 18 and 20 —
-// the per-lane BVH traversal is LDS-latency bound and more waves only add
-// contention), ties to the smaller workgroup.
+// Picks the workgroup size for this LDS mode and footprint: the most resident
+// waves per CU up to kTargetWavesPerCu (measured on C2: 16 waves/CU beat 18
+// and 20 — the per-lane BVH traversal is LDS-latency bound and more waves only
+// add contention), ties to the smaller workgroup.
 constexpr int kDefaultWavesPerCu = 16;
 
-hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
+hipError_t rt_pathtrace_pick_config(int mode, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
                                     uint32_t* threads, int* blocks_per_cu) {
     const int kTargetWavesPerCu = waves_cap ? (int)waves_cap : kDefaultWavesPerCu;
     int best_waves = -1;
-#define RT_OCC(T)                                                                                         \
-    {                                                                                                     \
+#define RT_OCC(M, T)                                                                                      \
+    if (mode == M) {                                                                                      \
         int n = 0;                                                                                        \
-        hipError_t e = scene_in_lds                                                                       \
-                           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<true, T>, T, lds_bytes) \
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<false, T>, T, lds_bytes); \
+        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T>));         \
         if (e != hipSuccess) return e;                                                                    \
-        const int waves = std::min(n * (int)(T / 64), kTargetWavesPerCu);                                  \
-        if (n > 0 && (force_threads ? force_threads == T : waves > best_waves)) {                                                               \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T>, T, lds_bytes);    \
+        if (e != hipSuccess) return e;                                                                    \
+        const int waves = std::min(n * (int)(T / 64), kTargetWavesPerCu);                                 \
+        if (n > 0 && (force_threads ? force_threads == T : waves > best_waves)) {                         \
             best_waves = waves;                                                                           \
             *threads = T;                                                                                 \
             *blocks_per_cu = force_threads ? n : std::max(1, std::min(n, kTargetWavesPerCu / (int)(T / 64))); \
         }                                                                                                 \
     }
-    RT_FOR_EACH_BLOCK(RT_OCC)
+    RT_FOR_EACH_CONFIG(RT_OCC)
 #undef RT_OCC
     if (best_waves <= 0) return hipErrorInvalidConfiguration;
     return hipSuccess;

@@ -21,9 +21,9 @@
 #include "rt_kernel_args.h"
 #include "sphere_bvh.h"
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, bool scene_in_lds, uint32_t threads, size_t lds_bytes,
-                               uint32_t blocks, hipStream_t stream);
-hipError_t rt_pathtrace_pick_config(bool scene_in_lds, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, uint32_t threads, size_t lds_bytes, uint32_t blocks,
+                               hipStream_t stream);
+hipError_t rt_pathtrace_pick_config(int mode, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
                                     uint32_t* threads, int* blocks_per_cu);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
@@ -45,7 +45,8 @@ static_assert(sizeof(rt_sub_object_info) == sizeof(RtSubObject), "sub-object rec
 
 namespace {
 
-constexpr size_t kLdsSceneBudget = 64 * 1024;  // dynamic LDS the scene may take per workgroup
+constexpr size_t kLdsSceneBudget = 64 * 1024;    // mode 1: spheres/materials/objects/sphere BVH per workgroup
+constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerator (one 1024-thread workgroup per CU)
 
 thread_local std::string g_create_error;
 
@@ -80,7 +81,8 @@ struct rt_ctx {
     int n_cu = 0;
     bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
     size_t occ_lds_bytes = 0;
-    bool occ_lds_scene = false;
+    int occ_mode = -1;
+    int max_lds_mode = 2;               // RT_LDS_MODE (A/B switch): highest staging mode allowed
     int occ_blocks_per_cu = 0;
     uint32_t occ_threads = 0;
     uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
@@ -94,6 +96,7 @@ struct rt_ctx {
     bool slots_dirty = true;
     uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
     bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
+    uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
     uint32_t n_always = 0, n_nodes = 0;
     float sphere_extent = 0.0f;
     // triangle accelerator over (object, sub-object) pairs (sphere_bvh.h)
@@ -103,7 +106,7 @@ struct rt_ctx {
     bool tri_dirty = true;
     uint32_t tri_count_built = 0xffffffffu;
     bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
-    uint32_t tri_nodes = 0;
+    uint32_t tri_nodes = 0, tri_prim_count = 0;
     float tri_extent = 0.0f;
     RtMaterial* d_mat = nullptr;
     RtObject* d_obj = nullptr;
@@ -216,7 +219,7 @@ int upload_spheres(rt_ctx* ctx, const rt_scene_sphere* s, uint32_t n) {
 int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     if (!ctx->slots_dirty && ctx->slots_count == count) return RT_OK;
     SphereSlots sl;
-    build_sphere_slots(ctx->h_sph.data(), count, ctx->use_bvh, &sl);
+    build_sphere_slots(ctx->h_sph.data(), count, ctx->use_bvh, &sl, ctx->sphere_leaf_max);
     std::vector<uint32_t> mat(count);
     for (uint32_t i = 0; i < count; i++) mat[i] = ctx->h_sph[i].material_index;
     int rc;
@@ -259,6 +262,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         (rc = upload_raw(ctx, ctx->d_tri_prims, acc.prims.data(), pb)))
         return rc;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
+    ctx->tri_prim_count = (uint32_t)acc.prims.size();
     ctx->tri_extent = acc.extent;
     ctx->tri_dirty = false;
     ctx->tri_count_built = object_count;
@@ -423,12 +427,16 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->n_cu = n_cu;
         const char* env = std::getenv("RT_SCENE_IN_LDS");
         ctx->force_global_scene = env && env[0] == '0';
+        env = std::getenv("RT_LDS_MODE");
+        if (env) ctx->max_lds_mode = (int)std::strtol(env, nullptr, 10);
         env = std::getenv("RT_BLOCK_THREADS");
         ctx->force_threads = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_WAVES_PER_CU");
         ctx->waves_cap = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_TRI_BVH");
         ctx->use_tri_bvh = !(env && env[0] == '0');
+        env = std::getenv("RT_SPHERE_LEAF");
+        ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
         ctx->use_bvh = !(env && env[0] == '0');
     }
@@ -648,6 +656,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.sphere_extent = ctx->sphere_extent;
     ka.tri_accel = (ctx->use_tri_bvh && p.object_count != 0) ? 1u : 0u;
     ka.tri_nodes = ka.tri_accel ? ctx->tri_nodes : 0u;
+    ka.tri_prim_count = ka.tri_accel ? ctx->tri_prim_count : 0u;
     ka.tri_extent = ctx->tri_extent;
     ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
     ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);
@@ -699,27 +708,42 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     off = al16(off + (size_t)p.sphere_count * 4);
     ka.lds_nodes_offset = (uint32_t)off;
     off = al16(off + (size_t)ctx->n_nodes * sizeof(SphereBvhNode));
-    const bool scene_in_lds = off + 1024 <= kLdsSceneBudget && !ctx->force_global_scene;
+    const size_t mode1_bytes = off + 1024;
+    ka.lds_tri_nodes_offset = (uint32_t)off;
+    off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
+    ka.lds_tri_prims_offset = (uint32_t)off;
+    off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
+    const size_t mode2_bytes = off + 1024;
+    int mode = 0;
+    if (!ctx->force_global_scene) {
+        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes <= kLdsAccelBudget && ctx->max_lds_mode >= 2)
+            mode = 2;
+        else if (mode1_bytes <= kLdsSceneBudget && ctx->max_lds_mode >= 1)
+            mode = 1;
+    }
     size_t lds_bytes;
-    if (scene_in_lds) {
-        ka.lds_srgb_offset = (uint32_t)off;
-        lds_bytes = off + 1024;
+    if (mode == 2) {
+        ka.lds_srgb_offset = (uint32_t)(mode2_bytes - 1024);
+        lds_bytes = mode2_bytes;
+    } else if (mode == 1) {
+        ka.lds_srgb_offset = (uint32_t)(mode1_bytes - 1024);
+        lds_bytes = mode1_bytes;
     } else {
         ka.lds_srgb_offset = 0;
         lds_bytes = 1024;
     }
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
-    if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_lds_scene != scene_in_lds) {
+    if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode) {
         int per_cu = 0;
         uint32_t threads = 0;
         hipError_t oe =
-            rt_pathtrace_pick_config(scene_in_lds, lds_bytes, ctx->force_threads, ctx->waves_cap, &threads, &per_cu);
+            rt_pathtrace_pick_config(mode, lds_bytes, ctx->force_threads, ctx->waves_cap, &threads, &per_cu);
         if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
         ctx->occ_blocks_per_cu = per_cu;
         ctx->occ_threads = threads;
         ctx->occ_lds_bytes = lds_bytes;
-        ctx->occ_lds_scene = scene_in_lds;
+        ctx->occ_mode = mode;
     }
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
@@ -740,7 +764,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
         }
         RT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
     }
-    hipError_t e = rt_launch_pathtrace(ka, scene_in_lds, ctx->occ_threads, lds_bytes, blocks, ctx->stream);
+    hipError_t e = rt_launch_pathtrace(ka, mode, ctx->occ_threads, lds_bytes, blocks, ctx->stream);
     ctx->last_blocks = blocks;
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
@@ -887,7 +911,7 @@ int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uin
     *threads = ctx->occ_threads;
     *blocks = ctx->last_blocks;
     *lds_bytes = ctx->last_lds;
-    *scene_in_lds = ctx->occ_lds_scene ? 1u : 0u;
+    *scene_in_lds = ctx->occ_mode < 0 ? 0u : (uint32_t)ctx->occ_mode;
     return RT_OK;
 }
 

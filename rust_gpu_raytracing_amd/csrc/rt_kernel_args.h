@@ -92,6 +92,7 @@ struct KernelArgs {
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)
+    uint32_t tri_prim_count;  // triangle BVH leaves
     uint32_t tri_accel;       // 1: use the triangle BVH, 0: the reference's sweep
     float tri_extent;         // max |coordinate| over sub-object boxes (margin scale)
     uint32_t compute_per_frame;
@@ -118,5 +119,7 @@ struct KernelArgs {
     uint32_t lds_orig_offset;
     uint32_t lds_smat_offset;
     uint32_t lds_nodes_offset;
+    uint32_t lds_tri_nodes_offset;
+    uint32_t lds_tri_prims_offset;
     uint32_t lds_srgb_offset;
 };

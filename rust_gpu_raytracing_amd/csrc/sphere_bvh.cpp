@@ -174,7 +174,7 @@ void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, 
     out->extent = std::nextafter((float)extent, INFINITY);
 }
 
-void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, SphereSlots* out) {
+void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, SphereSlots* out, uint32_t leaf_max) {
     out->n_always = 0;
     out->slot_sph.clear();
     out->slot_orig.clear();
@@ -230,7 +230,7 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
         out->n_always = (uint32_t)out->slot_orig.size();
         return;
     }
-    Builder b{prims, out->nodes, {}, kSphereBvhLeafMax};
+    Builder b{prims, out->nodes, {}, leaf_max ? leaf_max : kSphereBvhLeafMax};
     b.build(0, (uint32_t)prims.size());
     for (uint32_t orig : b.leaf_order) push_slot(orig);
     // leaf fields index the BVH part of the slot array; shift by the brute-force prefix

@@ -39,7 +39,8 @@ struct SphereSlots {
 
 // Build the slot layout for the first `count` spheres. With `use_bvh` false (or
 // too few spheres to pay off) every sphere is in the brute-force set.
-void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use_bvh, SphereSlots* out);
+void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use_bvh, SphereSlots* out,
+                        uint32_t leaf_max = kSphereBvhLeafMax);
 
 // Generic builder: binned-SAH BVH over axis-aligned boxes (lo/hi, 3 floats each
 // per primitive), leaves of at most `leaf_max` primitives. Returns depth-first

@@ -72,11 +72,14 @@ def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0
     if packed.shape[0] < cap:
         pad = torch.zeros((cap - packed.shape[0], 4), dtype=packed.dtype, device=packed.device)
         packed = torch.cat([packed, pad])
+    device = packed.device
+    if dist.get_backend() == "gloo" and packed.is_cuda:  # gloo moves host tensors only
+        packed = packed.cpu()
     bufs = [torch.empty_like(packed) for _ in range(world_size)] if rank == dst else None
     dist.gather(packed, gather_list=bufs, dst=dst)
     if rank != dst:
         return None
-    return [b[: owned_tiles(n_tiles, r, world_size).shape[0] * 64] for r, b in enumerate(bufs)]
+    return [b[: owned_tiles(n_tiles, r, world_size).shape[0] * 64].to(device) for r, b in enumerate(bufs)]
 
 
 def gather_accumulation(renderer, dst: int = 0):
