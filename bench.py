@@ -8,10 +8,18 @@ are resident in HBM before timing; the timed region holds exactly `--steps`
 frames bracketed by barrier + device synchronize.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-the fixed 1920x1080 image is tile-split across ranks (8x8 tile t -> rank t % N,
-SURVEY §8e), so total work is fixed ("scaling": "strong"). No collective runs in
-the timed loop; one RCCL gather of the accumulated RGBA32F tiles to rank 0 runs
-afterwards and is reported separately as gather_ms.
+the 1920x1080 image is tile-split across ranks (8x8 tile t -> rank t % N,
+SURVEY §8e). Default "--scaling weak": one step advances the progressive render
+by N frames (N samples per pixel), each rank rendering its 1/N of the tiles for
+all N frames in one fused launch (rt_compute_frames) -- per-GPU work per step is
+one frame's worth at every N, and the image is bit-identical to N sequential
+1-GPU frames. "--scaling strong": one frame per step split N ways. No collective
+runs in the timed loop; one RCCL gather of the accumulated RGBA32F tiles to rank
+0 runs afterwards and is reported separately as gather_ms.
+
+roofline.traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
+(profiles/pmc_traffic.json, FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE), when
+it was measured on this workload; null otherwise.
 
 Prints ONE JSON line on rank 0.
 """
@@ -49,6 +57,19 @@ def scene_bytes(scene) -> int:
     return int(scene.spheres.nbytes + scene.materials.nbytes + objs.nbytes + subs.nbytes + tris.shape[0] * 80)
 
 
+def pmc_traffic(workload: str):
+    """HBM bytes per launch measured by rocprofv3 PMC for this workload (tools/profile.sh ->
+    profiles/pmc_traffic.json), or None when no committed measurement matches."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None, None
+    d = json.loads(f.read_text())
+    e = d.get(workload)
+    if not e:
+        return None, None
+    return float(e["fetch_bytes_x2"] + e["write_bytes"]), e.get("source")
+
+
 def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
     """The CPU oracle (scalar C restatement, OpenMP over the host cores) on a bounded
     sample of the same workload: the tiles t % sample_world == 0, frames k = 1, 2, ...
@@ -68,7 +89,7 @@ def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
         p = scene.params(accumulation_index=frames)
         rays += o.render_frame(p, bounces, accum, out, rank=0, world_size=sample_world, threads=threads)
         el = time.perf_counter() - t0
-        if el >= min_seconds or frames >= 64:
+        if el >= min_seconds or frames >= 512:
             break
     return {
         "value": rays / el / 1e6,
@@ -94,6 +115,9 @@ def main() -> int:
     ap.add_argument("--cpu-sample-world", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="N>1: weak = N frames per step (1/N of the tiles each, per-GPU work fixed); "
+                         "strong = one frame per step split N ways")
     args = ap.parse_args()
 
     import torch
@@ -131,6 +155,13 @@ def main() -> int:
     bounces = args.bounces or default_bounces
     r = Renderer(scene, device=device, rank=rank, world_size=world)
     owned_px = r.owned_pixel_count()
+    frames_per_step = world if args.scaling == "weak" else 1
+
+    def step():
+        if frames_per_step == 1:
+            r.compute_frame(bounces)
+        else:
+            r.compute_frames(bounces, frames_per_step)
 
     def barrier_sync():
         r.synchronize()
@@ -139,7 +170,7 @@ def main() -> int:
             dist.barrier()
 
     for _ in range(args.warmup):
-        r.compute_frame(bounces)
+        step()
     barrier_sync()
     r.reset_ray_count()
     r.reset_timing()
@@ -147,7 +178,7 @@ def main() -> int:
     barrier_sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        r.compute_frame(bounces)
+        step()
         if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
             log(f"step {i + 1}/{args.steps}")
     barrier_sync()
@@ -180,7 +211,7 @@ def main() -> int:
         if os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
             # the assembled tile-split image must equal a 1-GPU render of the same frames
             with Renderer(scene, device=device) as ref:
-                for _ in range(args.warmup + args.steps):
+                for _ in range(frames_per_step * (args.warmup + args.steps)):
                     ref.compute_frame(bounces)
                 same = np.array_equal(ref.read_accumulation().view(np.uint32), r.read_accumulation().view(np.uint32))
                 same = same and np.array_equal(ref.read_output(), r.read_output())
@@ -191,8 +222,12 @@ def main() -> int:
     if rank == 0:
         avg_kernel_s = kern_ms / max(n_timed, 1) / 1e3
         rays_per_launch = rays / max(args.steps, 1)
+        # one launch reads/writes each owned pixel's framebuffer words once, whatever its frame count
         b_launch = algorithmic_bytes(owned_px, rays_per_launch, scene_bytes(scene))
         achieved = b_launch / avg_kernel_s / 1e9
+        workload = (f"{args.config} {args.width}x{args.height}, {bounces} bounces, 1 spp/frame, "
+                    f"{frames_per_step} frame(s) per step, accumulate")
+        traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
         result = {
             "metric": METRIC,
             "value": rays_total / elapsed_max / 1e6,
@@ -202,20 +237,21 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if args.scaling == "weak" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.config} {args.width}x{args.height}, {bounces} bounces, 1 spp/frame, accumulate",
+                "workload": workload,
                 "width": args.width,
                 "height": args.height,
                 "bounces": bounces,
                 "spheres": int(scene.spheres.shape[0]),
                 "triangles": int(scene.flatten()[2].shape[0]),
                 "parallelism": f"tile{world}" if world > 1 else "single",
+                "frames_per_step": frames_per_step,
                 "rays_per_step": rays_total / args.steps,
-                "nominal_rays_per_step": args.width * args.height * bounces,
+                "nominal_rays_per_step": args.width * args.height * bounces * frames_per_step,
             },
             "roofline": {
                 "bound": "hbm",
@@ -223,7 +259,8 @@ def main() -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "rt_pathtrace_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "launch": launch,

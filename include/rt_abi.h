@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -194,6 +194,14 @@ RT_API int rt_reset_accumulation(rt_ctx* ctx, const rt_params* params);
  * `count` must not exceed the capacity given at rt_create. */
 RT_API int rt_update_ray_directions(rt_ctx* ctx, const rt_ray* rays, uint32_t count);
 RT_API int rt_update_camera(rt_ctx* ctx, const rt_ray_camera* camera);
+
+/* Device-side primary rays: instead of reading camera_rays,
+ * the kernel computes each pixel's direction with the per-pixel arithmetic of
+ * Camera::recalculate_ray_directions (src/camera.rs:139-182) from the camera's
+ * inverse projection and inverse view (column-major 4x4 f32, glam layout), in
+ * f32 with glam's operation order -- the same bits the host generator would
+ * upload. Stays in effect until the next rt_update_ray_directions. */
+RT_API int rt_update_camera_matrices(rt_ctx* ctx, const float inverse_projection[16], const float inverse_view[16]);
 RT_API int rt_update_spheres(rt_ctx* ctx, const rt_scene_sphere* spheres, uint32_t count);
 RT_API int rt_update_triangles(rt_ctx* ctx, const rt_scene_triangle* triangles, uint32_t count);
 RT_API int rt_update_object_info(rt_ctx* ctx, const rt_object_info* objects, uint32_t count);
@@ -210,6 +218,15 @@ RT_API int rt_dispatch(rt_ctx* ctx, uint32_t bounces);
  * is 1, write Params with accumulation_index = k and then k += 1; then
  * rt_dispatch. Asynchronous. */
 RT_API int rt_compute_frame(rt_ctx* ctx, uint32_t bounces);
+
+/* `frames` consecutive rt_compute_frame calls fused into one launch: each
+ * pixel runs its frames back to back on one lane, so the accumulation, the
+ * packed output and the ray count afterwards are exactly those of the
+ * sequence of calls (the per-frame outputs in between are never observable:
+ * the reference only reads output_data after a frame, src/renderer.rs:254).
+ * Used by the multi-GPU bench, where each rank advances its tiles by N frames
+ * per step. frames >= 1. Asynchronous. */
+RT_API int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
 
 /* Blocks until all work on the context's stream has finished. */
 RT_API int rt_synchronize(rt_ctx* ctx);

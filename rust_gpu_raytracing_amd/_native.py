@@ -95,6 +95,7 @@ SIGNATURES = {
     "rt_reset_accumulation": (ctypes.c_int, [_P, ctypes.POINTER(rt_params)]),
     "rt_update_ray_directions": (ctypes.c_int, [_P, _P, _U32]),
     "rt_update_camera": (ctypes.c_int, [_P, ctypes.POINTER(rt_ray_camera)]),
+    "rt_update_camera_matrices": (ctypes.c_int, [_P, _P, _P]),
     "rt_update_spheres": (ctypes.c_int, [_P, _P, _U32]),
     "rt_update_triangles": (ctypes.c_int, [_P, _P, _U32]),
     "rt_update_object_info": (ctypes.c_int, [_P, _P, _U32]),
@@ -102,6 +103,7 @@ SIGNATURES = {
     "rt_update_materials": (ctypes.c_int, [_P, _P, _U32]),
     "rt_dispatch": (ctypes.c_int, [_P, _U32]),
     "rt_compute_frame": (ctypes.c_int, [_P, _U32]),
+    "rt_compute_frames": (ctypes.c_int, [_P, _U32, _U32]),
     "rt_synchronize": (ctypes.c_int, [_P]),
     "rt_read_output": (ctypes.c_int, [_P, _P]),
     "rt_read_accumulation": (ctypes.c_int, [_P, _P]),

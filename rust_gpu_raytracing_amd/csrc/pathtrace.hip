@@ -77,7 +77,7 @@ __device__ __forceinline__ f4 decode_texel(uint32_t texel, const float* srgb) {
 // (t, index) over spheres with disc >= 0 and t > 0. Here spheres are visited
 // in slot order (brute-force set, then BVH leaves), so acceptance compares
 // (t, original index) lexicographically, which yields the same sphere in any
-// visiting order. `c_orig` starts at 0 so that t == F32_MAX is never taken.
+// visiting order. `orig` starts at 0 so that t == F32_MAX is never taken.
 struct SphereHit {
     float t;
     uint32_t orig;
@@ -104,68 +104,45 @@ __device__ __forceinline__ float sphere_disc(const float4 s, f3 o, f3 d, float f
     return b * b - four_a * c;
 }
 
+// Tests the aligned group of 4 slots starting at `slot` (sphere_bvh.h: padded
+// with NaN spheres that no ray hits). All loads are issued together and the
+// four tests are independent, so the group costs one LDS round trip.
+__device__ __forceinline__ void test_sphere_group(const SceneView& sv, uint32_t slot, f3 o, f3 d, float four_a,
+                                                  float two_a, SphereHit& best) {
+    const float4 s0 = sv.sph[slot], s1 = sv.sph[slot + 1u], s2 = sv.sph[slot + 2u], s3 = sv.sph[slot + 3u];
+    const uint4 og = *reinterpret_cast<const uint4*>(sv.orig + slot);
+    float b[4], disc[4];
+    disc[0] = sphere_disc(s0, o, d, four_a, b[0]);
+    disc[1] = sphere_disc(s1, o, d, four_a, b[1]);
+    disc[2] = sphere_disc(s2, o, d, four_a, b[2]);
+    disc[3] = sphere_disc(s3, o, d, four_a, b[3]);
+    // any(disc[k] >= 0): max of the four (NaN operands ignored, as `NaN >= 0` is false)
+    if (fmax_nn(fmax_nn(disc[0], disc[1]), fmax_nn(disc[2], disc[3])) >= 0.0f) {
+        sphere_candidate(disc[0], b[0], two_a, og.x, slot, best);
+        sphere_candidate(disc[1], b[1], two_a, og.y, slot + 1u, best);
+        sphere_candidate(disc[2], b[2], two_a, og.z, slot + 2u, best);
+        sphere_candidate(disc[3], b[3], two_a, og.w, slot + 3u, best);
+    }
+}
+
 // Box inflation per unit of (|o| + extent): covers both the f32 rounding of the
 // discriminant (a float disc >= 0 implies the ray line passes within
 // sqrt(r^2 + 32u|o-C|^2) of the centre, u = 2^-24) and of the near root
 // (|t_f - t| <= ~1.4e-3 |o-C| / |d|), with slack for the slab test's own
 // rounding. DESIGN.md §5.2 has the derivation.
 constexpr float kBvhMarginScale = 4.0e-3f;
+// Triangle side: covers the f32 rounding of the reference's slab test.
+constexpr float kTriMarginScale = 1.0e-5f;
 
-__device__ __forceinline__ SphereHit closest_sphere(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d,
-                                                    float limit) {
-    SphereHit best{kF32Max, 0u, 0u};
-    const float a = dot(d, d);
-    const float four_a = 4.0f * a;
-    const float two_a = 2.0f * a;
-    // brute-force set: wave-uniform sweep, 4 at a time, one exec-masked branch per group
-    const uint32_t n_always = ka.sphere_always;
-    uint32_t i = 0;
-    for (; i + 4u <= n_always; i += 4u) {
-        float b[4], disc[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) disc[k] = sphere_disc(sv.sph[i + k], o, d, four_a, b[k]);
-        // any(disc[k] >= 0): max of the four (NaN operands ignored, as `NaN >= 0` is false)
-        if (fmax_nn(fmax_nn(disc[0], disc[1]), fmax_nn(disc[2], disc[3])) >= 0.0f) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) sphere_candidate(disc[k], b[k], two_a, sv.orig[i + k], i + k, best);
-        }
-    }
-    for (; i < n_always; ++i) {
-        float b;
-        const float disc = sphere_disc(sv.sph[i], o, d, four_a, b);
-        sphere_candidate(disc, b, two_a, sv.orig[i], i, best);
-    }
-    // BVH set: per-lane stackless traversal over depth-first nodes with skip links
-    const uint32_t n_nodes = ka.sphere_nodes;
-    if (n_nodes != 0) {
-        const float m = kBvhMarginScale * (sqrt_rn(dot(o, o)) + ka.sphere_extent) + 1.0e-6f;
-        const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        uint32_t node = 0;
-        while (node < n_nodes) {
-            const float4 lo = sv.nodes[2u * node];
-            const float4 hi = sv.nodes[2u * node + 1u];
-            const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
-            const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
-            const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
-            const float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
-            const float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
-            // enters the inflated box, not wholly behind the origin, not beyond the best
-            // sphere or the triangle hit (a sphere wins only when strictly closer, :347)
-            const bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= fmin_nn(best.t, limit) * 1.00001f;
-            const uint32_t leaf = __float_as_uint(hi.w);
-            if (hit && leaf != 0xffffffffu) {
-                const uint32_t first = leaf & 0xffffffu;
-                const uint32_t cnt = leaf >> 24;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    float b;
-                    const float disc = sphere_disc(sv.sph[first + k], o, d, four_a, b);
-                    sphere_candidate(disc, b, two_a, sv.orig[first + k], first + k, best);
-                }
-            }
-            node = (hit && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
-        }
-    }
-    return best;
+// Slab test of a BVH node box inflated by m on every side (culling only: the
+// margins make it conservative).
+__device__ __forceinline__ void node_slabs(const float4 lo, const float4 hi, f3 o, f3 inv, float m, float& near_t,
+                                           float& far_t) {
+    const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
+    const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
+    const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
+    near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
+    far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
 }
 
 // ray_in_bounds, compute_shader.wgsl:407-419.
@@ -178,9 +155,20 @@ __device__ __forceinline__ bool ray_in_bounds(f3 o, f3 inv, const float* mn, con
     return near_t <= far_t && far_t >= 0.0f;
 }
 
-// check_triangles, compute_shader.wgsl:422-517. Updates `h` when a triangle
-// is closer than `closest` (which starts at F32_MAX, independent of spheres).
-__device__ __forceinline__ void closest_triangle(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, Hit& h) {
+// Closest triangle found so far: distance, position in the reference's sweep
+// order (tie-break), triangle and object index, facing.
+struct TriHit {
+    float t;
+    uint32_t seq, tri, obj;
+    bool front;
+};
+
+// check_triangles, compute_shader.wgsl:422-517: the reference's own sweep over
+// objects -> sub-objects -> triangles (first wins on equal distance, `>=`
+// rejects, :457). Used when the accelerator is off, and as the fallback for
+// the measure-zero NaN-distance case.
+__device__ __forceinline__ TriHit sweep_triangles(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d) {
+    TriHit th{kF32Max, 0u, 0u, 0u, false};
     float closest = kF32Max;
     const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const uint32_t n_obj = ka.object_count;
@@ -209,58 +197,89 @@ __device__ __forceinline__ void closest_triangle(const SceneView& sv, const Kern
                 if (u < 0.0f) continue;
                 const float w = 1.0f - u - v;
                 if (w < 0.0f) continue;
-                const f3 fn = ld3(tr.face_normal);
-                h.front_face = det > 0.0f;
-                h.n = h.front_face ? fn : -fn;
                 closest = dist;
-                h.t = dist;
-                h.p = o + d * dist;
-                // object_texture_coords, :568-578 (uv from the OBJECT bounds)
-                h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
-                h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
-                h.material_index = ob.material_index;
+                th.t = dist;
+                th.tri = ti;
+                th.obj = oi;
+                th.front = det > 0.0f;
             }
         }
     }
+    return th;
 }
 
-// Accelerated check_triangles: same candidates, same winner.
-// A BVH over the (object, sub-object) pairs of the reference's sweep culls
-// pairs whose sub-object box the ray cannot reach (boxes inflated by a per-ray
-// margin that covers the f32 rounding of the reference's slab test, :407-419);
-// each reached pair then runs the reference's own object and sub-object
-// ray_in_bounds tests and triangle tests. Among accepted triangles the winner
-// is the lexicographic minimum of (distance, position in the reference's
-// object -> sub-object -> triangle order), which is the sweep's first-wins
-// result. A NaN distance (ray lying exactly in a triangle's plane) makes the
-// sweep accept later candidates unconditionally (:457); if one is met, the lane
-// reruns the reference sweep itself.
-constexpr float kTriMarginScale = 1.0e-5f;
+// One ray's closest-hit search, resumable one BVH node at a time so that a
+// wave can interleave it with other lanes' shading (see the kernel).
+//
+// Phase 0 walks the triangle accelerator: a BVH over the
+// (object, sub-object) pairs of the reference's sweep; each reached pair runs
+// the reference's own object and sub-object ray_in_bounds tests and triangle
+// tests, and the winner is the lexicographic minimum of (distance, sweep
+// position) — the sweep's first-wins result. A NaN distance (ray lying
+// exactly in a triangle's plane) makes the sweep accept later candidates
+// unconditionally (:457); if one is met, the lane reruns the sweep itself.
+// Phase 1 walks the sphere BVH, pruned by the best sphere and
+// the triangle hit (a sphere wins only when strictly closer, :347).
+// Phase 2: done.
+struct TraceState {
+    f3 inv;
+    float a4, a2;     // 4*dot(d,d), 2*dot(d,d) (:372-379)
+    float m;          // box inflation of the current phase's BVH
+    uint32_t node;
+    uint32_t phase;
+    bool nan_hit;
+    SphereHit sph;
+    TriHit tri;
+};
 
-__device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, Hit& h) {
-    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float m = kTriMarginScale * (sqrt_rn(dot(o, o)) + ka.tri_extent) + 1.0e-30f;
-    float best = kF32Max;
-    uint32_t best_seq = 0, best_tri = 0, best_obj = 0;
-    bool best_front = false, nan_hit = false;
-    const uint32_t n_nodes = ka.tri_nodes;
-    uint32_t node = 0;
-    while (node < n_nodes) {
-        const float4 lo = sv.tri_nodes[2u * node];
-        const float4 hi = sv.tri_nodes[2u * node + 1u];
-        const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
-        const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
-        const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
-        const float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
-        const float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
+__device__ __forceinline__ float phase_margin(const KernelArgs& ka, f3 o, uint32_t phase) {
+    const float r = sqrt_rn(dot(o, o));
+    return phase == 0 ? kTriMarginScale * (r + ka.tri_extent) + 1.0e-30f
+                      : kBvhMarginScale * (r + ka.sphere_extent) + 1.0e-6f;
+}
+
+// kTris: the scene has objects (triangles); false compiles the triangle side out.
+template <bool kTris>
+__device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
+    ts.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float a = dot(d, d);
+    ts.a4 = 4.0f * a;
+    ts.a2 = 2.0f * a;
+    ts.sph = SphereHit{kF32Max, 0u, 0u};
+    ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
+    ts.nan_hit = false;
+    ts.node = 0;
+    // brute-force sphere set: wave-uniform sweep over groups of 4 (a sphere's
+    // own test is exact, so the visiting order is free)
+    for (uint32_t i = 0; i < ka.sphere_always; i += 4u) test_sphere_group(sv, i, o, d, ts.a4, ts.a2, ts.sph);
+    if constexpr (!kTris) {
+        ts.phase = 1;
+    } else if (!ka.tri_accel) {
+        ts.tri = sweep_triangles(sv, ka, o, d);
+        ts.phase = 1;
+    } else {
+        ts.phase = ka.tri_nodes != 0 ? 0u : 1u;
+    }
+    if (ts.phase == 1 && ka.sphere_nodes == 0) ts.phase = 2;
+    ts.m = phase_margin(ka, o, ts.phase);
+}
+
+// Advances the search by one BVH node (and that node's leaf, if reached).
+template <bool kTris>
+__device__ __forceinline__ void trace_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
+    if (kTris && ts.phase == 0) {
+        const float4 lo = sv.tri_nodes[2u * ts.node];
+        const float4 hi = sv.tri_nodes[2u * ts.node + 1u];
+        float near_t, far_t;
+        node_slabs(lo, hi, o, ts.inv, ts.m, near_t, far_t);
         const bool hit = near_t <= far_t && far_t >= 0.0f;
         const uint32_t leaf = __float_as_uint(hi.w);
         if (hit && leaf != 0xffffffffu) {
             const uint4 pr = sv.tri_prims[leaf & 0xffffffu];  // object, sub, seq_base
             const RtObject& ob = sv.obj[pr.x];
             const RtSubObject sub = ka.sub_objects[pr.y];
-            if (ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds) &&
-                ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) {
+            if (ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) &&
+                ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) {
                 for (uint32_t j = 0; j < sub.triangle_count; ++j) {
                     const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
                     const uint32_t seq = pr.z + j;
@@ -272,7 +291,7 @@ __device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const 
                     const float dist = dot(ao, cn) * inv_det;
                     const bool nan_dist = dist != dist;
                     if (dist < 0.0f) continue;
-                    if (!nan_dist && !(dist < best || (dist == best && seq < best_seq))) continue;
+                    if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) continue;
                     const f3 dao = cross(ao, d);
                     const float v = -dot(ld3(tr.edge_ab), dao) * inv_det;
                     if (v < 0.0f) continue;
@@ -281,56 +300,38 @@ __device__ __forceinline__ void closest_triangle_bvh(const SceneView& sv, const 
                     const float w = 1.0f - u - v;
                     if (w < 0.0f) continue;
                     if (nan_dist) {
-                        nan_hit = true;
+                        ts.nan_hit = true;
                         continue;
                     }
-                    best = dist;
-                    best_seq = seq;
-                    best_tri = ti;
-                    best_obj = pr.x;
-                    best_front = det > 0.0f;
+                    ts.tri = TriHit{dist, seq, ti, pr.x, det > 0.0f};
                 }
             }
         }
-        node = (hit && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
-    }
-    if (nan_hit) {  // measure-zero case: the sweep's own semantics decide
-        closest_triangle(sv, ka, o, d, h);
-        return;
-    }
-    if (best < kF32Max) {
-        const RtObject& ob = sv.obj[best_obj];
-        const f3 fn = ld3(ka.triangles[best_tri].face_normal);
-        h.front_face = best_front;
-        h.n = best_front ? fn : -fn;
-        h.t = best;
-        h.p = o + d * best;
-        h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
-        h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
-        h.material_index = ob.material_index;
+        ts.node = (hit && leaf == 0xffffffffu) ? ts.node + 1u : __float_as_uint(lo.w);
+        if (ts.node >= ka.tri_nodes) {
+            if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
+            ts.node = 0;
+            ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
+            ts.m = phase_margin(ka, o, 1);
+        }
+    } else {
+        const float4 lo = sv.nodes[2u * ts.node];
+        const float4 hi = sv.nodes[2u * ts.node + 1u];
+        float near_t, far_t;
+        node_slabs(lo, hi, o, ts.inv, ts.m, near_t, far_t);
+        // enters the inflated box, not wholly behind the origin, not beyond the best
+        // sphere or the triangle hit (a sphere wins only when strictly closer, :347)
+        const bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f;
+        const uint32_t leaf = __float_as_uint(hi.w);
+        if (hit && leaf != 0xffffffffu) test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
+        ts.node = (hit && leaf == 0xffffffffu) ? ts.node + 1u : __float_as_uint(lo.w);
+        if (ts.node >= ka.sphere_nodes) ts.phase = 2;
     }
 }
 
-#ifdef RT_DIAG
-// Diagnostic build only: wave-level cycle stamps (s_memtime) accumulated per
-// wave and added to ka.diag at exit. Never compiled into the product build.
-struct DiagAcc {
-    unsigned long long tri = 0, sph = 0;
-};
-__device__ __forceinline__ unsigned long long stamp() {
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-#define RT_DIAG_ARG , DiagAcc& dg
-#define RT_DIAG_PASS , dg
-#else
-#define RT_DIAG_ARG
-#define RT_DIAG_PASS
-#endif
-
-// trace_ray, compute_shader.wgsl:342-353: sphere wins only if strictly closer.
-__device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d RT_DIAG_ARG) {
+// trace_ray's result (:342-353): the sphere wins only if strictly closer.
+template <bool kTris>
+__device__ __forceinline__ Hit trace_end(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, const TraceState& ts) {
     Hit h;
     h.t = kF32Max;
     h.p = mk(0.f, 0.f, 0.f);
@@ -339,54 +340,47 @@ __device__ __forceinline__ Hit trace_ray(const SceneView& sv, const KernelArgs& 
     h.front_face = false;
     h.u = 0.f;
     h.v = 0.f;
-#ifdef RT_DIAG
-    const unsigned long long t0 = stamp();
-#endif
-    if (ka.object_count != 0) {
-        if (ka.tri_accel)
-            closest_triangle_bvh(sv, ka, o, d, h);
-        else
-            closest_triangle(sv, ka, o, d, h);
+    if (kTris && ts.tri.t != kF32Max) {  // found (the sweep can accept a NaN distance, :457)
+        const RtObject& ob = sv.obj[ts.tri.obj];
+        const f3 fn = ld3(ka.triangles[ts.tri.tri].face_normal);
+        h.front_face = ts.tri.front;
+        h.n = ts.tri.front ? fn : -fn;
+        h.t = ts.tri.t;
+        h.p = o + d * ts.tri.t;
+        // object_texture_coords, :568-578 (uv from the OBJECT bounds)
+        h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
+        h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
+        h.material_index = ob.material_index;
     }
-#ifdef RT_DIAG
-    const unsigned long long t1 = stamp();
-#endif
-    // a sphere must be strictly closer than the triangle hit to win: prune with it
-    const SphereHit sh = closest_sphere(sv, ka, o, d, h.t);
-#ifdef RT_DIAG
-    const unsigned long long t2 = stamp();
-    dg.tri += t1 - t0;
-    dg.sph += t2 - t1;
-#endif
-    if (sh.t < h.t) {  // sphere wins only if strictly closer (:347); no sphere -> F32_MAX
+    if (ts.sph.t < h.t) {  // no sphere -> F32_MAX
         // sphere_hit, :530-555, and sphere_texture_coords, :557-566
-        const float4 s = sv.sph[sh.slot];
-        const float ts = sh.t;
-        const f3 p = o + d * ts;
+        const float4 s = sv.sph[ts.sph.slot];
+        const float t = ts.sph.t;
+        const f3 p = o + d * t;
         const f3 outward = normalize(p - ld3(s));
         const float theta = acosf_c(-outward.y);
         const float phi = atan2f_c(-outward.z, outward.x) + kWgslPi;
-        h.t = ts;
+        h.t = t;
         h.p = p;
         h.u = phi / kTwoPiWgsl;
         h.v = theta / kWgslPi;
         h.front_face = dot(d, outward) < 0.0f;
         h.n = h.front_face ? outward : -outward;
-        h.material_index = sv.sph_mat[sh.orig];
+        h.material_index = sv.sph_mat[ts.sph.orig];
     }
     return h;
 }
 
-__device__ __forceinline__ f4 sample_texture(const KernelArgs& ka, const float* srgb, uint32_t layer, float u,
-                                             float v) {
+// sample_texture, compute_shader.wgsl:26-32: the raw RGBA8 texel (decoded later).
+__device__ __forceinline__ uint32_t fetch_texture(const KernelArgs& ka, uint32_t layer, float u, float v) {
     const int x = texel_coord(u * (float)(int32_t)ka.texture_width, ka.tex_w);
     const int y = texel_coord(v * (float)(int32_t)ka.texture_height, ka.tex_h);
     const uint32_t l = min(layer, ka.tex_layers - 1u);
     const size_t off = ((size_t)l * ka.tex_h + (size_t)y) * ka.tex_w + (size_t)x;
 #ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
-    return decode_texel(0xff8040c0u ^ (uint32_t)off, srgb);
+    return 0xff8040c0u ^ (uint32_t)off;
 #else
-    return decode_texel(ka.textures[off], srgb);
+    return ka.textures[off];
 #endif
 }
 
@@ -411,16 +405,44 @@ struct Path {
     uint32_t bounce;
 };
 
-// per_pixel prologue, :212-222.
-__device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t index, uint32_t random_index, Path& p) {
+// Camera::recalculate_ray_directions (src/camera.rs:139-182) for one pixel, in
+// f32 with glam's operation order (Mat4 * Vec4 = ((c0*x + c1*y) + c2*z) + c3*w,
+// Vec3A::normalize = v * (1/length)): bit-identical to the host generator
+// (rust_gpu_raytracing_amd/camera.py) given the same matrices.
+__device__ __forceinline__ f3 mat4_mul_xyz(const float* m, float x, float y, float z, float w, float& out_w) {
+    const float r0 = ((m[0] * x + m[4] * y) + m[8] * z) + m[12] * w;
+    const float r1 = ((m[1] * x + m[5] * y) + m[9] * z) + m[13] * w;
+    const float r2 = ((m[2] * x + m[6] * y) + m[10] * z) + m[14] * w;
+    out_w = ((m[3] * x + m[7] * y) + m[11] * z) + m[15] * w;
+    return mk(r0, r1, r2);
+}
+
+// `cam` is the LDS camera block: inverse projection [16], inverse view [16], aspect.
+__device__ __forceinline__ f3 camera_ray(const KernelArgs& ka, const float* cam, uint32_t x, uint32_t y) {
+    const float xc = (float)x / (float)ka.width;
+    const float yc = (float)y / (float)ka.height;
+    const float nx = xc * 2.0f - 1.0f;
+    const float ny = yc * 2.0f - 1.0f;
+    const float ax = nx * cam[32];
+    float tw;
+    const f3 t = mat4_mul_xyz(cam, ax, ny, 1.0f, 1.0f, tw);
+    const f3 ws = normalize(mk(t.x / tw, t.y / tw, t.z / tw));
+    float unused;
+    return mat4_mul_xyz(cam + 16, ws.x, ws.y, ws.z, 0.0f, unused);
+}
+
+__device__ __forceinline__ f3 pixel_ray(const KernelArgs& ka, const float* cam, uint32_t index, uint32_t x,
+                                        uint32_t y) {
+    if (ka.gen_rays) return camera_ray(ka, cam, x, y);
+    const float4 cr = ka.camera_rays[index];  // binding 1
+    return mk(cr.x, cr.y, cr.z);
+}
+
+// per_pixel prologue, :212-222, given the pixel's camera ray direction.
+__device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t index, uint32_t random_index, f3 cam,
+                                             Path& p) {
     p.o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
-#ifdef RT_EXP_NO_FB  // timing experiment only: results are wrong
-    const float4 cr = make_float4(ka.camera_origin[0] * 0.0f + 0.1f * (float)(index & 255u) / 255.0f - 0.05f,
-                                  (float)(index % ka.width) * 1e-4f - 0.02f, -1.0f, 0.0f);
-#else
-    const float4 cr = ka.camera_rays[index];
-#endif
-    p.d = mk(cr.x, cr.y, cr.z);
+    p.d = cam;
     p.seed = index * random_index * 326624u;
     const float rx = random01(p.seed), ry = random01(p.seed), rz = random01(p.seed);
     const f3 jit = mk(rx * 2.0f - 1.0f, ry * 2.0f - 1.0f, rz * 2.0f - 1.0f);
@@ -430,13 +452,10 @@ __device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t inde
     p.bounce = 0;
 }
 
-// One iteration of the bounce loop, :226-311. Returns true when the path is
-// finished (escaped to the environment, or the bounce limit is reached).
-__device__ __forceinline__ bool path_step(const SceneView& sv, const KernelArgs& ka, Path& p,
-                                          uint32_t& rays RT_DIAG_ARG) {
-    if (p.bounce >= ka.bounces) return true;
-    const Hit h = trace_ray(sv, ka, p.o, p.d RT_DIAG_PASS);
-    ++rays;
+// The shading half of one iteration of the bounce loop, :228-311, given the
+// trace result. Returns true when the path is finished (escaped to the
+// environment, or the bounce limit is reached).
+__device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka, Path& p, const Hit& h) {
     if (h.t == kF32Max) {
         const f4 c = sample_env(ka, sv.srgb, p.d);
         p.light.x = p.light.x + c.x * p.contrib.x;
@@ -446,12 +465,14 @@ __device__ __forceinline__ bool path_step(const SceneView& sv, const KernelArgs&
         return true;
     }
     const RtMaterial m = sv.mat[min(h.material_index, ka.material_count - 1u)];
+    // the texel load is issued first so that its latency overlaps the draws
+    const uint32_t texel = fetch_texture(ka, m.texture_index, h.u, h.v);
     const float gx = normal01(p.seed);
     const float gy = normal01(p.seed);
     const float gz = normal01(p.seed);
     const f3 diffuse = normalize(h.n + mk(gx, gy, gz));
     const f3 specular = p.d - h.n * (2.0f * dot(h.n, p.d));  // reflect(d, n)
-    const f4 color = sample_texture(ka, sv.srgb, m.texture_index, h.u, h.v);
+    const f4 color = decode_texel(texel, sv.srgb);
     const float e = m.emission_power;
     p.light.x = p.light.x + (color.x * e) * p.contrib.x;
     p.light.y = p.light.y + (color.y * e) * p.contrib.y;
@@ -522,15 +543,23 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 // start, so no per-frame reset is needed: a launch performs exactly
 // owned_tiles + waves increments, one failing claim per wave).
 __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
-    const uint64_t live = __ballot(1);
-    const uint32_t leader = (uint32_t)__ffsll((long long)live) - 1u;
     unsigned long long v = 0;
-    if ((threadIdx.x & 63u) == leader) v = atomicAdd(ka.tile_counter, 1ull);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, leader);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), leader);
+    if ((threadIdx.x & 63u) == 0) v = atomicAdd(ka.tile_counter, 1ull);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 0);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 0);
     const uint64_t rel = ((uint64_t)hi << 32 | lo) - ka.tile_base;
     return rel > 0xffffffffull ? 0xffffffffu : (uint32_t)rel;
 }
+
+#ifdef RT_DIAG
+// Diagnostic build only: wave-level cycle stamps (s_memtime) accumulated per
+// wave and added to ka.diag at exit. Never compiled into the product build.
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#endif
 
 // Dynamic LDS image, in this order (all 16-byte aligned):
 //   float4   sphere slots[sphere_count]   centre.xyz, radius^2
@@ -556,7 +585,7 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
-template <int kMode, uint32_t kThreads>
+template <int kMode, uint32_t kThreads, bool kTris>
 __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
@@ -573,14 +602,15 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
         uint32_t* l_smat = reinterpret_cast<uint32_t*>(lds + ka.lds_smat_offset);
         float4* l_nodes = reinterpret_cast<float4*>(lds + ka.lds_nodes_offset);
-        for (uint32_t i = tid; i < ka.sphere_count; i += kThreads) {
+        for (uint32_t i = tid; i < ka.sphere_slot_count; i += kThreads) {
             l_sph[i] = ka.sphere_slots[i];
             l_orig[i] = ka.sphere_orig[i];
-            l_smat[i] = ka.sphere_material[i];
         }
+        for (uint32_t i = tid; i < ka.sphere_count; i += kThreads) l_smat[i] = ka.sphere_material[i];
         for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
         for (uint32_t i = tid; i < ka.material_count; i += kThreads) l_mat[i] = ka.materials[i];
-        for (uint32_t i = tid; i < ka.object_count; i += kThreads) l_obj[i] = ka.objects[i];
+        if constexpr (kTris)
+            for (uint32_t i = tid; i < ka.object_count; i += kThreads) l_obj[i] = ka.objects[i];
         sv.sph = l_sph;
         sv.orig = l_orig;
         sv.sph_mat = l_smat;
@@ -597,37 +627,131 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         sv.tri_prims = l_tp;
     }
     for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];
+    float* l_cam = l_srgb + 256;  // camera block for device-side primary rays
+    if (tid < 16u) {
+        l_cam[tid] = ka.inv_proj[tid];
+        l_cam[16u + tid] = ka.inv_view[tid];
+    }
+    if (tid == 0) l_cam[32] = ka.aspect;
     __syncthreads();
 
     const bool accumulate = ka.accumulate == 1u;
     const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;  // :158-175
 
+    // Lane states. A lane owns one pixel at a time and one ray of its path.
+    constexpr uint32_t kIdle = 0, kSetup = 1, kTrav = 2, kDone = 3;
     uint32_t rays = 0;
-    bool active = false;
-    uint32_t index = 0, sample = 0;
+    uint32_t mode = kIdle;
+    uint32_t index = 0, sample = 0, frame = 0;
     float4 pix = make_float4(0.f, 0.f, 0.f, 0.f);
     Path p;
     p.o = p.d = mk(0.f, 0.f, 0.f);
     p.light = p.contrib = f4{0.f, 0.f, 0.f, 0.f};
     p.seed = p.bounce = 0;
+    TraceState ts;
+    ts.inv = mk(0.f, 0.f, 0.f);
+    ts.a4 = ts.a2 = 0.f;
+    ts.node = 0;
+    ts.phase = 2;
+    ts.nan_hit = false;
+    ts.sph = SphereHit{kF32Max, 0u, 0u};
+    ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
+
+    // Write-behind of finished pixels: their stores are issued just before the
+    // traversal phase (LDS-only for sphere scenes) instead of where the pixel
+    // finishes, so the next refill's loads do not queue behind them in vmcnt.
+    uint32_t wb_index = 0xffffffffu, wb_out = 0;
+    float4 wb_pix = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto flush_write = [&]() {
+        if (wb_index != 0xffffffffu) {
+#ifndef RT_EXP_NO_STORE  // timing experiment only: results are wrong
+            if (accumulate) ka.accum[wb_index] = wb_pix;  // :164
+            ka.output[wb_index] = wb_out;                 // :178
+#else
+            if (wb_pix.x == 1234.5f) ka.output[wb_index] = wb_out;
+#endif
+            wb_index = 0xffffffffu;
+        }
+    };
+
+    // random_index of a sample (:154, :162): the frame's accumulation index
+    // (advanced per frame by the host only when accumulating, src/renderer.rs:216-235)
+    // plus the sample number.
+    auto random_index = [&]() { return ka.accumulation_index + (accumulate ? frame : 0u) + sample; };
+
+    // A finished sample: pixel_color += per_pixel(...) (:161); then the pixel's
+    // next sample (random_index += 1, :162), its next frame (a multi-frame
+    // launch runs the frames of one pixel back to back on its lane), or its
+    // final write (:164-178).
+    auto finish_sample = [&]() {
+        sample += 1;
+        if (accumulate) {
+            pix.x = pix.x + p.light.x;
+            pix.y = pix.y + p.light.y;
+            pix.z = pix.z + p.light.z;
+            pix.w = pix.w + p.light.w;
+        }
+        if (sample == samples && frame + 1u < ka.frames) {
+            frame += 1;
+            sample = 0;
+        }
+        if (sample < samples) {
+            start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, index % ka.width, index / ka.width), p);
+            mode = kSetup;
+        } else {
+            float r, g, b, a;
+            if (accumulate) {
+                const float div = (float)((ka.accumulation_index + frame) * ka.compute_per_frame);
+                r = clamp01(pix.x / div);
+                g = clamp01(pix.y / div);
+                b = clamp01(pix.z / div);
+                a = clamp01(pix.w / div);
+            } else {
+                r = clamp01(p.light.x);
+                g = clamp01(p.light.y);
+                b = clamp01(p.light.z);
+                a = clamp01(p.light.w);
+            }
+            flush_write();  // at most one pixel pending per lane
+            wb_index = index;
+            wb_pix = pix;
+            wb_out = pack_rgba8(r, g, b, a);
+            mode = kIdle;
+        }
+    };
 
     uint32_t tile = claim_tile(ka);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
 #ifdef RT_DIAG
-    DiagAcc dg;
-    unsigned long long iters = 0;
+    unsigned long long iters = 0, trav_cyc = 0, steps = 0, step_lanes = 0, shade_cyc = 0, refill_cyc = 0,
+                       setup_cyc = 0;
     const unsigned long long t_start = stamp();
 #endif
     while (true) {
 #ifdef RT_DIAG
         ++iters;
+        const unsigned long long ts0 = stamp();
 #endif
-        // Refill: idle lanes take the next pixels, in slot order.
+        // 1. Shade the lanes whose trace has finished (:228-311).
+        if (mode == kDone) {
+            const Hit h = trace_end<kTris>(sv, ka, p.o, p.d, ts);
+            ++rays;
+            if (shade(sv, ka, p, h))
+                finish_sample();
+            else
+                mode = kSetup;
+        }
+#ifdef RT_DIAG
+        const unsigned long long ts1 = stamp();
+        shade_cyc += ts1 - ts0;
+#endif
+        // 2. Refill: idle lanes take the next pixels of the wave's tile, in slot
+        // order (ballot + mbcnt = a wave-wide prefix sum over the idle lanes).
         while (true) {
-            const uint64_t need = __ballot(!active);
+            const uint64_t need = __ballot(mode == kIdle);
             if (need == 0 || tile >= ka.owned_tiles) break;
             const uint32_t avail = 64u - next;
-            if (!active) {
+            if (mode == kIdle) {
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 if (rank < avail) {
@@ -638,13 +762,10 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                     if (x < ka.width && y < ka.height) {
                         index = y * ka.width + x;  // :148
                         sample = 0;
-                        active = true;
-#ifndef RT_EXP_NO_FB
+                        frame = 0;
+                        mode = kSetup;
                         if (accumulate) pix = ka.accum[index];  // :156
-#else
-                        pix = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-                        start_sample(ka, index, ka.accumulation_index, p);
+                        start_sample(ka, index, ka.accumulation_index, pixel_ray(ka, l_cam, index, x, y), p);
                     }
                 }
             }
@@ -654,43 +775,59 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                 next = 0;
             }
         }
-        if (__ballot(active) == 0) break;
-        if (active && path_step(sv, ka, p, rays RT_DIAG_PASS)) {
-            sample += 1;
-            if (accumulate) {  // pixel_color += per_pixel(...), :161
-                pix.x = pix.x + p.light.x;
-                pix.y = pix.y + p.light.y;
-                pix.z = pix.z + p.light.z;
-                pix.w = pix.w + p.light.w;
-            }
-            if (sample < samples) {
-                start_sample(ka, index, ka.accumulation_index + sample, p);  // random_index += 1, :162
-            } else {
-                float r, g, b, a;
-                if (accumulate) {
-                    ka.accum[index] = pix;  // :164
-                    const float div = (float)(ka.accumulation_index * ka.compute_per_frame);
-                    r = clamp01(pix.x / div);
-                    g = clamp01(pix.y / div);
-                    b = clamp01(pix.z / div);
-                    a = clamp01(pix.w / div);
-                } else {
-                    r = clamp01(p.light.x);
-                    g = clamp01(p.light.y);
-                    b = clamp01(p.light.z);
-                    a = clamp01(p.light.w);
-                }
-                ka.output[index] = pack_rgba8(r, g, b, a);  // :178
-                active = false;
+#ifdef RT_DIAG
+        const unsigned long long ts2 = stamp();
+        refill_cyc += ts2 - ts1;
+#endif
+        // 3. Start the next ray of every lane that has one (the bounce loop's
+        // bound, :226, ends a path without a trace only when bounces == 0).
+        if (mode == kSetup) {
+            while (mode == kSetup && p.bounce >= ka.bounces) finish_sample();
+            if (mode == kSetup) {
+                trace_begin<kTris>(sv, ka, p.o, p.d, ts);
+                mode = ts.phase == 2 ? kDone : kTrav;
             }
         }
+        flush_write();
+#ifdef RT_DIAG
+        setup_cyc += stamp() - ts2;
+#endif
+        if (__ballot(mode != kIdle) == 0 && tile >= ka.owned_tiles) break;
+        // 4. Traverse. Lanes whose trace finishes wait (kDone) until fewer than
+        // `trav_threshold` lanes are still traversing; then the wave goes back
+        // to shade and refill them together, so neither the traversal tail nor
+        // the shading runs on a nearly empty wave. With no tiles left, traverse
+        // to the end.
+        const uint32_t thresh = tile >= ka.owned_tiles ? 0u : ka.trav_threshold;
+#ifdef RT_DIAG
+        const unsigned long long t0 = stamp();
+#endif
+        while (true) {
+            const uint64_t trav = __ballot(mode == kTrav);
+            if ((uint32_t)__popcll(trav) <= thresh || trav == 0) break;
+#ifdef RT_DIAG
+            ++steps;
+            step_lanes += (unsigned long long)__popcll(trav);
+#endif
+            if (mode == kTrav) {
+                trace_step<kTris>(sv, ka, p.o, p.d, ts);
+                if (ts.phase == 2) mode = kDone;
+            }
+        }
+#ifdef RT_DIAG
+        trav_cyc += stamp() - t0;
+#endif
     }
 #ifdef RT_DIAG
     if ((threadIdx.x & 63u) == 0) {
         atomicAdd(ka.diag + 0, stamp() - t_start);
-        atomicAdd(ka.diag + 1, dg.tri);
-        atomicAdd(ka.diag + 2, dg.sph);
+        atomicAdd(ka.diag + 1, trav_cyc);
+        atomicAdd(ka.diag + 2, steps);
         atomicAdd(ka.diag + 3, iters);
+        atomicAdd(ka.diag + 4, step_lanes);
+        atomicAdd(ka.diag + 5, shade_cyc);
+        atomicAdd(ka.diag + 6, refill_cyc);
+        atomicAdd(ka.diag + 7, setup_cyc);
     }
 #endif
     atomicAdd(&block_rays, rays);
@@ -698,12 +835,16 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     if (tid == 0 && block_rays != 0) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
 }
 
-// Instantiations: LDS mode x workgroup size. All waves of a workgroup share
-// one LDS copy of the scene, so the best size depends on the scene's LDS
-// footprint against the VGPR-limited waves per SIMD; the host picks the size
-// with the most resident waves up to a cap (rt_pathtrace_pick_config).
-#define RT_FOR_EACH_CONFIG(X) \
-    X(0, 256) X(0, 512) X(0, 1024) X(1, 256) X(1, 512) X(1, 1024) X(2, 256) X(2, 512) X(2, 1024)
+// Instantiations: LDS mode x workgroup size x triangles present. All waves of
+// a workgroup share one LDS copy of the scene, so the best size depends on the
+// scene's LDS footprint against the VGPR-limited waves per SIMD; the host picks
+// the size with the most resident waves up to a cap (rt_pathtrace_pick_config).
+// Sphere-only scenes get kernels without the triangle side (fewer live scalar
+// registers: the kernel arguments of the triangle path no longer spill).
+#define RT_FOR_EACH_CONFIG(X)                                                                                   \
+    X(0, 256, true) X(0, 512, true) X(0, 1024, true) X(1, 256, true) X(1, 512, true) X(1, 1024, true)           \
+    X(2, 256, true) X(2, 512, true) X(2, 1024, true) X(0, 256, false) X(0, 512, false) X(0, 1024, false)        \
+    X(1, 256, false) X(1, 512, false) X(1, 1024, false)
 
 namespace {
 // Dynamic LDS above 64 KiB must be opted into per kernel.
@@ -717,12 +858,12 @@ hipError_t allow_big_lds(const void* fn) {
 }
 }  // namespace
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, uint32_t threads, size_t lds_bytes, uint32_t blocks,
-                               hipStream_t stream) {
-#define RT_LAUNCH(M, T)                                                                                    \
-    if (mode == M && threads == T) {                                                                      \
-        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T>), dim3(blocks), dim3(T), lds_bytes, stream, ka);    \
-        return hipGetLastError();                                                                         \
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes,
+                               uint32_t blocks, hipStream_t stream) {
+#define RT_LAUNCH(M, T, TR)                                                                                  \
+    if (mode == M && threads == T && tris == TR) {                                                          \
+        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T, TR>), dim3(blocks), dim3(T), lds_bytes, stream, ka);  \
+        return hipGetLastError();                                                                           \
     }
     RT_FOR_EACH_CONFIG(RT_LAUNCH)
 #undef RT_LAUNCH
@@ -735,16 +876,16 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, uint32_t threads,
 // add contention), ties to the smaller workgroup.
 constexpr int kDefaultWavesPerCu = 16;
 
-hipError_t rt_pathtrace_pick_config(int mode, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
-                                    uint32_t* threads, int* blocks_per_cu) {
+hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, uint32_t force_threads,
+                                    uint32_t waves_cap, uint32_t* threads, int* blocks_per_cu) {
     const int kTargetWavesPerCu = waves_cap ? (int)waves_cap : kDefaultWavesPerCu;
     int best_waves = -1;
-#define RT_OCC(M, T)                                                                                      \
-    if (mode == M) {                                                                                      \
+#define RT_OCC(M, T, TR)                                                                                  \
+    if (mode == M && tris == TR) {                                                                        \
         int n = 0;                                                                                        \
-        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T>));         \
+        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T, TR>));     \
         if (e != hipSuccess) return e;                                                                    \
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T>, T, lds_bytes);    \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T, TR>, T, lds_bytes); \
         if (e != hipSuccess) return e;                                                                    \
         const int waves = std::min(n * (int)(T / 64), kTargetWavesPerCu);                                 \
         if (n > 0 && (force_threads ? force_threads == T : waves > best_waves)) {                         \

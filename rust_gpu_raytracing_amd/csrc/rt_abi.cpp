@@ -9,6 +9,7 @@
 // Stream order gives the same visibility guarantees as wgpu's queue order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -21,9 +22,9 @@
 #include "rt_kernel_args.h"
 #include "sphere_bvh.h"
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, uint32_t threads, size_t lds_bytes, uint32_t blocks,
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes, uint32_t blocks,
                                hipStream_t stream);
-hipError_t rt_pathtrace_pick_config(int mode, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
+hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
                                     uint32_t* threads, int* blocks_per_cu);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
@@ -47,6 +48,12 @@ namespace {
 
 constexpr size_t kLdsSceneBudget = 64 * 1024;    // mode 1: spheres/materials/objects/sphere BVH per workgroup
 constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerator (one 1024-thread workgroup per CU)
+// Always staged at the end of the LDS image: the sRGB table (256 floats) and the
+// camera block (inverse projection, inverse view, aspect: 33 floats).
+constexpr size_t kLdsTailBytes = 1024 + 160;
+// A wave goes back to shading once at most this many of its 64 lanes are still
+// traversing (pathtrace.hip, step 4 of the kernel loop).
+constexpr uint32_t kDefaultTravThreshold = 8;
 
 thread_local std::string g_create_error;
 
@@ -82,11 +89,13 @@ struct rt_ctx {
     bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
     size_t occ_lds_bytes = 0;
     int occ_mode = -1;
+    bool occ_tris = false;
     int max_lds_mode = 2;               // RT_LDS_MODE (A/B switch): highest staging mode allowed
     int occ_blocks_per_cu = 0;
     uint32_t occ_threads = 0;
     uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
     uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
+    uint32_t trav_threshold = kDefaultTravThreshold;  // RT_TRAV_THRESHOLD (A/B switch)
     uint32_t last_blocks = 0, last_lds = 0;
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
@@ -97,7 +106,7 @@ struct rt_ctx {
     uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
     bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
     uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
-    uint32_t n_always = 0, n_nodes = 0;
+    uint32_t n_always = 0, n_nodes = 0, n_slots = 0;
     float sphere_extent = 0.0f;
     // triangle accelerator over (object, sub-object) pairs (sphere_bvh.h)
     SphereBvhNode* d_tri_bvh = nullptr;
@@ -130,6 +139,8 @@ struct rt_ctx {
 
     // timing
     bool timing = false;
+    bool gen_rays = false;  // rt_update_camera_matrices: primary rays computed on the device
+    float inv_proj[16] = {}, inv_view[16] = {};
     std::vector<EventPair> pending;
     std::vector<EventPair> pool;
     double total_ms = 0.0;
@@ -229,6 +240,7 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
         (rc = upload_raw(ctx, ctx->d_bvh, sl.nodes.data(), sl.nodes.size() * sizeof(SphereBvhNode))))
         return rc;
     ctx->n_always = sl.n_always;
+    ctx->n_slots = (uint32_t)sl.slot_orig.size();
     ctx->n_nodes = (uint32_t)sl.nodes.size();
     ctx->sphere_extent = sl.extent;
     ctx->slots_dirty = false;
@@ -439,6 +451,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
         ctx->use_bvh = !(env && env[0] == '0');
+        env = std::getenv("RT_TRAV_THRESHOLD");
+        if (env) ctx->trav_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
@@ -454,8 +468,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
         (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9)) ||
         (rc = dev_alloc(ctx, &ctx->d_tile_counter, 1)) ||
-        (rc = dev_alloc(ctx, &ctx->d_slot_sph, info->sphere_count)) ||
-        (rc = dev_alloc(ctx, &ctx->d_slot_orig, info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_slot_sph, 4 * (size_t)info->sphere_count + 4)) ||  // padded groups
+        (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_bvh, 2 * (size_t)info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
@@ -569,7 +583,17 @@ int rt_update_ray_directions(rt_ctx* ctx, const rt_ray* rays, uint32_t count) {
     RT_ENTER(ctx);
     if (count && !rays) return fail(ctx, RT_E_INVALID, "rays is NULL");
     if (count > ctx->n_pixels) return fail(ctx, RT_E_CAPACITY, "more rays than pixels");
+    ctx->gen_rays = false;
     return upload_raw(ctx, ctx->d_rays, rays, (size_t)count * 16);
+}
+
+int rt_update_camera_matrices(rt_ctx* ctx, const float inverse_projection[16], const float inverse_view[16]) {
+    RT_ENTER(ctx);
+    if (!inverse_projection || !inverse_view) return fail(ctx, RT_E_INVALID, "matrix is NULL");
+    std::memcpy(ctx->inv_proj, inverse_projection, sizeof(ctx->inv_proj));
+    std::memcpy(ctx->inv_view, inverse_view, sizeof(ctx->inv_view));
+    ctx->gen_rays = true;
+    return RT_OK;
 }
 
 int rt_update_camera(rt_ctx* ctx, const rt_ray_camera* camera) {
@@ -630,8 +654,15 @@ int rt_update_materials(rt_ctx* ctx, const rt_scene_material* materials, uint32_
     return upload_raw(ctx, ctx->d_mat, materials, (size_t)count * 32);
 }
 
+static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
+
 int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     RT_ENTER(ctx);
+    return dispatch_frames(ctx, bounces, 1);
+}
+
+// One launch rendering `frames` frames starting at Params.accumulation_index.
+static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     const rt_params& p = ctx->params;
     {
         int rc = refresh_sphere_slots(ctx, p.sphere_count);
@@ -674,6 +705,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.accumulation_index = p.accumulation_index;
     ka.accumulate = p.accumulate;
     ka.sphere_count = p.sphere_count;
+    ka.sphere_slot_count = ctx->n_slots;
     ka.object_count = p.object_count;
     ka.compute_per_frame = p.compute_per_frame;
     ka.texture_width = p.texture_width;
@@ -689,32 +721,39 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     ka.env_w = ctx->env_w;
     ka.env_h = ctx->env_h;
     ka.height = ctx->height;
+    ka.gen_rays = ctx->gen_rays ? 1u : 0u;
+    ka.aspect = (float)ctx->width / (float)ctx->height;  // src/camera.rs:142
+    std::memcpy(ka.inv_proj, ctx->inv_proj, sizeof(ka.inv_proj));
+    std::memcpy(ka.inv_view, ctx->inv_view, sizeof(ka.inv_view));
     ka.bounces = bounces;
     ka.tiles_x = ctx->tiles_x;
     ka.owned_tiles = ctx->owned_tiles;
     ka.rank = ctx->rank;
     ka.world_size = ctx->world;
+    ka.trav_threshold = ctx->trav_threshold;
+    ka.frames = frames;
 
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
-    size_t off = al16((size_t)p.sphere_count * 16);
+    size_t off = al16((size_t)ctx->n_slots * 16);
     ka.lds_mat_offset = (uint32_t)off;
     off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
     ka.lds_obj_offset = (uint32_t)off;
     off = al16(off + (size_t)p.object_count * sizeof(RtObject));
     ka.lds_orig_offset = (uint32_t)off;
-    off = al16(off + (size_t)p.sphere_count * 4);
+    off = al16(off + (size_t)ctx->n_slots * 4);
     ka.lds_smat_offset = (uint32_t)off;
     off = al16(off + (size_t)p.sphere_count * 4);
     ka.lds_nodes_offset = (uint32_t)off;
     off = al16(off + (size_t)ctx->n_nodes * sizeof(SphereBvhNode));
-    const size_t mode1_bytes = off + 1024;
+    const size_t mode1_bytes = off + kLdsTailBytes;
     ka.lds_tri_nodes_offset = (uint32_t)off;
     off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
     ka.lds_tri_prims_offset = (uint32_t)off;
     off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
-    const size_t mode2_bytes = off + 1024;
+    const size_t mode2_bytes = off + kLdsTailBytes;
     int mode = 0;
+    const bool tris = p.object_count != 0;  // else the sphere-only kernels
     if (!ctx->force_global_scene) {
         if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes <= kLdsAccelBudget && ctx->max_lds_mode >= 2)
             mode = 2;
@@ -723,27 +762,29 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     }
     size_t lds_bytes;
     if (mode == 2) {
-        ka.lds_srgb_offset = (uint32_t)(mode2_bytes - 1024);
+        ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
         lds_bytes = mode2_bytes;
     } else if (mode == 1) {
-        ka.lds_srgb_offset = (uint32_t)(mode1_bytes - 1024);
+        ka.lds_srgb_offset = (uint32_t)(mode1_bytes - kLdsTailBytes);
         lds_bytes = mode1_bytes;
     } else {
         ka.lds_srgb_offset = 0;
-        lds_bytes = 1024;
+        lds_bytes = kLdsTailBytes;
     }
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
-    if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode) {
+    if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode ||
+        ctx->occ_tris != tris) {
         int per_cu = 0;
         uint32_t threads = 0;
         hipError_t oe =
-            rt_pathtrace_pick_config(mode, lds_bytes, ctx->force_threads, ctx->waves_cap, &threads, &per_cu);
+            rt_pathtrace_pick_config(mode, tris, lds_bytes, ctx->force_threads, ctx->waves_cap, &threads, &per_cu);
         if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
         ctx->occ_blocks_per_cu = per_cu;
         ctx->occ_threads = threads;
         ctx->occ_lds_bytes = lds_bytes;
         ctx->occ_mode = mode;
+        ctx->occ_tris = tris;
     }
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
@@ -764,7 +805,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
         }
         RT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
     }
-    hipError_t e = rt_launch_pathtrace(ka, mode, ctx->occ_threads, lds_bytes, blocks, ctx->stream);
+    hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, ctx->stream);
     ctx->last_blocks = blocks;
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
@@ -777,13 +818,16 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     return RT_OK;
 }
 
-int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) {
+int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) { return rt_compute_frames(ctx, bounces, 1); }
+
+int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     RT_ENTER(ctx);
+    if (frames == 0) return fail(ctx, RT_E_INVALID, "frames must be >= 1");
     if (ctx->params.accumulate) {  // src/renderer.rs:216-235 (`accumulate` is a bool there)
         ctx->params.accumulation_index = ctx->k;
-        ctx->k += 1;
+        ctx->k += frames;
     }
-    return rt_dispatch(ctx, bounces);
+    return dispatch_frames(ctx, bounces, frames);
 }
 
 int rt_synchronize(rt_ctx* ctx) {

@@ -82,13 +82,19 @@ struct KernelArgs {
     const uint32_t* __restrict__ env;
     const float* __restrict__ srgb;
     float camera_origin[3];
+    // device-side primary rays (rt_update_camera_matrices): column-major 4x4
+    float inv_proj[16];
+    float inv_view[16];
+    float aspect;        // f32(width) / f32(height), src/camera.rs:142
+    uint32_t gen_rays;   // 1: compute camera rays, 0: read camera_rays
     // Params (binding 0), passed by value at launch
     uint32_t width;
     uint32_t accumulation_index;
     uint32_t accumulate;
     uint32_t sphere_count;
     uint32_t object_count;
-    uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
+    uint32_t sphere_slot_count;  // padded slots (groups of 4, sphere_bvh.h)
+    uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force (a multiple of 4)
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)
@@ -96,6 +102,7 @@ struct KernelArgs {
     uint32_t tri_accel;       // 1: use the triangle BVH, 0: the reference's sweep
     float tri_extent;         // max |coordinate| over sub-object boxes (margin scale)
     uint32_t compute_per_frame;
+    uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     uint32_t texture_width;
     uint32_t texture_height;
     uint32_t env_map_width;
@@ -113,6 +120,7 @@ struct KernelArgs {
     uint32_t owned_tiles;
     uint32_t rank;
     uint32_t world_size;
+    uint32_t trav_threshold;  // resume shading once at most this many lanes still traverse
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;
     uint32_t lds_obj_offset;

@@ -3,6 +3,7 @@
 #include "sphere_bvh.h"
 
 #include <algorithm>
+#include <limits>
 #include <cmath>
 #include <numeric>
 
@@ -205,8 +206,18 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
         const double cap = 8.0 * std::max(sorted[count / 2], 1e-30);
         for (uint32_t i = 0; i < count; i++) in_bvh[i] = std::isfinite(ext[i]) && ext[i] <= cap;
     }
+    // Pad to a multiple of kSphereGroup with slots no ray can hit (NaN centre:
+    // disc is NaN, never >= 0), so the kernel reads spheres in aligned groups.
+    auto pad_group = [&]() {
+        while (out->slot_orig.size() % kSphereGroup) {
+            const float qnan = std::numeric_limits<float>::quiet_NaN();
+            out->slot_sph.insert(out->slot_sph.end(), {qnan, qnan, qnan, qnan});
+            out->slot_orig.push_back(kSphereDummyOrig);
+        }
+    };
     for (uint32_t i = 0; i < count; i++)
         if (!in_bvh[i]) push_slot(i);
+    pad_group();
     out->n_always = (uint32_t)out->slot_orig.size();
 
     std::vector<Prim> prims;
@@ -227,14 +238,21 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
     }
     if (prims.size() < 2) {  // nothing worth a tree: brute-force everything
         for (const Prim& p : prims) push_slot(p.orig);
+        pad_group();
         out->n_always = (uint32_t)out->slot_orig.size();
         return;
     }
-    Builder b{prims, out->nodes, {}, leaf_max ? leaf_max : kSphereBvhLeafMax};
+    const uint32_t lmax = std::min<uint32_t>(leaf_max ? leaf_max : kSphereBvhLeafMax, kSphereGroup);
+    Builder b{prims, out->nodes, {}, lmax};
     b.build(0, (uint32_t)prims.size());
-    for (uint32_t orig : b.leaf_order) push_slot(orig);
-    // leaf fields index the BVH part of the slot array; shift by the brute-force prefix
-    for (SphereBvhNode& nd : out->nodes)
-        if (nd.leaf != kSphereBvhInternal) nd.leaf += out->n_always;
+    // one aligned group of kSphereGroup slots per leaf (padded), in node order
+    for (SphereBvhNode& nd : out->nodes) {
+        if (nd.leaf == kSphereBvhInternal) continue;
+        const uint32_t first = nd.leaf & 0xffffffu, cnt = nd.leaf >> 24;
+        const uint32_t slot = (uint32_t)out->slot_orig.size();
+        for (uint32_t k = 0; k < cnt; k++) push_slot(b.leaf_order[first + k]);
+        pad_group();
+        nd.leaf = slot | (kSphereGroup << 24);
+    }
     out->extent = std::nextafter((float)extent, INFINITY);
 }

@@ -26,10 +26,16 @@ static_assert(sizeof(SphereBvhNode) == 32, "node layout");
 
 constexpr uint32_t kSphereBvhInternal = 0xffffffffu;
 constexpr uint32_t kSphereBvhLeafMax = 4;
+// The kernel tests spheres in aligned groups of 4 slots (one leaf = one group);
+// unused slots hold a NaN sphere that no ray hits, and this original index.
+constexpr uint32_t kSphereGroup = 4;
+constexpr uint32_t kSphereDummyOrig = 0xffffffffu;
 
 struct SphereSlots {
     // Spheres in kernel order: the brute-force ("always") set first, in
-    // original index order, then the BVH leaves' spheres in leaf order.
+    // original index order, then the BVH leaves' spheres in leaf order; both
+    // parts padded to whole groups of kSphereGroup slots (at most
+    // 4 * count + 4 slots in all).
     uint32_t n_always = 0;
     std::vector<float> slot_sph;        // 4 per slot: centre.xyz, radius*radius
     std::vector<uint32_t> slot_orig;    // original sphere index of each slot

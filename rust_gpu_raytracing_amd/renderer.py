@@ -41,8 +41,13 @@ class Renderer:
         rank: int = 0,
         world_size: int = 1,
         camera_rays: np.ndarray | None = None,
+        device_rays: bool | None = None,
         lib=None,
     ):
+        """``camera_rays``: explicit per-pixel directions (the reference's ray buffer).
+        Without them, primary rays are computed on the device from the camera's
+        matrices (``device_rays``, default when no rays are given; bit-identical to
+        ``camera.recalculate_ray_directions()``, rt_update_camera_matrices)."""
         self._lib = N.load_library() if lib is None else lib
         self.scene = scene
         self.accumulate = accumulate
@@ -71,6 +76,9 @@ class Renderer:
         N.check(None, self._lib.rt_create(ctypes.byref(info), ctypes.byref(ctx)), self._lib)
         self._ctx = ctx
         self._upload_textures()
+        self.device_rays = (camera_rays is None) if device_rays is None else device_rays
+        if self.device_rays:
+            self._set_camera_matrices(scene.camera)
 
     # ------------------------------------------------------------------ helpers
     def _params(self, accumulation_index: int) -> np.ndarray:
@@ -113,6 +121,11 @@ class Renderer:
         self._call("rt_update_sub_object_info", N.ptr(subs), subs.shape[0])
         self._call("rt_update_materials", N.ptr(s.materials), s.materials.shape[0])
 
+    def _set_camera_matrices(self, camera) -> None:
+        self._inv = [np.ascontiguousarray(camera.inverse_projection, np.float32).reshape(16),
+                     np.ascontiguousarray(camera.inverse_view, np.float32).reshape(16)]
+        self._call("rt_update_camera_matrices", N.ptr(self._inv[0]), N.ptr(self._inv[1]))
+
     def update_camera(self, camera) -> None:
         """src/renderer.rs:109-129 after a move: reset, new origin, new ray directions."""
         self.scene.camera = camera
@@ -120,6 +133,9 @@ class Renderer:
         rc = N.rt_ray_camera()
         rc.origin[:] = [float(x) for x in camera.position]
         self._call("rt_update_camera", ctypes.byref(rc))
+        if self.device_rays:
+            self._set_camera_matrices(camera)
+            return
         self.camera_rays = np.ascontiguousarray(camera.recalculate_ray_directions())
         self._keep[0] = self.camera_rays
         self._call("rt_update_ray_directions", N.ptr(self.camera_rays), self.camera_rays.shape[0])
@@ -127,6 +143,11 @@ class Renderer:
     def compute_frame(self, bounces: int = REFERENCE_BOUNCES) -> None:
         """src/renderer.rs:201-252 (asynchronous)."""
         self._call("rt_compute_frame", bounces)
+
+    def compute_frames(self, bounces: int = REFERENCE_BOUNCES, frames: int = 1) -> None:
+        """``frames`` compute_frame calls fused into one launch (same results;
+        rt_compute_frames in include/rt_abi.h). Asynchronous."""
+        self._call("rt_compute_frames", bounces, frames)
 
     # ------------------------------------------------------------------ readback & stats
     def synchronize(self) -> None:
@@ -182,7 +203,7 @@ class Renderer:
         self._call("rt_unpack_accumulation", ctypes.c_void_p(src_device_ptr), src_rank, world_size, divisor)
 
     def debug_counters(self) -> list:
-        """RT_DIAG builds only: [frame-loop, triangle, sphere wave-cycles, loop iterations]."""
+        """RT_DIAG builds only: the 8 diagnostic counters (tools/diag_split.py)."""
         v = (ctypes.c_uint64 * 8)()
         N.check(self._ctx, self._lib.rt_debug_counters(self._ctx, v, 8), self._lib)
         return list(v)

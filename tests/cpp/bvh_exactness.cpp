@@ -136,8 +136,21 @@ int main(int argc, char** argv) {
     if (sl.nodes.empty()) { printf("no bvh built\n"); return 2; }
     // structural checks
     std::vector<int> seen(s.size(), 0);
-    for (uint32_t i = 0; i < sl.slot_orig.size(); i++) seen[sl.slot_orig[i]]++;
+    for (uint32_t i = 0; i < sl.slot_orig.size(); i++) {
+        if (sl.slot_orig[i] == kSphereDummyOrig) {  // padding: a NaN sphere no ray can hit
+            if (!std::isnan(sl.slot_sph[4 * i])) { printf("padding slot %u is not NaN\n", i); return 1; }
+            continue;
+        }
+        seen[sl.slot_orig[i]]++;
+    }
     for (size_t i = 0; i < s.size(); i++) if (seen[i] != 1) { printf("slot coverage broken at %zu\n", i); return 1; }
+    // the kernel reads aligned groups of kSphereGroup slots: brute-force prefix and every leaf
+    if (sl.n_always % kSphereGroup || sl.slot_orig.size() % kSphereGroup) { printf("slot groups unaligned\n"); return 1; }
+    for (const SphereBvhNode& nd : sl.nodes)
+        if (nd.leaf != kSphereBvhInternal && ((nd.leaf & 0xffffffu) % kSphereGroup || (nd.leaf >> 24) != kSphereGroup)) {
+            printf("leaf group unaligned\n");
+            return 1;
+        }
     long hits = 0;
     for (long r = 0; r < n_rays; r++) {
         V o, d;

@@ -234,3 +234,43 @@ def test_gpu_determinism_and_timing(gpu):
     assert n == 3 and ms > 0
     a2, _, _ = gpu_render(scene, bounces, 3)
     assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
+
+
+@pytest.mark.parametrize("config,spp,accumulate,frames,kw", [
+    ("c2_rtiow", 1, 1, 4, {}),
+    ("c3_chess", 3, 1, 3, dict(env_size=(512, 256))),
+    ("c1_four_spheres", 1, 0, 3, {}),
+])
+def test_gpu_multi_frame_launch(gpu, config, spp, accumulate, frames, kw):
+    """rt_compute_frames(b, F) == F x rt_compute_frame(b), bit for bit (the fused launch the
+    multi-GPU bench uses), also after ordinary frames and with a tile split."""
+    scene, bounces = build_config(config, width=96, height=56, **kw)
+    acc1, out1, rays1 = gpu_render(scene, bounces, 1 + frames, spp=spp, accumulate=accumulate)
+    with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp) as r:
+        r.compute_frame(bounces)
+        r.compute_frames(bounces, frames)
+        assert r.accumulation_index == (1 + (1 + frames) if accumulate else 1)
+        acc, out, rays = r.read_accumulation(), r.read_output(), r.ray_count()
+    assert rays == rays1
+    assert np.array_equal(out, out1) and np.array_equal(acc.view(np.uint32), acc1.view(np.uint32))
+    world, total = 2, 0
+    for rank in range(world):
+        with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp, rank=rank, world_size=world) as r:
+            r.compute_frames(bounces, 1 + frames)
+            total += r.ray_count()
+    assert total == rays1
+
+
+@pytest.mark.parametrize("config,w,h", [("c2_rtiow", 1920, 1080), ("c3_chess", 13, 7), ("c1_four_spheres", 800, 600)])
+def test_gpu_device_camera_rays(gpu, config, w, h):
+    """Device-side primary rays (rt_update_camera_matrices) == the host generator's ray buffer
+    (src/camera.rs:139-182 restated in camera.py), bit for bit, through a whole frame."""
+    kw = dict(env_size=(256, 128)) if config == "c3_chess" else {}
+    scene, bounces = build_config(config, width=w, height=h, **kw)
+    host = scene.camera.recalculate_ray_directions()
+    a1, o1, r1 = gpu_render(scene, bounces, 1, rays=host)
+    with Renderer(scene, device_rays=True) as r:
+        r.compute_frame(bounces)
+        a2, o2, r2 = r.read_accumulation(), r.read_output(), r.ray_count()
+    assert r1 == r2
+    assert np.array_equal(o1, o2) and np.array_equal(a1.view(np.uint32), a2.view(np.uint32))

@@ -35,13 +35,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--env", nargs="*", default=[])
+    ap.add_argument("--device-rays", action="store_true", help="generate primary rays on the device")
     args = ap.parse_args()
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     rays_dirs = scene.camera.recalculate_ray_directions()
     rs = []
     for p in args.libs:
         lib = N.load_library(Path(p).resolve())
-        rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib))
+        if args.device_rays:
+            rs.append(Renderer(scene, lib=lib, device_rays=True))
+        else:
+            rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib))
     for r in rs:  # warmup
         r.compute_frame(bounces)
         r.synchronize()

@@ -1,8 +1,9 @@
 """Time split of the frame loop from an RT_DIAG build (in-kernel s_memtime stamps).
 
 usage: RT_LIB=build/ab/lib_diag.so python tools/diag_split.py [config ...]
-Reports, summed over waves, the share of wave-cycles spent in triangle and
-sphere traversal; the rest is shading, RNG, refill and framebuffer I/O.
+Reports, summed over waves, the share of wave-cycles spent in the traversal
+loop (step 4 of the kernel loop); the rest is shading, RNG, refill and
+framebuffer I/O. Also: traversal steps per ray and mean lanes per step.
 Stamps serialise the wave around each trace: read shares, not absolute times.
 """
 import json
@@ -28,7 +29,9 @@ for name in sys.argv[1:] or list(SIZES):
             r.compute_frame(bounces)
         c = r.debug_counters()
         rays = r.ray_count()
-    total, tri, sph, it = c[:4]
-    print(json.dumps({"config": name, "tri_share": tri / total, "sphere_share": sph / total,
-                      "other_share": 1 - (tri + sph) / total, "cycles_per_ray": total / rays,
-                      "loop_iters_per_ray": it / rays}))
+    total, trav, steps, it, step_lanes, shade, refill, setup = c[:8]
+    print(json.dumps({"config": name, "trav_share": trav / total, "shade_share": shade / total,
+                      "refill_share": refill / total, "setup_share": setup / total,
+                      "rest_share": 1 - (trav + shade + refill + setup) / total,
+                      "cycles_per_ray": total / rays, "steps_per_ray": steps / rays,
+                      "lanes_per_step": step_lanes / max(steps, 1), "outer_iters_per_ray": it / rays}))

@@ -1,0 +1,40 @@
+"""Record the PMC-measured HBM traffic of a tools/profile.sh run for bench.py.
+
+usage: python tools/update_traffic.py gpurun_out/prof_<tag> profiles/<tag>
+Copies the kernel stats + counter summary into profiles/<tag>/ and stores
+{workload: {fetch_bytes_x2, write_bytes, avg_ns, source}} in
+profiles/pmc_traffic.json (bench.py's roofline.traffic; FETCH_SIZE doubled per
+the gfx950 note in MI355X_MICROARCH.md, WRITE_SIZE as is, both per launch).
+"""
+import json
+import shutil
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+import summarize_prof  # noqa: E402
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def main(prof_dir, dest):
+    prof_dir, dest = Path(prof_dir), Path(dest)
+    dest.mkdir(parents=True, exist_ok=True)
+    summ = summarize_prof.main(prof_dir)
+    (dest / "summary.json").write_text(json.dumps(summ, indent=1) + "\n")
+    ks = prof_dir / "trace" / "run_kernel_stats.csv"
+    if ks.exists():
+        shutil.copy(ks, dest / "kernel_stats.csv")
+    bench_line = json.loads((prof_dir / "trace_bench.json").read_text().strip().splitlines()[-1])
+    shutil.copy(prof_dir / "trace_bench.json", dest / "trace_bench.json")
+    workload = bench_line["config"]["workload"]
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    table = json.loads(f.read_text()) if f.exists() else {}
+    table[workload] = {"fetch_bytes_x2": summ["fetch_bytes_x2"], "write_bytes": summ["write_bytes"],
+                       "avg_ns": summ.get("avg_ns"), "source": str(dest.relative_to(ROOT))}
+    f.write_text(json.dumps(table, indent=1, sort_keys=True) + "\n")
+    print(json.dumps(table[workload]))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
