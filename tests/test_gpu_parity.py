@@ -274,3 +274,55 @@ def test_gpu_device_camera_rays(gpu, config, w, h):
         a2, o2, r2 = r.read_accumulation(), r.read_output(), r.ray_count()
     assert r1 == r2
     assert np.array_equal(o1, o2) and np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
+
+
+@pytest.mark.parametrize("config,kw", [("c3_chess", dict(env_size=(512, 256))), ("c5_heightfield", dict(nx=40, nz=20))])
+def test_gpu_reference_sweep_without_accelerator(gpu, oracle_lib, monkeypatch, config, kw):
+    """RT_TRI_BVH=0: the kernel walks the reference's own object -> sub-object -> triangle
+    sweep (phase 3 of the trace state), same results as the oracle."""
+    monkeypatch.setenv("RT_TRI_BVH", "0")
+    scene, bounces = build_config(config, width=64, height=40, **kw)
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
+    assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
+
+
+def _pcg_f32(seed):
+    state = (seed * 747796405 + 2891336453) & 0xFFFFFFFF
+    word = (((state >> ((state >> 28) + 4)) ^ state) * 277803737) & 0xFFFFFFFF
+    seed = ((word >> 22) ^ word) & 0xFFFFFFFF
+    return seed, np.float32(seed) / np.float32(4294967296.0)
+
+
+def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib):
+    """Rays lying exactly in a triangle's plane (det == 0, origin on the plane) give a NaN
+    distance that the reference's sweep accepts (:449-481, :457); the accelerator hands such
+    lanes to the sweep itself. Primary directions are chosen so that d.y + jitter.y == 0
+    exactly (the jitter is the kernel's own PCG draw, :217-219)."""
+    from rust_gpu_raytracing_amd.camera import Camera
+    from rust_gpu_raytracing_amd.scene import SceneObject
+
+    scene, bounces = build_config("c1_four_spheres", width=48, height=32)
+    y0 = np.float32(0.5)
+    a = np.array([[-1, y0, -1], [1, y0, -1]], np.float32)
+    b = np.array([[1, y0, -1], [1, y0, 1]], np.float32)
+    c = np.array([[-1, y0, 1], [-1, y0, 1]], np.float32)
+    info = np.zeros((), B.OBJECT_INFO)
+    info["min_bounds"] = [-1, y0, -1]
+    info["max_bounds"] = [1, y0, 1]
+    obj = SceneObject(info, B.scene_triangles(a, b, c))
+    obj.create_sub_objects(0, 0)
+    scene.objects = [obj]
+    scene.camera = Camera(48, 32, position=np.array([0.0, y0, 4.0], np.float32))
+    rays = scene.camera.recalculate_ray_directions()
+    for i in range(rays.shape[0]):  # frame k = 1: seed = index * 1 * 326624
+        s = (i * 326624) & 0xFFFFFFFF
+        s, _ = _pcg_f32(s)
+        s, ry = _pcg_f32(s)
+        jy = (ry * np.float32(2.0) - np.float32(1.0)) * np.float32(0.0005)
+        rays["direction"][i, 1] = -jy
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((32, 48, 4), np.float32)
+    out_o = np.zeros((32, 48), np.uint32)
+    rays_o = o.render_frame(scene.params(accumulation_index=1), bounces, acc_o, out_o)
+    acc, out, n = gpu_render(scene, bounces, 1, rays=rays)
+    assert_same(acc, out, n, acc_o, out_o, rays_o)
