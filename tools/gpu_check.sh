@@ -1,11 +1,11 @@
 #!/bin/bash
 # One GPU-box pass: parity tests, smoke, headline bench, all configs, profile.
 # usage (via gpurun): bash tools/gpu_check.sh <tag> [steps...]
-#   steps: any of tests smoke bench all prof (default: all of them)
+#   steps: any of tests smoke bench all prof multi (default: all of them)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -e -o pipefail
 TAG=${1:-r01}; shift || true
-STEPS=${*:-tests smoke bench all prof}
+STEPS=${*:-tests smoke bench all prof multi}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -17,7 +17,13 @@ for s in $STEPS; do
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     all)   timeout -k 10 600 python3 tools/bench_all.py --no-cpu > "$OUT/bench_all.jsonl" 2> "$OUT/bench_all.err" ;;
-    prof)  bash tools/profile.sh "$TAG" ;;
+    prof)  bash tools/profile.sh "$TAG" ;;  # then locally: python tools/update_traffic.py gpurun_out/prof_<tag> profiles/<tag>
+    multi) # N-rank rehearsal on the one GPU of the box (gloo; the real run is RCCL, one GPU per rank)
+           for n in 2 4; do
+             RT_BENCH_ONE_DEVICE=1 RT_DIST_BACKEND=gloo RT_BENCH_VERIFY_GATHER=1 timeout -k 10 300 \
+               python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+               --master-port $((29500 + n)) bench.py --gpus $n --steps 10 --warmup 2 > "$OUT/multi_$n.json" 2> "$OUT/multi_$n.err"
+           done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   tail -3 "$OUT"/*.log 2>/dev/null | tail -3 || true

@@ -18,7 +18,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def main(prof_dir, dest):
-    prof_dir, dest = Path(prof_dir), Path(dest)
+    prof_dir, dest = Path(prof_dir).resolve(), Path(dest).resolve()
     dest.mkdir(parents=True, exist_ok=True)
     summ = summarize_prof.main(prof_dir)
     (dest / "summary.json").write_text(json.dumps(summ, indent=1) + "\n")
