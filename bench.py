@@ -9,13 +9,14 @@ frames bracketed by barrier + device synchronize.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 the 1920x1080 image is tile-split across ranks (8x8 tile t -> rank t % N,
-SURVEY §8e). Default "--scaling weak": one step advances the progressive render
-by N frames (N samples per pixel), each rank rendering its 1/N of the tiles for
-all N frames in one fused launch (rt_compute_frames) -- per-GPU work per step is
-one frame's worth at every N, and the image is bit-identical to N sequential
-1-GPU frames. "--scaling strong": one frame per step split N ways. No collective
-runs in the timed loop; one RCCL gather of the accumulated RGBA32F tiles to rank
-0 runs afterwards and is reported separately as gather_ms.
+SURVEY §8e). Default "--scaling weak": the same view rendered at N times the
+pixels -- (1920*sqrt(N)) x (1080*sqrt(N)) rounded to whole 8x8 tiles (N=4 is
+3840x2160) -- so every GPU owns one 1920x1080 frame's worth of tiles at every N
+and each step is still one single-frame launch per GPU (one frame of the job's
+image). "--scaling strong": the 1920x1080 frame split N ways (0.1 ms of work
+per GPU at N=8). No collective runs in the timed loop; one RCCL gather of the
+accumulated RGBA32F tiles to rank 0 runs afterwards and is reported separately
+as gather_ms.
 
 roofline.traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
 (profiles/pmc_traffic.json, FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE), when
@@ -151,17 +152,18 @@ def main() -> int:
     if world > 1:
         dist.barrier()
 
-    scene, default_bounces = build_config(args.config, width=args.width, height=args.height)
+    width, height = args.width, args.height
+    if world > 1 and args.scaling == "weak":
+        scale = world ** 0.5  # same view, N x the pixels: per-GPU work fixed
+        width = int(round(args.width * scale / 8.0)) * 8
+        height = int(round(args.height * scale / 8.0)) * 8
+    scene, default_bounces = build_config(args.config, width=width, height=height)
     bounces = args.bounces or default_bounces
     r = Renderer(scene, device=device, rank=rank, world_size=world)
     owned_px = r.owned_pixel_count()
-    frames_per_step = world if args.scaling == "weak" else 1
 
     def step():
-        if frames_per_step == 1:
-            r.compute_frame(bounces)
-        else:
-            r.compute_frames(bounces, frames_per_step)
+        r.compute_frame(bounces)
 
     def barrier_sync():
         r.synchronize()
@@ -211,7 +213,7 @@ def main() -> int:
         if os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
             # the assembled tile-split image must equal a 1-GPU render of the same frames
             with Renderer(scene, device=device) as ref:
-                for _ in range(frames_per_step * (args.warmup + args.steps)):
+                for _ in range(args.warmup + args.steps):
                     ref.compute_frame(bounces)
                 same = np.array_equal(ref.read_accumulation().view(np.uint32), r.read_accumulation().view(np.uint32))
                 same = same and np.array_equal(ref.read_output(), r.read_output())
@@ -225,8 +227,7 @@ def main() -> int:
         # one launch reads/writes each owned pixel's framebuffer words once, whatever its frame count
         b_launch = algorithmic_bytes(owned_px, rays_per_launch, scene_bytes(scene))
         achieved = b_launch / avg_kernel_s / 1e9
-        workload = (f"{args.config} {args.width}x{args.height}, {bounces} bounces, 1 spp/frame, "
-                    f"{frames_per_step} frame(s) per step, accumulate")
+        workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
         traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
         result = {
             "metric": METRIC,
@@ -243,15 +244,15 @@ def main() -> int:
             "data": "synthetic",
             "config": {
                 "workload": workload,
-                "width": args.width,
-                "height": args.height,
+                "width": width,
+                "height": height,
                 "bounces": bounces,
                 "spheres": int(scene.spheres.shape[0]),
                 "triangles": int(scene.flatten()[2].shape[0]),
                 "parallelism": f"tile{world}" if world > 1 else "single",
-                "frames_per_step": frames_per_step,
+                "pixels_per_gpu": owned_px,
                 "rays_per_step": rays_total / args.steps,
-                "nominal_rays_per_step": args.width * args.height * bounces * frames_per_step,
+                "nominal_rays_per_step": width * height * bounces,
             },
             "roofline": {
                 "bound": "hbm",

@@ -278,10 +278,10 @@ RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t 
 RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
                             uint32_t* scene_in_lds);
 
-/* Diagnostic counters (filled only by builds compiled with -DRT_DIAG, zeros
- * otherwise): out[0..n) receives up to 8 u64 — [0] wave-cycles in the frame
- * loop, [1] in triangle traversal, [2] in sphere traversal, [3] loop
- * iterations — summed over all waves since the last rt_reset_ray_count. */
+/* Diagnostic counters (filled only by builds compiled with -DRT_DIAG or
+ * -DRT_DIAG_TAIL, zeros otherwise): out[0..n) receives up to 8 u64 counters
+ * (tools/diag_split.py, tools/tail_probe.py), then, for n > 8, per-wave
+ * (start, end) real-time stamps of the last launch (-DRT_DIAG_TAIL). */
 RT_API int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* The context's HIP stream (hipStream_t), for callers that want to order

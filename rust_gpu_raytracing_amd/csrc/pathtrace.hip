@@ -309,6 +309,9 @@ __device__ __forceinline__ void trace_step(const SceneView& sv, const KernelArgs
         }
         ts.node = (hit && leaf == 0xffffffffu) ? ts.node + 1u : __float_as_uint(lo.w);
         if (ts.node >= ka.tri_nodes) {
+#ifdef RT_DIAG_TAIL
+            if (ts.nan_hit) atomicAdd(ka.diag + 6, 1ull);
+#endif
             if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
             ts.node = 0;
             ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
@@ -538,18 +541,60 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 
 }  // namespace
 
-// Claim the next local tile for this wave: one atomic per 64 pixels on a
-// monotonically increasing 64-bit counter (ka.tile_base is its value at launch
-// start, so no per-frame reset is needed: a launch performs exactly
-// owned_tiles + waves increments, one failing claim per wave).
-__device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka) {
-    unsigned long long v = 0;
-    if ((threadIdx.x & 63u) == 0) v = atomicAdd(ka.tile_counter, 1ull);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 0);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 0);
-    const uint64_t rel = ((uint64_t)hi << 32 | lo) - ka.tile_base;
-    return rel > 0xffffffffull ? 0xffffffffu : (uint32_t)rel;
+// The tile queue, striped over the XCDs. One device-scope atomic counter on a
+// single address serialises at the memory side (~15 ns per claim measured:
+// that alone capped C1 at 4x below a static schedule). Local tile t belongs to
+// stripe t % S (S = 8, one per XCD, counters 256 B apart); a wave claims from
+// its own XCD's stripe (HW_REG_XCC_ID), and once that is empty steals from the
+// others, checking each with a coherent load before spending an atomic on it.
+// Claims stay dynamic, so expensive tiles still balance across waves. The
+// counters start at zero: each launch zeroes the other half of the
+// double-buffered counter array for the next launch (stream order makes that
+// visible). Lane 0 does the memory operations; results are wave-uniform.
+constexpr uint32_t kQueueStride = 64;  // u32 between stripe counters (256 B)
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
 }
+
+struct TileQueue {
+    uint32_t stripe;  // stripe being drained (wave-uniform)
+    uint32_t tried;   // stripes found empty so far
+};
+
+__device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka, TileQueue& q) {
+    const uint32_t n_str = ka.queue_stripes;
+    const bool leader = (threadIdx.x & 63u) == 0;
+    while (q.tried < n_str) {
+        const uint32_t count = ka.owned_tiles > q.stripe ? (ka.owned_tiles - q.stripe + n_str - 1u) / n_str : 0u;
+        uint32_t* ctr = ka.queue + q.stripe * kQueueStride;
+        bool attempt = true;
+        if (q.tried > 0) {  // stealing: skip stripes that are already drained
+            uint32_t v = 0;
+            if (leader) v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            attempt = __builtin_amdgcn_readlane(v, 0) < count;
+        }
+        if (attempt) {
+            uint32_t old = 0;
+            if (leader) old = atomicAdd(ctr, 1u);
+            old = __builtin_amdgcn_readlane(old, 0);
+            if (old < count) return old * n_str + q.stripe;
+        }
+        q.stripe = q.stripe + 1u == n_str ? 0u : q.stripe + 1u;
+        q.tried += 1;
+    }
+    return 0xffffffffu;
+}
+
+#ifdef RT_DIAG_TAIL
+// Diagnostic build only: wave start/end times (s_memrealtime, 100 MHz, one
+// clock for the whole device) -> ramp and tail of the persistent grid.
+__device__ __forceinline__ unsigned long long realtime() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#endif
 
 #ifdef RT_DIAG
 // Diagnostic build only: wave-level cycle stamps (s_memtime) accumulated per
@@ -720,7 +765,12 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         }
     };
 
-    uint32_t tile = claim_tile(ka);  // wave-uniform
+#ifdef RT_DIAG_TAIL
+    const unsigned long long wave_t0 = realtime();
+#endif
+    if (blockIdx.x == 0 && threadIdx.x < ka.queue_stripes) ka.queue_next[threadIdx.x * kQueueStride] = 0u;
+    TileQueue queue{xcc_id() % ka.queue_stripes, 0u};
+    uint32_t tile = claim_tile(ka, queue);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
 #ifdef RT_DIAG
     unsigned long long iters = 0, trav_cyc = 0, steps = 0, step_lanes = 0, shade_cyc = 0, refill_cyc = 0,
@@ -771,7 +821,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             }
             next += min((uint32_t)__popcll(need), avail);
             if (next == 64u) {
-                tile = claim_tile(ka);
+                tile = claim_tile(ka, queue);
                 next = 0;
             }
         }
@@ -828,6 +878,23 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         atomicAdd(ka.diag + 5, shade_cyc);
         atomicAdd(ka.diag + 6, refill_cyc);
         atomicAdd(ka.diag + 7, setup_cyc);
+    }
+#endif
+#ifdef RT_DIAG_TAIL
+    if ((threadIdx.x & 63u) == 0) {
+        const unsigned long long wave_t1 = realtime();
+        atomicAdd(ka.diag + 0, wave_t1);
+        atomicMax(ka.diag + 1, wave_t1);
+        atomicMax(ka.diag + 2, ~wave_t0);  // min start (counters reset to 0)
+        atomicAdd(ka.diag + 3, 1ull);
+        atomicAdd(ka.diag + 4, wave_t0);
+        atomicMax(ka.diag + 5, wave_t0);
+        atomicMax(ka.diag + 7, wave_t1 - wave_t0);
+        const uint32_t w = blockIdx.x * (kThreads / 64u) + (threadIdx.x >> 6);
+        if (w < 65536u) {
+            ka.diag[8 + 2 * w] = wave_t0;
+            ka.diag[8 + 2 * w + 1] = wave_t1;
+        }
     }
 #endif
     atomicAdd(&block_rays, rays);

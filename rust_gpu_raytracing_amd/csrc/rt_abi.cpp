@@ -51,6 +51,12 @@ constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerat
 // Always staged at the end of the LDS image: the sRGB table (256 floats) and the
 // camera block (inverse projection, inverse view, aspect: 33 floats).
 constexpr size_t kLdsTailBytes = 1024 + 160;
+// Diagnostic builds (-DRT_DIAG_TAIL) record (start, end) per wave after the 8
+// counters: room for 65,536 waves.
+constexpr size_t kDiagWaveRecords = 2 * 65536;
+// Tile queue: one counter per XCD stripe (pathtrace.hip, claim_tile), 256 B apart.
+constexpr uint32_t kQueueStripes = 8;
+constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
 // traversing (pathtrace.hip, step 4 of the kernel loop).
 constexpr uint32_t kDefaultTravThreshold = 8;
@@ -83,8 +89,8 @@ struct rt_ctx {
     float4* d_accum = nullptr;
     uint32_t* d_out = nullptr;
     unsigned long long* d_counter = nullptr;
-    unsigned long long* d_tile_counter = nullptr;
-    unsigned long long tile_base = 0;  // value of *d_tile_counter when the next launch starts
+    uint32_t* d_queue = nullptr;  // 2 x kQueueStripes tile-queue counters, kQueueStride apart
+    uint32_t queue_parity = 0;    // which half the next launch uses (the launch zeroes the other)
     int n_cu = 0;
     bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
     size_t occ_lds_bytes = 0;
@@ -466,8 +472,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
     ctx->k = 1;  // src/renderer.rs:96
 
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
-        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9)) ||
-        (rc = dev_alloc(ctx, &ctx->d_tile_counter, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9 + kDiagWaveRecords)) ||
+        (rc = dev_alloc(ctx, &ctx->d_queue, 2 * kQueueStripes * kQueueStride)) ||
         (rc = dev_alloc(ctx, &ctx->d_slot_sph, 4 * (size_t)info->sphere_count + 4)) ||  // padded groups
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
@@ -501,7 +507,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_tile_counter, ctx->d_slot_sph,
+    void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_queue, ctx->d_slot_sph,
                     ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb};
@@ -676,8 +682,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.output = ctx->d_out;
     ka.ray_counter = ctx->d_counter;
     ka.diag = ctx->d_counter + 1;
-    ka.tile_counter = ctx->d_tile_counter;
-    ka.tile_base = ctx->tile_base;
+    ka.queue = ctx->d_queue + (size_t)ctx->queue_parity * kQueueStripes * kQueueStride;
+    ka.queue_next = ctx->d_queue + (size_t)(ctx->queue_parity ^ 1u) * kQueueStripes * kQueueStride;
+    ka.queue_stripes = kQueueStripes;
     ka.sphere_slots = ctx->d_slot_sph;
     ka.sphere_orig = ctx->d_slot_orig;
     ka.sphere_material = ctx->d_sph_mat;
@@ -810,7 +817,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
     // every tile is claimed once and every wave makes one final failing claim
-    ctx->tile_base += (unsigned long long)ctx->owned_tiles + (unsigned long long)blocks * waves_per_block;
+    ctx->queue_parity ^= 1u;  // this launch zeroes the other half for the next one
     if (ctx->timing) {
         RT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
         ctx->pending.push_back(ev);
@@ -942,10 +949,9 @@ int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_ran
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n) {
     RT_ENTER(ctx);
     if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
-    unsigned long long v[8] = {};
-    RT_HIP(ctx, hipMemcpyAsync(v, ctx->d_counter + 1, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+    const size_t m = std::min<size_t>(n, 8 + kDiagWaveRecords);
+    RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_counter + 1, m * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (uint32_t i = 0; i < n && i < 8; i++) out[i] = v[i];
     return RT_OK;
 }
 

@@ -64,8 +64,8 @@ struct KernelArgs {
     uint32_t* __restrict__ output;
     unsigned long long* __restrict__ ray_counter;
     unsigned long long* __restrict__ diag;          // 8 diagnostic counters (RT_DIAG builds)
-    unsigned long long* __restrict__ tile_counter;  // monotonically increasing tile queue head
-    unsigned long long tile_base;                   // its value at launch start
+    uint32_t* __restrict__ queue;       // this launch's tile-queue stripe counters (zero at launch start)
+    uint32_t* __restrict__ queue_next;  // the next launch's counters, zeroed by this launch
     // scene (bindings 3, 4, 5, 7, 8, 10)
     const float4* __restrict__ sphere_slots;      // centre.xyz, radius*radius (f32), kernel order (sphere_bvh.h)
     const uint32_t* __restrict__ sphere_orig;     // slot -> original sphere index
@@ -121,6 +121,7 @@ struct KernelArgs {
     uint32_t rank;
     uint32_t world_size;
     uint32_t trav_threshold;  // resume shading once at most this many lanes still traverse
+    uint32_t queue_stripes;   // tile-queue stripes (one per XCD)
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;
     uint32_t lds_obj_offset;

@@ -203,10 +203,10 @@ class Renderer:
     def unpack_accumulation(self, src_device_ptr: int, src_rank: int, world_size: int, divisor: int) -> None:
         self._call("rt_unpack_accumulation", ctypes.c_void_p(src_device_ptr), src_rank, world_size, divisor)
 
-    def debug_counters(self) -> list:
-        """RT_DIAG builds only: the 8 diagnostic counters (tools/diag_split.py)."""
-        v = (ctypes.c_uint64 * 8)()
-        N.check(self._ctx, self._lib.rt_debug_counters(self._ctx, v, 8), self._lib)
+    def debug_counters(self, n: int = 8) -> list:
+        """Diagnostic builds only: the 8 counters, then per-wave stamps (include/rt_abi.h)."""
+        v = (ctypes.c_uint64 * n)()
+        N.check(self._ctx, self._lib.rt_debug_counters(self._ctx, v, n), self._lib)
         return list(v)
 
     def launch_config(self) -> dict:

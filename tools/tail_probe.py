@@ -1,0 +1,43 @@
+"""Ramp and tail of the persistent grid, from an RT_DIAG_TAIL build.
+
+usage: RT_LIB=build/ab/lib_tail.so python tools/tail_probe.py [config ...]
+Per launch: first wave start -> mean/last wave start (ramp), mean/last wave end
+(tail), in microseconds of the device's 100 MHz real-time clock.
+"""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from rust_gpu_raytracing_amd import Renderer  # noqa: E402
+from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
+
+for name in sys.argv[1:] or ["c2_rtiow"]:
+    scene, bounces = build_config(name)
+    with Renderer(scene) as r:
+        r.compute_frame(bounces)
+        r.synchronize()
+        res = []
+        for _ in range(5):
+            r.reset_ray_count()  # zeroes the diag counters too
+            r.reset_timing()
+            r.set_timing(True)
+            r.compute_frame(bounces)
+            r.synchronize()
+            r.set_timing(False)
+            kern_ms, _ = r.dispatch_time_total()
+            c = r.debug_counters(8 + 2 * 65536)
+            waves = np.array(c[8:8 + 2 * c[3]], np.float64).reshape(-1, 2)
+            dur = (waves[:, 1] - waves[:, 0]) / 100.0
+            ends = (waves[:, 1] - waves[:, 0].min()) / 100.0
+            n = c[3]
+            t_first = (~np.uint64(c[2])).item()  # stored as the max of ~start
+            res.append({"waves": n, "ramp_mean_us": (c[4] / n - t_first) / 100, "ramp_last_us": (c[5] - t_first) / 100,
+                        "end_mean_us": (c[0] / n - t_first) / 100, "end_last_us": (c[1] - t_first) / 100,
+                        "nan_fallbacks": c[6], "longest_wave_us": c[7] / 100, "kernel_us": kern_ms * 1e3,
+                        "wave_dur_pct": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 99, 100)],
+                        "end_pct": [round(float(np.percentile(ends, q)), 1) for q in (10, 50, 90, 99, 100)]})
+        print(json.dumps({"config": name, "runs": res[1:]}))
