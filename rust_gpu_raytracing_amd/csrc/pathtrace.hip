@@ -544,8 +544,8 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 // The tile queue, striped over the XCDs. One device-scope atomic counter on a
 // single address serialises at the memory side (~15 ns per claim measured:
 // that alone capped C1 at 4x below a static schedule). Local tile t belongs to
-// stripe t % S (S = 8, one per XCD, counters 256 B apart); a wave claims from
-// its own XCD's stripe (HW_REG_XCC_ID), and once that is empty steals from the
+// stripe t % S (S = 32 by default, 4 per XCD, counters 256 B apart); a wave claims from
+// a stripe of its own XCD (HW_REG_XCC_ID), and once that is empty steals from the
 // others, checking each with a coherent load before spending an atomic on it.
 // Claims stay dynamic, so expensive tiles still balance across waves. The
 // counters start at zero: each launch zeroes the other half of the
@@ -769,7 +769,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     const unsigned long long wave_t0 = realtime();
 #endif
     if (blockIdx.x == 0 && threadIdx.x < ka.queue_stripes) ka.queue_next[threadIdx.x * kQueueStride] = 0u;
-    TileQueue queue{xcc_id() % ka.queue_stripes, 0u};
+    // home stripe: this XCD's (blocks are dealt round-robin over the XCDs, so
+    // blockIdx / 8 spreads an XCD's blocks over its stripes when there are more)
+    TileQueue queue{(xcc_id() + 8u * (blockIdx.x >> 3)) % ka.queue_stripes, 0u};
     uint32_t tile = claim_tile(ka, queue);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
 #ifdef RT_DIAG

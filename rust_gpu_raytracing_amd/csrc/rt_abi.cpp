@@ -54,8 +54,11 @@ constexpr size_t kLdsTailBytes = 1024 + 160;
 // Diagnostic builds (-DRT_DIAG_TAIL) record (start, end) per wave after the 8
 // counters: room for 65,536 waves.
 constexpr size_t kDiagWaveRecords = 2 * 65536;
-// Tile queue: one counter per XCD stripe (pathtrace.hip, claim_tile), 256 B apart.
-constexpr uint32_t kQueueStripes = 8;
+// Tile queue: counters per stripe (pathtrace.hip, claim_tile), 256 B apart;
+// kQueueStripes = 4 per XCD by default (measured: C2 0.599 ms at 8, 0.595 at 32; C1
+// 0.076 -> 0.058 ms), up to kQueueStripesMax (RT_QUEUE_STRIPES).
+constexpr uint32_t kQueueStripes = 32;
+constexpr uint32_t kQueueStripesMax = 64;
 constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
 // traversing (pathtrace.hip, step 4 of the kernel loop).
@@ -91,6 +94,7 @@ struct rt_ctx {
     unsigned long long* d_counter = nullptr;
     uint32_t* d_queue = nullptr;  // 2 x kQueueStripes tile-queue counters, kQueueStride apart
     uint32_t queue_parity = 0;    // which half the next launch uses (the launch zeroes the other)
+    uint32_t queue_stripes = kQueueStripes;  // RT_QUEUE_STRIPES (A/B switch)
     int n_cu = 0;
     bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
     size_t occ_lds_bytes = 0;
@@ -457,6 +461,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
         ctx->use_bvh = !(env && env[0] == '0');
+        env = std::getenv("RT_QUEUE_STRIPES");
+        if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TRAV_THRESHOLD");
         if (env) ctx->trav_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
     }
@@ -473,7 +479,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
 
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
         (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9 + kDiagWaveRecords)) ||
-        (rc = dev_alloc(ctx, &ctx->d_queue, 2 * kQueueStripes * kQueueStride)) ||
+        (rc = dev_alloc(ctx, &ctx->d_queue, 2 * kQueueStripesMax * kQueueStride)) ||
         (rc = dev_alloc(ctx, &ctx->d_slot_sph, 4 * (size_t)info->sphere_count + 4)) ||  // padded groups
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
@@ -682,9 +688,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.output = ctx->d_out;
     ka.ray_counter = ctx->d_counter;
     ka.diag = ctx->d_counter + 1;
-    ka.queue = ctx->d_queue + (size_t)ctx->queue_parity * kQueueStripes * kQueueStride;
-    ka.queue_next = ctx->d_queue + (size_t)(ctx->queue_parity ^ 1u) * kQueueStripes * kQueueStride;
-    ka.queue_stripes = kQueueStripes;
+    ka.queue = ctx->d_queue + (size_t)ctx->queue_parity * kQueueStripesMax * kQueueStride;
+    ka.queue_next = ctx->d_queue + (size_t)(ctx->queue_parity ^ 1u) * kQueueStripesMax * kQueueStride;
+    ka.queue_stripes = ctx->queue_stripes;
     ka.sphere_slots = ctx->d_slot_sph;
     ka.sphere_orig = ctx->d_slot_orig;
     ka.sphere_material = ctx->d_sph_mat;
