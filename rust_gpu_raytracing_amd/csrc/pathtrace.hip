@@ -25,6 +25,7 @@
 
 #include <algorithm>
 
+#include "rt_bvh_slab.h"
 #include "rt_device_math.h"
 #include "rt_kernel_args.h"
 
@@ -134,17 +135,6 @@ constexpr float kBvhMarginScale = 4.0e-3f;
 // Triangle side: covers the f32 rounding of the reference's slab test.
 constexpr float kTriMarginScale = 1.0e-5f;
 
-// Slab test of a BVH node box inflated by m on every side (culling only: the
-// margins make it conservative).
-__device__ __forceinline__ void node_slabs(const float4 lo, const float4 hi, f3 o, f3 inv, float m, float& near_t,
-                                           float& far_t) {
-    const float tx0 = (lo.x - m - o.x) * inv.x, tx1 = (hi.x + m - o.x) * inv.x;
-    const float ty0 = (lo.y - m - o.y) * inv.y, ty1 = (hi.y + m - o.y) * inv.y;
-    const float tz0 = (lo.z - m - o.z) * inv.z, tz1 = (hi.z + m - o.z) * inv.z;
-    near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
-    far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
-}
-
 // ray_in_bounds, compute_shader.wgsl:407-419.
 __device__ __forceinline__ bool ray_in_bounds(f3 o, f3 inv, const float* mn, const float* mx) {
     const float tminx = (mn[0] - o.x) * inv.x, tmaxx = (mx[0] - o.x) * inv.x;
@@ -226,7 +216,7 @@ constexpr uint32_t kNoLeaf = 0xffffffffu;
 struct TraceState {
     f3 inv;
     float a4, a2;     // 4*dot(d,d), 2*dot(d,d) (:372-379)
-    float m;          // box inflation of the current phase's BVH
+    SlabRay slab;     // the current phase's BVH slab constants (margin folded in, rt_bvh_slab.h)
     uint32_t node;
     uint32_t phase;
     uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf
@@ -235,10 +225,11 @@ struct TraceState {
     TriHit tri;
 };
 
-__device__ __forceinline__ float phase_margin(const KernelArgs& ka, f3 o, uint32_t phase) {
+__device__ __forceinline__ SlabRay phase_slab(const KernelArgs& ka, f3 o, f3 inv, uint32_t phase) {
     const float r = sqrt_rn(dot(o, o));
-    return phase == 0 ? kTriMarginScale * (r + ka.tri_extent) + 1.0e-30f
-                      : kBvhMarginScale * (r + ka.sphere_extent) + 1.0e-6f;
+    const float m = phase == 0 ? kTriMarginScale * (r + ka.tri_extent) + 1.0e-30f
+                               : kBvhMarginScale * (r + ka.sphere_extent) + 1.0e-6f;
+    return slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
 }
 
 // kTris: the scene has objects (triangles); false compiles the triangle side out.
@@ -265,7 +256,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
         ts.phase = ka.tri_nodes != 0 ? 0u : 1u;
     }
     if (ts.phase == 1 && ka.sphere_nodes == 0) ts.phase = 2;
-    ts.m = phase_margin(ka, o, ts.phase);
+    ts.slab = phase_slab(ka, o, ts.inv, ts.phase);
 }
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
@@ -317,7 +308,7 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
         if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
         ts.node = 0;
         ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
-        ts.m = phase_margin(ka, o, 1);
+        ts.slab = phase_slab(ka, o, ts.inv, 1);
     } else if (ts.node >= ka.sphere_nodes) {
         ts.phase = 2;
     }
@@ -337,7 +328,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     const float4 lo = nodes[2u * ts.node];
     const float4 hi = nodes[2u * ts.node + 1u];
     float near_t, far_t;
-    node_slabs(lo, hi, o, ts.inv, ts.m, near_t, far_t);
+    slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
     // enters the inflated box and is not wholly behind the origin; on the sphere
     // side also not beyond the best sphere or the triangle hit (a sphere wins
     // only when strictly closer, :347)

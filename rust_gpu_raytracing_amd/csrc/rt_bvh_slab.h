@@ -1,0 +1,61 @@
+// rt_bvh_slab.h — the BVH culling slab test, shared by the kernel and the CPU
+// exactness harnesses (tests/cpp/*_exactness.cpp), so both run the same f32
+// arithmetic.
+//
+// Culling only: a node box inflated by a per-ray margin m is tested, and the
+// margin covers the rounding of the reference's own
+// sphere and slab arithmetic with orders of magnitude to spare. This test is
+// therefore free to use its own arithmetic: per axis
+//     t_lo = (lo - m - o) * inv = fma(lo, inv, -(o + m) * inv)
+//     t_hi = (hi + m - o) * inv = fma(hi, inv, -(o - m) * inv)
+// one FMA per plane with the ray constants precomputed, instead of sub, sub,
+// mul. Its error in position units is <= ~u (|lo| + |o| + m) << m.
+// A zero (or denormal) direction component makes 1/d infinite, and an FMA of
+// an infinite slope can produce a NaN for only one of the two planes, which the
+// NaN-ignoring min/max would turn into a false miss; |inv| is therefore capped
+// at 1e30: such a ray moves < 1e-21 along that axis over any parameter range a
+// hit can lie in, and an origin inside the inflated slab by >= m/2 still yields
+// t_lo <= -5e23 <= +5e23 <= t_hi (unconstrained), one outside it an entry far
+// beyond every other axis' exit (a miss) -- a superset of the exact answer.
+#pragma once
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define RT_SLAB_FN __host__ __device__ __forceinline__
+#else
+#define RT_SLAB_FN inline
+#endif
+
+struct SlabRay {
+    float ix, iy, iz;     // 1/d, |.| capped at 1e30
+    float lx, ly, lz;     // -(o + m) * inv
+    float hx, hy, hz;     // -(o - m) * inv
+};
+
+RT_SLAB_FN float slab_cap_inv(float v) { return fabsf(v) > 1e30f ? copysignf(1e30f, v) : v; }
+
+// inv: the ray's 1/d (exact, as the reference computes it); m: the margin.
+RT_SLAB_FN SlabRay slab_ray(float ox, float oy, float oz, float inv_x, float inv_y, float inv_z, float m) {
+    SlabRay r;
+    r.ix = slab_cap_inv(inv_x);
+    r.iy = slab_cap_inv(inv_y);
+    r.iz = slab_cap_inv(inv_z);
+    r.lx = -(ox + m) * r.ix;
+    r.ly = -(oy + m) * r.iy;
+    r.lz = -(oz + m) * r.iz;
+    r.hx = -(ox - m) * r.ix;
+    r.hy = -(oy - m) * r.iy;
+    r.hz = -(oz - m) * r.iz;
+    return r;
+}
+
+// near/far parameters of the inflated box [lo, hi] (min/max ignore NaN operands).
+RT_SLAB_FN void slab_hit(const SlabRay& r, float lox, float loy, float loz, float hix, float hiy, float hiz,
+                         float& near_t, float& far_t) {
+    const float tx0 = fmaf(lox, r.ix, r.lx), tx1 = fmaf(hix, r.ix, r.hx);
+    const float ty0 = fmaf(loy, r.iy, r.ly), ty1 = fmaf(hiy, r.iy, r.hy);
+    const float tz0 = fmaf(loz, r.iz, r.lz), tz1 = fmaf(hiz, r.iz, r.hz);
+    near_t = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+    far_t = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+}

@@ -11,6 +11,7 @@
 #include <random>
 #include <vector>
 
+#include "rt_bvh_slab.h"
 #include "sphere_bvh.h"
 
 static const float F32_MAX_ = 3.4028235e+38f;
@@ -65,15 +66,13 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
     if (n) {
         const float m = (getenv("MARGIN") ? (float)atof(getenv("MARGIN")) : 4.0e-3f) * (std::sqrt(dot(o, o)) + sl.extent) + (getenv("MARGIN") ? 0.0f : 1.0e-6f);
         V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);  // the kernel's slab test
         uint32_t node = 0;
         while (node < n) {
             g_nodes++;
             const SphereBvhNode& nd = sl.nodes[node];
-            float tx0 = (nd.bmin[0] - m - o.x) * inv.x, tx1 = (nd.bmax[0] + m - o.x) * inv.x;
-            float ty0 = (nd.bmin[1] - m - o.y) * inv.y, ty1 = (nd.bmax[1] + m - o.y) * inv.y;
-            float tz0 = (nd.bmin[2] - m - o.z) * inv.z, tz1 = (nd.bmax[2] + m - o.z) * inv.z;
-            float near_t = fmax_nn(fmax_nn(fmin_nn(tx0, tx1), fmin_nn(ty0, ty1)), fmin_nn(tz0, tz1));
-            float far_t = fmin_nn(fmin_nn(fmax_nn(tx0, tx1), fmax_nn(ty0, ty1)), fmax_nn(tz0, tz1));
+            float near_t, far_t;
+            slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], near_t, far_t);
             bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= bt * 1.00001f;
             if (hit && nd.leaf != kSphereBvhInternal) {
                 uint32_t first = nd.leaf & 0xffffffu, cnt = nd.leaf >> 24;

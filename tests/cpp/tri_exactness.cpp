@@ -11,6 +11,7 @@
 #include <cstring>
 #include <vector>
 
+#include "rt_bvh_slab.h"
 #include "sphere_bvh.h"
 
 static const float F32_MAX_ = 3.4028235e+38f;
@@ -84,15 +85,13 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     uint32_t best_seq = 0;
     Res r{F32_MAX_, -1, -1, 0};
     bool nan_hit = false;
+    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
     uint32_t node = 0, n = (uint32_t)A.nodes.size();
     while (node < n) {
         g_nodes++;
         const SphereBvhNode& nd = A.nodes[node];
-        float tx0 = (nd.bmin[0] - m - o.x) * inv.x, tx1 = (nd.bmax[0] + m - o.x) * inv.x;
-        float ty0 = (nd.bmin[1] - m - o.y) * inv.y, ty1 = (nd.bmax[1] + m - o.y) * inv.y;
-        float tz0 = (nd.bmin[2] - m - o.z) * inv.z, tz1 = (nd.bmax[2] + m - o.z) * inv.z;
-        float nt = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmin(tz0, tz1));
-        float ft = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmax(tz0, tz1));
+        float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
+        slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
         bool hit = nt <= ft && ft >= 0.0f;
         if (hit && nd.leaf != kSphereBvhInternal) {
             const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
