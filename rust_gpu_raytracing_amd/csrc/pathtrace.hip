@@ -244,9 +244,19 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
     ts.nan_hit = false;
     ts.node = 0;
     ts.pending = kNoLeaf;
-    // brute-force sphere set: wave-uniform sweep over groups of 4 (a sphere's
-    // own test is exact, so the visiting order is free)
-    for (uint32_t i = 0; i < ka.sphere_always; i += 4u) test_sphere_group(sv, i, o, d, ts.a4, ts.a2, ts.sph);
+    // brute-force sphere set: wave-uniform sweep over groups of 4, then the rest
+    // one by one (a sphere's own test is exact, so the visiting order is free)
+    // (the slots after the set up to the next group boundary are NaN padding:
+    // a remainder of 2-3 spheres takes one group, a lone sphere a single test)
+    uint32_t i = 0;
+    for (; i + 4u <= ka.sphere_always; i += 4u) test_sphere_group(sv, i, o, d, ts.a4, ts.a2, ts.sph);
+    if (ka.sphere_always - i >= 2u) {
+        test_sphere_group(sv, i, o, d, ts.a4, ts.a2, ts.sph);
+    } else if (ka.sphere_always - i == 1u) {
+        float b;
+        const float disc = sphere_disc(sv.sph[i], o, d, ts.a4, b);
+        sphere_candidate(disc, b, ts.a2, sv.orig[i], i, ts.sph);
+    }
     if constexpr (!kTris) {
         ts.phase = 1;
     } else if (!ka.tri_accel) {

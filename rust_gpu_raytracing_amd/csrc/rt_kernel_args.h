@@ -94,7 +94,7 @@ struct KernelArgs {
     uint32_t sphere_count;
     uint32_t object_count;
     uint32_t sphere_slot_count;  // padded slots (groups of 4, sphere_bvh.h)
-    uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force (a multiple of 4)
+    uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)

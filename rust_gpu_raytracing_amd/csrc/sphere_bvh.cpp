@@ -217,8 +217,8 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
     };
     for (uint32_t i = 0; i < count; i++)
         if (!in_bvh[i]) push_slot(i);
-    pad_group();
-    out->n_always = (uint32_t)out->slot_orig.size();
+    out->n_always = (uint32_t)out->slot_orig.size();  // swept in groups of 4, then one by one
+    pad_group();  // BVH leaves start group-aligned
 
     std::vector<Prim> prims;
     double extent = 0.0;
@@ -237,9 +237,11 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
         extent = std::max(extent, ext[i]);
     }
     if (prims.size() < 2) {  // nothing worth a tree: brute-force everything
+        out->slot_sph.resize(4 * out->n_always);
+        out->slot_orig.resize(out->n_always);
         for (const Prim& p : prims) push_slot(p.orig);
-        pad_group();
         out->n_always = (uint32_t)out->slot_orig.size();
+        pad_group();
         return;
     }
     const uint32_t lmax = std::min<uint32_t>(leaf_max ? leaf_max : kSphereBvhLeafMax, kSphereGroup);

@@ -33,10 +33,11 @@ constexpr uint32_t kSphereDummyOrig = 0xffffffffu;
 
 struct SphereSlots {
     // Spheres in kernel order: the brute-force ("always") set first, in
-    // original index order, then the BVH leaves' spheres in leaf order; both
-    // parts padded to whole groups of kSphereGroup slots (at most
+    // original index order (n_always slots, swept in groups of 4 and then one by
+    // one), padding to a group boundary, then the BVH leaves' spheres in leaf
+    // order, each leaf one padded group of kSphereGroup slots (at most
     // 4 * count + 4 slots in all).
-    uint32_t n_always = 0;
+    uint32_t n_always = 0;            // brute-force slots (not padded)
     std::vector<float> slot_sph;        // 4 per slot: centre.xyz, radius*radius
     std::vector<uint32_t> slot_orig;    // original sphere index of each slot
     std::vector<SphereBvhNode> nodes;   // empty when every sphere is brute-forced
