@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -283,6 +283,13 @@ RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* bloc
  * (tools/diag_split.py, tools/tail_probe.py), then, for n > 8, per-wave
  * (start, end) real-time stamps of the last launch (-DRT_DIAG_TAIL). */
 RT_API int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
+
+/* Device self-check of the kernel's fast exact-arithmetic helpers against the
+ * IEEE operations they replace, over every f32 input (current device):
+ * which 0 = sqrt on {+-0} U [2^-96, inf], 1..4 = x / 2pi, x / pi, x / 255,
+ * x / 10. *mismatches = number of differing results (0 = bit-exact),
+ * *first_bad = smallest differing input's bit pattern (0xffffffff if none). */
+RT_API int rt_math_selftest(uint32_t which, uint64_t* mismatches, uint32_t* first_bad);
 
 /* The context's HIP stream (hipStream_t), for callers that want to order
  * their own device work (e.g. an RCCL collective) after a frame. */

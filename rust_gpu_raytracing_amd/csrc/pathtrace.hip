@@ -68,7 +68,7 @@ __device__ __forceinline__ int texel_coord(float c, uint32_t size) {
 
 __device__ __forceinline__ f4 decode_texel(uint32_t texel, const float* srgb) {
     return f4{srgb[texel & 0xffu], srgb[(texel >> 8) & 0xffu], srgb[(texel >> 16) & 0xffu],
-              (float)(texel >> 24) / 255.0f};
+              div_const((float)(texel >> 24), 255.0f, kInv255)};
 }
 
 // check_spheres, compute_shader.wgsl:355-404.
@@ -217,6 +217,7 @@ struct TraceState {
     f3 inv;
     float a4, a2;     // 4*dot(d,d), 2*dot(d,d) (:372-379)
     SlabRay slab;     // the current phase's BVH slab constants (margin folded in, rt_bvh_slab.h)
+    float limit;      // sphere-walk pruning distance: min(best sphere, triangle hit) * 1.00001
     uint32_t node;
     uint32_t phase;
     uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf
@@ -224,6 +225,11 @@ struct TraceState {
     SphereHit sph;
     TriHit tri;
 };
+
+// A sphere must be strictly closer than the best sphere so far and than the
+// triangle hit to win (:347, :391); boxes entered beyond that (with slack for
+// the box-entry rounding) cannot hold the winner. Updated when either changes.
+__device__ __forceinline__ float prune_limit(const TraceState& ts) { return fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f; }
 
 __device__ __forceinline__ SlabRay phase_slab(const KernelArgs& ka, f3 o, f3 inv, uint32_t phase) {
     const float r = sqrt_rn(dot(o, o));
@@ -267,6 +273,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
     }
     if (ts.phase == 1 && ka.sphere_nodes == 0) ts.phase = 2;
     ts.slab = phase_slab(ka, o, ts.inv, ts.phase);
+    ts.limit = prune_limit(ts);
 }
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
@@ -319,6 +326,7 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
         ts.node = 0;
         ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
         ts.slab = phase_slab(ka, o, ts.inv, 1);
+        ts.limit = prune_limit(ts);
     } else if (ts.node >= ka.sphere_nodes) {
         ts.phase = 2;
     }
@@ -343,13 +351,16 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     // side also not beyond the best sphere or the triangle hit (a sphere wins
     // only when strictly closer, :347)
     const bool hit = near_t <= far_t && far_t >= 0.0f &&
-                     (tri || near_t <= fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f);
+                     (tri || near_t <= ts.limit);
     const uint32_t leaf = __float_as_uint(hi.w);
     if (hit && leaf != 0xffffffffu) {
         if constexpr (kTris)
             ts.pending = leaf & 0xffffffu;
         else  // sphere-only scenes: the group is cheap and its hit prunes the rest of the walk
+        {
             test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
+            ts.limit = prune_limit(ts);
+        }
     }
     ts.node = (hit && leaf == 0xffffffffu) ? ts.node + 1u : __float_as_uint(lo.w);
 }
@@ -359,7 +370,10 @@ __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs&
     if (kTris && ts.phase == 0)
         tri_leaf(sv, ka, o, d, ts, ts.pending);
     else
+    {
         test_sphere_group(sv, ts.pending, o, d, ts.a4, ts.a2, ts.sph);
+        ts.limit = prune_limit(ts);
+    }
     ts.pending = kNoLeaf;
 }
 
@@ -396,8 +410,8 @@ __device__ __forceinline__ Hit trace_end(const SceneView& sv, const KernelArgs& 
         const float phi = atan2f_c(-outward.z, outward.x) + kWgslPi;
         h.t = t;
         h.p = p;
-        h.u = phi / kTwoPiWgsl;
-        h.v = theta / kWgslPi;
+        h.u = div_const(phi, kTwoPiWgsl, kInvTwoPiWgsl);  // exact: rt_math_selftest
+        h.v = div_const(theta, kWgslPi, kInvWgslPi);
         h.front_face = dot(d, outward) < 0.0f;
         h.n = h.front_face ? outward : -outward;
         h.material_index = sv.sph_mat[ts.sph.orig];
@@ -420,8 +434,8 @@ __device__ __forceinline__ uint32_t fetch_texture(const KernelArgs& ka, uint32_t
 
 __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb, f3 d) {
     // environment_map_coords, :580-585
-    const float u = 0.5f + atan2f_c(d.z, d.x) / kTwoPiWgsl;
-    const float v = 0.5f + asinf_c(d.y) / kWgslPi;
+    const float u = 0.5f + div_const(atan2f_c(d.z, d.x), kTwoPiWgsl, kInvTwoPiWgsl);
+    const float v = 0.5f + div_const(asinf_c(d.y), kWgslPi, kInvWgslPi);
     const int x = texel_coord(u * (float)(int32_t)ka.env_map_width, ka.env_w);
     const int y = texel_coord(v * (float)(int32_t)ka.env_map_height, ka.env_h);
 #ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
@@ -518,7 +532,7 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
         float ior = m.refraction_index;
         if (h.front_face) ior = 1.0f / ior;
         const float cos_t = fmin_nn(dot(-p.d, h.n), 1.0f);
-        const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
+        const float sin_t = sqrt_rn_nrm(1.0f - cos_t * cos_t);  // 0, >= 2^-24, or NaN
         const bool reflects = ior * sin_t > 1.0f;
         float r0 = (1.0f - ior) / (1.0f + ior);  // specular_percentage, :328-334
         r0 = r0 * r0;
@@ -533,8 +547,9 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
             const f3 perp = (p.d + h.n * cos_t) * ior;
             const float len = sqrt_rn(dot(perp, perp));
             const float len_sq = len * len;
-            const f3 refr = perp + h.n * (-sqrt_rn(__builtin_fabsf(1.0f - len_sq)));
-            p.d = lerp(refr, diffuse, m.roughness / 10.0f);
+            // |1 - len_sq| is 0 or >= 2^-24 (exact difference near 1): sqrt_rn_nrm's domain
+            const f3 refr = perp + h.n * (-sqrt_rn_nrm(__builtin_fabsf(1.0f - len_sq)));
+            p.d = lerp(refr, diffuse, div_const(m.roughness, 10.0f, kInv10));
             p.o = h.p - h.n * 0.0001f;
             tint = true;
         }
@@ -1068,5 +1083,51 @@ hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, 
     const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
     hipLaunchKernelGGL(rt_unpack_tiles_kernel, dim3(blocks), dim3(256), 0, stream, src, accum, output, width, height,
                        tiles_x, owned_tiles, rank, world, divisor);
+    return hipGetLastError();
+}
+
+// Exhaustive device check of the fast exact-arithmetic helpers in
+// rt_device_math.h against the IEEE operations they replace (rt_math_selftest).
+// which: 0 sqrt_rn_nrm over its domain, 1 x / 2pi, 2 x / pi, 3 x / 255, 4 x / 10,
+// each over all 2^32 f32 bit patterns (sqrt: those in its domain).
+extern "C" __global__ void __launch_bounds__(256) rt_math_selftest_kernel(uint32_t which,
+                                                                         unsigned long long* mismatches,
+                                                                         uint32_t* first_bad) {
+    unsigned long long bad = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+        const uint32_t bits = (uint32_t)i;
+        const float x = __uint_as_float(bits);
+        float got, want;
+        if (which == 0) {
+            const float ax = __builtin_fabsf(x);
+            if (ax != 0.0f && ax < 0x1p-96f) continue;  // outside the domain (tiny and denormal)
+            got = sqrt_rn_nrm(x);
+            want = __builtin_sqrtf(x);
+        } else if (which == 1) {
+            got = div_const(x, kTwoPiWgsl, kInvTwoPiWgsl);
+            want = x / kTwoPiWgsl;
+        } else if (which == 2) {
+            got = div_const(x, kWgslPi, kInvWgslPi);
+            want = x / kWgslPi;
+        } else if (which == 3) {
+            got = div_const(x, 255.0f, kInv255);
+            want = x / 255.0f;
+        } else {
+            got = div_const(x, 10.0f, kInv10);
+            want = x / 10.0f;
+        }
+        const bool same = __float_as_uint(got) == __float_as_uint(want) || (got != got && want != want);
+        if (!same) {
+            ++bad;
+            atomicMin(first_bad, bits);
+        }
+    }
+    if (bad) atomicAdd(mismatches, bad);
+}
+
+hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
+                                   hipStream_t stream) {
+    hipLaunchKernelGGL(rt_math_selftest_kernel, dim3(8192), dim3(256), 0, stream, which, mismatches, first_bad);
     return hipGetLastError();
 }

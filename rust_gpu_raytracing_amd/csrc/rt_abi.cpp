@@ -22,6 +22,8 @@
 #include "rt_kernel_args.h"
 #include "sphere_bvh.h"
 
+hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
+                                   hipStream_t stream);
 hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes, uint32_t blocks,
                                hipStream_t stream);
 hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
@@ -974,3 +976,23 @@ int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uin
 void* rt_stream(rt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 }  // extern "C"
+
+int rt_math_selftest(uint32_t which, uint64_t* mismatches, uint32_t* first_bad) {
+    if (!mismatches || !first_bad || which > 4) return RT_E_INVALID;
+    unsigned long long* d_bad = nullptr;
+    uint32_t* d_first = nullptr;
+    hipError_t e = hipMalloc(&d_bad, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&d_first, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(d_bad, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_first, 0xff, sizeof(uint32_t));
+    if (e == hipSuccess) e = rt_launch_math_selftest(which, d_bad, d_first, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    unsigned long long bad = 0;
+    if (e == hipSuccess) e = hipMemcpy(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(first_bad, d_first, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (d_bad) (void)hipFree(d_bad);
+    if (d_first) (void)hipFree(d_first);
+    if (e != hipSuccess) return RT_E_HIP;
+    *mismatches = bad;
+    return RT_OK;
+}

@@ -21,6 +21,11 @@ constexpr float kF32Max = 3.4028235e+38f;   // compute_shader.wgsl:1
 constexpr float kWgslPi = 3.1415926536f;    // compute_shader.wgsl:3 (f32: 3.14159274)
 constexpr float kTwoPiWgsl = 2.0f * kWgslPi;
 constexpr float kBoxMullerTwoPi = 6.2831850051879883f;  // `2.0 * 3.1415926` folded to f32, :624
+// RN(1/c) for div_const (compile-time f32 divisions are correctly rounded)
+constexpr float kInvTwoPiWgsl = 1.0f / kTwoPiWgsl;
+constexpr float kInvWgslPi = 1.0f / kWgslPi;
+constexpr float kInv255 = 1.0f / 255.0f;
+constexpr float kInv10 = 1.0f / 10.0f;
 constexpr float kPiO2 = 1.5707963267948966f;
 constexpr float kPiO4 = 0.7853981633974483f;
 constexpr float kPi = 3.141592653589793f;
@@ -45,6 +50,38 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
 __device__ __forceinline__ float fmin_nn(float a, float b) { return __builtin_fminf(a, b); }
 __device__ __forceinline__ float fmax_nn(float a, float b) { return __builtin_fmaxf(a, b); }
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+
+// Correctly rounded sqrt for x in {+-0} U [2^-96, +inf] (NaN and negative x give
+// NaN): the core of the compiler's IEEE expansion -- hardware v_sqrt_f32, then
+// pick among s - 1ulp, s, s + 1ulp by the sign of the exact FMA residual --
+// without the denormal rescaling and the special-value select the general case
+// needs (16 -> 10 VALU). Used only where the argument is provably in that
+// domain (each call site says why); rt_math_selftest checks it bit for bit
+// against __builtin_sqrtf over every such f32 on the device.
+__device__ __forceinline__ float sqrt_rn_nrm(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x);
+    const float rp = __builtin_fmaf(-sp, s, x);
+    float r = rm <= 0.0f ? sm : s;
+    r = rp > 0.0f ? sp : r;
+    return r;
+}
+
+// x / c for a constant c > 1, correctly rounded: q = x * RN(1/c) corrected once
+// by the exact residual x - q*c (3 VALU + selects instead of the 10-instruction
+// general division). The residual is not exact for quotients near the
+// denormal range, so |x| < 2^-100 (and zeros, for their sign) take the IEEE
+// division, a branch no lane takes in practice. Valid for the constants below
+// only: rt_math_selftest compares it with IEEE x / c for all 2^32 f32 x.
+__device__ __forceinline__ float div_const(float x, float c, float rc) {
+    if (__builtin_fabsf(x) < 0x1p-100f) return x / c;
+    const float q = x * rc;
+    const float r = __builtin_fmaf(-q, c, x);
+    const float q2 = __builtin_fmaf(r, rc, q);
+    return __builtin_isinf(x) ? q : q2;
+}
 __device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / sqrt_rn(dot(v, v))); }
 __device__ __forceinline__ f3 lerp(f3 a, f3 b, float t) { return a + (b - a) * t; }
 
@@ -167,7 +204,7 @@ __device__ __forceinline__ float asinf_c(float x) {
         const bool flag = a > 0.5f;
         if (flag) {
             zz = 0.5f * (1.0f - a);
-            t = sqrt_rn(zz);
+            t = sqrt_rn_nrm(zz);  // zz = (1 - a)/2, a in (0.5, 1]: 0 or a multiple of 2^-25
         } else {
             t = a;
             zz = t * t;
@@ -189,8 +226,9 @@ __device__ __forceinline__ float asinf_c(float x) {
 __device__ __forceinline__ float acosf_c(float x) {
     if (x != x) return x;
     if (x < -1.0f || x > 1.0f) return __uint_as_float(0x7fc00000u);
-    if (x < -0.5f) return kPi - 2.0f * asinf_c(sqrt_rn(0.5f * (1.0f + x)));
-    if (x > 0.5f) return 2.0f * asinf_c(sqrt_rn(0.5f * (1.0f - x)));
+    // the arguments are 0 or multiples of 2^-25 (Sterbenz): sqrt_rn_nrm's domain
+    if (x < -0.5f) return kPi - 2.0f * asinf_c(sqrt_rn_nrm(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * asinf_c(sqrt_rn_nrm(0.5f * (1.0f - x)));
     return kPiO2 - asinf_c(x);
 }
 
@@ -211,7 +249,8 @@ __device__ __forceinline__ float random01(uint32_t& seed) {
 // normal_distribution, compute_shader.wgsl:622-628 (theta drawn before rho).
 __device__ __forceinline__ float normal01(uint32_t& seed) {
     const float theta = kBoxMullerTwoPi * random01(seed);
-    const float rho = sqrt_rn(-2.0f * logf_c(random01(seed)));
+    // -2 log(r), r in {0} U [2^-32, 1]: -0, +inf, or >= 1.1e-7 (sqrt_rn_nrm's domain)
+    const float rho = sqrt_rn_nrm(-2.0f * logf_c(random01(seed)));
     return rho * cosf_c(theta);
 }
 

@@ -326,3 +326,16 @@ def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib):
     rays_o = o.render_frame(scene.params(accumulation_index=1), bounces, acc_o, out_o)
     acc, out, n = gpu_render(scene, bounces, 1, rays=rays)
     assert_same(acc, out, n, acc_o, out_o, rays_o)
+
+
+@pytest.mark.parametrize("which,name", [(0, "sqrt on {0} U [2^-96, inf]"), (1, "x / 2pi"), (2, "x / pi"),
+                                        (3, "x / 255"), (4, "x / 10")])
+def test_gpu_fast_exact_math_selftest(gpu, which, name):
+    """The kernel's short correctly-rounded sqrt and constant divisions equal the IEEE
+    operations bit for bit over every f32 input of their domain (exhaustive, on the device)."""
+    import ctypes
+
+    lib = N.load_library()
+    bad, first = ctypes.c_uint64(), ctypes.c_uint32()
+    assert lib.rt_math_selftest(which, ctypes.byref(bad), ctypes.byref(first)) == 0
+    assert bad.value == 0, (name, bad.value, hex(first.value))
