@@ -126,13 +126,8 @@ __device__ __forceinline__ void test_sphere_group(const SceneView& sv, uint32_t 
     }
 }
 
-// Box inflation per unit of (|o| + extent): covers both the f32 rounding of the
-// discriminant (a float disc >= 0 implies the ray line passes within
-// sqrt(r^2 + 32u|o-C|^2) of the centre, u = 2^-24) and of the near root
-// (|t_f - t| <= ~1.4e-3 |o-C| / |d|), with slack for the slab test's own
-// rounding. DESIGN.md §5.2 has the derivation.
-constexpr float kBvhMarginScale = 4.0e-3f;
-// Triangle side: covers the f32 rounding of the reference's slab test.
+// Sphere side: lateral box inflation and depth slack from sphere_cull_bounds
+// (rt_bvh_slab.h). Triangle side: covers the f32 rounding of the reference's slab test.
 constexpr float kTriMarginScale = 1.0e-5f;
 
 // ray_in_bounds, compute_shader.wgsl:407-419.
@@ -217,7 +212,8 @@ struct TraceState {
     f3 inv;
     float a4, a2;     // 4*dot(d,d), 2*dot(d,d) (:372-379)
     SlabRay slab;     // the current phase's BVH slab constants (margin folded in, rt_bvh_slab.h)
-    float limit;      // sphere-walk pruning distance: min(best sphere, triangle hit) * 1.00001
+    float slack;      // depth slack of the sphere walk (0 on the triangle walk)
+    float limit;      // pruning distance: min(best sphere, triangle hit) * 1.00001 + slack (inf: none)
     uint32_t node;
     uint32_t phase;
     uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf
@@ -228,14 +224,26 @@ struct TraceState {
 
 // A sphere must be strictly closer than the best sphere so far and than the
 // triangle hit to win (:347, :391); boxes entered beyond that (with slack for
-// the box-entry rounding) cannot hold the winner. Updated when either changes.
-__device__ __forceinline__ float prune_limit(const TraceState& ts) { return fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f; }
+// the float near root's deviation, ts.slack) cannot hold the winner. Updated
+// when either changes.
+__device__ __forceinline__ float prune_limit(const TraceState& ts) {
+    return fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f + ts.slack;
+}
 
-__device__ __forceinline__ SlabRay phase_slab(const KernelArgs& ka, f3 o, f3 inv, uint32_t phase) {
+// Slab constants and depth bounds of a BVH walk. The triangle walk culls by
+// box only: no slack, no distance limit.
+__device__ __forceinline__ void phase_setup(const KernelArgs& ka, f3 o, float a, uint32_t phase, TraceState& ts) {
     const float r = sqrt_rn(dot(o, o));
-    const float m = phase == 0 ? kTriMarginScale * (r + ka.tri_extent) + 1.0e-30f
-                               : kBvhMarginScale * (r + ka.sphere_extent) + 1.0e-6f;
-    return slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
+    float m;
+    if (phase == 0) {
+        m = kTriMarginScale * (r + ka.tri_extent) + 1.0e-30f;
+        ts.slack = 0.0f;
+    } else {
+        sphere_cull_bounds(r, ka.sphere_extent, ka.sphere_rmin, ka.sphere_rmax, __builtin_amdgcn_rsqf(a), m,
+                           ts.slack);
+    }
+    ts.slab = slab_ray(o.x, o.y, o.z, ts.inv.x, ts.inv.y, ts.inv.z, m);
+    ts.limit = phase == 0 ? __builtin_inff() : prune_limit(ts);
 }
 
 // kTris: the scene has objects (triangles); false compiles the triangle side out.
@@ -272,8 +280,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
         ts.phase = ka.tri_nodes != 0 ? 0u : 1u;
     }
     if (ts.phase == 1 && ka.sphere_nodes == 0) ts.phase = 2;
-    ts.slab = phase_slab(ka, o, ts.inv, ts.phase);
-    ts.limit = prune_limit(ts);
+    phase_setup(ka, o, a, ts.phase, ts);
 }
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
@@ -325,23 +332,33 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
         if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
         ts.node = 0;
         ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
-        ts.slab = phase_slab(ka, o, ts.inv, 1);
-        ts.limit = prune_limit(ts);
+        phase_setup(ka, o, ts.a2 * 0.5f, 1, ts);
     } else if (ts.node >= ka.sphere_nodes) {
         ts.phase = 2;
     }
 }
 
-// Advances the walk by one BVH node. In scenes with triangles a reached leaf is
-// not tested here but postponed (ts.pending): the wave tests leaves in batches
-// (leaf_step), so the leaf body -- two box tests and up to 7 triangle tests with
-// their global loads, or a sphere group -- runs for many lanes at once instead
-// of for the few lanes that happen to sit on a leaf each step (C3 1.66 -> 1.29
-// ms, C4 3.67 -> 3.39, C5 101 -> 83). Sphere-only scenes test a group at once:
-// postponing it measured slower there (C2 0.593 -> 0.637 ms).
+// Advances the walk by one BVH node. A reached leaf is not tested here but
+// deferred (ts.pending) and the walk goes on past it: the wave tests leaves in
+// batches (leaf_step), so the leaf body -- two box tests and up to 7 triangle
+// tests with their global loads, or a sphere group -- runs for many lanes at
+// once instead of for the few lanes that sit on a leaf in a given step. A lane
+// that reaches a second leaf while one is deferred stays on it until the batch.
+// Testing a leaf late only delays the pruning distance it would set: the result
+// is the lexicographic minimum over the tested primitives either way.
+// Sphere-only scenes test a group on the spot (kDeferLeaves false): deferring
+// measured slower there.
+#ifndef RT_SPHERE_DEFER
+#define RT_SPHERE_DEFER 0
+#endif
+template <bool kTris>
+constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
+
 template <bool kTris>
 __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     const bool tri = kTris && ts.phase == 0;
+    if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
+        return;  // walk over, a leaf still deferred
     const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
     const float4 lo = nodes[2u * ts.node];
     const float4 hi = nodes[2u * ts.node + 1u];
@@ -349,20 +366,19 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
     // enters the inflated box and is not wholly behind the origin; on the sphere
     // side also not beyond the best sphere or the triangle hit (a sphere wins
-    // only when strictly closer, :347)
-    const bool hit = near_t <= far_t && far_t >= 0.0f &&
-                     (tri || near_t <= ts.limit);
+    // only when strictly closer, :347); ts.slack / ts.limit are 0 / inf on the
+    // triangle side
+    const bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
     const uint32_t leaf = __float_as_uint(hi.w);
-    if (hit && leaf != 0xffffffffu) {
-        if constexpr (kTris)
-            ts.pending = leaf & 0xffffffu;
-        else  // sphere-only scenes: the group is cheap and its hit prunes the rest of the walk
-        {
-            test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
-            ts.limit = prune_limit(ts);
-        }
+    const bool at_leaf = hit && leaf != 0xffffffffu;
+    if (at_leaf && !kDeferLeaves<kTris>) {
+        test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
+        ts.limit = prune_limit(ts);
+    } else if (at_leaf) {
+        if (ts.pending != kNoLeaf) return;  // blocked until the batch tests the deferred leaf
+        ts.pending = leaf & 0xffffffu;
     }
-    ts.node = (hit && leaf == 0xffffffffu) ? ts.node + 1u : __float_as_uint(lo.w);
+    ts.node = (hit && !at_leaf) ? ts.node + 1u : __float_as_uint(lo.w);
 }
 
 template <bool kTris>
@@ -908,15 +924,16 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             ++steps;
             step_lanes += (unsigned long long)n_trav;
 #endif
-            // Test the postponed (triangle) leaves once at least half of the
-            // traversing lanes hold one; otherwise advance the others by one node.
+            // Test the deferred leaves once enough of the traversing lanes
+            // hold one (ka.leaf_batch eighths); otherwise advance every lane by
+            // one node.
             bool leaves = false;
-            if constexpr (kTris) {
+            if constexpr (kDeferLeaves<kTris>) {
                 const uint32_t n_pend = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
-                leaves = 2u * n_pend >= n_trav;
+                leaves = 8u * n_pend >= ka.leaf_batch * n_trav;
             }
-            if (mode == kTrav && (ts.pending != kNoLeaf) == leaves) {
-                if (kTris && leaves)
+            if (mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
+                if (kDeferLeaves<kTris> && leaves)
                     leaf_step<kTris>(sv, ka, p.o, p.d, ts);
                 else
                     node_step<kTris>(sv, ka, p.o, p.d, ts);

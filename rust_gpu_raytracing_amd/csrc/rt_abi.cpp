@@ -108,6 +108,7 @@ struct rt_ctx {
     uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
     uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
     uint32_t trav_threshold = kDefaultTravThreshold;  // RT_TRAV_THRESHOLD (A/B switch)
+    uint32_t leaf_batch = 7;                          // RT_LEAF_BATCH, in eighths (A/B switch)
     uint32_t last_blocks = 0, last_lds = 0;
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
@@ -120,6 +121,7 @@ struct rt_ctx {
     uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
     uint32_t n_always = 0, n_nodes = 0, n_slots = 0;
     float sphere_extent = 0.0f;
+    float sphere_rmin = 0.0f, sphere_rmax = 0.0f;
     // triangle accelerator over (object, sub-object) pairs (sphere_bvh.h)
     SphereBvhNode* d_tri_bvh = nullptr;
     SubObjectPrim* d_tri_prims = nullptr;
@@ -255,6 +257,8 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     ctx->n_slots = (uint32_t)sl.slot_orig.size();
     ctx->n_nodes = (uint32_t)sl.nodes.size();
     ctx->sphere_extent = sl.extent;
+    ctx->sphere_rmin = sl.r_min;
+    ctx->sphere_rmax = sl.r_max;
     ctx->slots_dirty = false;
     ctx->slots_count = count;
     return RT_OK;
@@ -467,6 +471,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TRAV_THRESHOLD");
         if (env) ctx->trav_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
+        env = std::getenv("RT_LEAF_BATCH");
+        if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
@@ -700,6 +706,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.sphere_always = ctx->n_always;
     ka.sphere_nodes = ctx->n_nodes;
     ka.sphere_extent = ctx->sphere_extent;
+    ka.sphere_rmin = ctx->sphere_rmin;
+    ka.sphere_rmax = ctx->sphere_rmax;
     ka.tri_accel = (ctx->use_tri_bvh && p.object_count != 0) ? 1u : 0u;
     ka.tri_nodes = ka.tri_accel ? ctx->tri_nodes : 0u;
     ka.tri_prim_count = ka.tri_accel ? ctx->tri_prim_count : 0u;
@@ -746,6 +754,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.rank = ctx->rank;
     ka.world_size = ctx->world;
     ka.trav_threshold = ctx->trav_threshold;
+    ka.leaf_batch = ctx->leaf_batch;
     ka.frames = frames;
 
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb

@@ -50,6 +50,36 @@ RT_SLAB_FN SlabRay slab_ray(float ox, float oy, float oz, float inv_x, float inv
     return r;
 }
 
+// Culling bounds of the sphere BVH for one ray, with X =
+// |o| + extent >= |o - C| for every BVH sphere (centre C, radius r in
+// [r_min, r_max]) and u = 2^-24:
+//
+//  * lateral (position units, the box inflation). The reference's float
+//    discriminant (:372-379) differs from the exact 4|d|^2 (r^2 - p^2) (p = the
+//    distance from C to the ray line) by at most |d|^2 (80u X^2 + 24u r^2) to
+//    first order, so `disc >= 0` implies p^2 <= r^2 (1 + 8u) + 20u X^2, i.e.
+//    p - r <= min(10u X^2 / r, sqrt(20u) X) + 4u r. Taken 4x, plus the
+//    builder's f32 box rounding and this slab test's own (<= ~2u X each, 16u X
+//    allowed).
+//  * slack (parameter units, for the depth tests `far >= -slack` and
+//    `near <= limit + slack`). The float near root lies at most
+//    sqrt(|E|) / (2|d|^2) <= sqrt(20u) (X + r) / |d| (+ ~6u X / |d| of
+//    rounding) before the exact entry point, or -- for a line that misses the
+//    exact sphere but still has disc >= 0 -- before the closest-approach point,
+//    which lies inside the laterally inflated box. Taken 4x.
+//
+// With the RTIOW field (r = 0.2, X ~ 30) the lateral inflation is ~0.011
+// instead of the 0.12 of the r-independent sqrt(u) X bound alone.
+RT_SLAB_FN void sphere_cull_bounds(float olen, float extent, float r_min, float r_max, float inv_dlen,
+                                   float& lateral, float& slack) {
+    const float u = 5.9604645e-8f;  // 2^-24
+    const float X = (olen + extent) * 1.0000005f;
+    const float quad = r_min > 0.0f ? (40.0f * u) * (X * X) / r_min : INFINITY;  // 4 x 10u X^2 / r
+    const float lin = 4.4e-3f * X;                                               // ~4 x sqrt(20u) X
+    lateral = fminf(quad, lin) + (16.0f * u) * X + (16.0f * u) * r_max + 1.0e-6f;
+    slack = (4.4e-3f * (X + r_max) + (32.0f * u) * X) * (inv_dlen * 1.01f) + 1.0e-30f;
+}
+
 // near/far parameters of the inflated box [lo, hi] (min/max ignore NaN operands).
 RT_SLAB_FN void slab_hit(const SlabRay& r, float lox, float loy, float loz, float hix, float hiy, float hiz,
                          float& near_t, float& far_t) {

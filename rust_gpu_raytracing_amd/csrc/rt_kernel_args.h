@@ -97,6 +97,7 @@ struct KernelArgs {
     uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
+    float sphere_rmin, sphere_rmax;  // radius range over BVH spheres (culling bounds, rt_bvh_slab.h)
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)
     uint32_t tri_prim_count;  // triangle BVH leaves
     uint32_t tri_accel;       // 1: use the triangle BVH, 0: the reference's sweep
@@ -121,6 +122,7 @@ struct KernelArgs {
     uint32_t rank;
     uint32_t world_size;
     uint32_t trav_threshold;  // resume shading once at most this many lanes still traverse
+    uint32_t leaf_batch;      // test deferred leaves once 8 * pending >= leaf_batch * traversing
     uint32_t queue_stripes;   // tile-queue stripes (one per XCD)
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;

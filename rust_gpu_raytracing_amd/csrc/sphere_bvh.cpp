@@ -221,12 +221,14 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
     pad_group();  // BVH leaves start group-aligned
 
     std::vector<Prim> prims;
-    double extent = 0.0;
+    double extent = 0.0, r_min = INFINITY, r_max = 0.0;
     for (uint32_t i = 0; i < count; i++) {
         if (!in_bvh[i]) continue;
         const rt_scene_sphere& sp = s[i];
         Prim p;
         const double r = std::fabs((double)sp.radius);
+        r_min = std::min(r_min, r);
+        r_max = std::max(r_max, r);
         for (int k = 0; k < 3; k++) {
             p.c[k] = sp.position[k];
             p.box.lo[k] = p.c[k] - r;
@@ -257,4 +259,7 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
         nd.leaf = slot | (kSphereGroup << 24);
     }
     out->extent = std::nextafter((float)extent, INFINITY);
+    // radii are f32 already: r_min is exact, r_max too (kept as the float value)
+    out->r_min = (float)r_min;
+    out->r_max = (float)r_max;
 }

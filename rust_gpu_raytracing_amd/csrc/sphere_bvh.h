@@ -42,6 +42,7 @@ struct SphereSlots {
     std::vector<uint32_t> slot_orig;    // original sphere index of each slot
     std::vector<SphereBvhNode> nodes;   // empty when every sphere is brute-forced
     float extent = 0.0f;                // max over BVH spheres of |centre| + radius (rounded up)
+    float r_min = 0.0f, r_max = 0.0f;   // radius range over BVH spheres (rounded down / up)
 };
 
 // Build the slot layout for the first `count` spheres. With `use_bvh` false (or

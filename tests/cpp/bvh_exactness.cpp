@@ -58,6 +58,54 @@ static void cand(const SphereSlots& sl, uint32_t slot, V o, V d, float four_a, f
     }
 }
 
+// Experiment (ORDERED=1): ordered stack traversal, both child boxes tested at
+// each internal node, nearer first. g_nodes counts box tests.
+static Res ordered_like(const SphereSlots& sl, V o, V d) {
+    float bt = F32_MAX_;
+    uint32_t bo = 0;
+    bool found = false;
+    float a = dot(d, d), four_a = 4.0f * a, two_a = 2.0f * a;
+    for (uint32_t i = 0; i < sl.n_always; i++) cand(sl, i, o, d, four_a, two_a, bt, bo, found);
+    if (sl.nodes.empty()) return {bt, found ? (int)bo : -1};
+    float lateral, slack;
+    sphere_cull_bounds(std::sqrt(dot(o, o)), sl.extent, sl.r_min, sl.r_max, 1.0f / std::sqrt(a), lateral, slack);
+    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);
+    auto box = [&](uint32_t n, float& nt) {
+        g_nodes++;
+        const SphereBvhNode& nd = sl.nodes[n];
+        float near_t, far_t;
+        slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], near_t, far_t);
+        nt = near_t;
+        return near_t <= far_t && far_t >= -slack && near_t <= bt * 1.00001f + slack;
+    };
+    uint32_t stack[64]; float st[64]; int sp = 0;
+    float nt0;
+    if (!box(0, nt0)) return {bt, found ? (int)bo : -1};
+    stack[sp] = 0; st[sp++] = nt0;
+    while (sp) {
+        --sp;
+        uint32_t n = stack[sp];
+        if (st[sp] > bt * 1.00001f + slack) continue;
+        for (;;) {
+            const SphereBvhNode& nd = sl.nodes[n];
+            if (nd.leaf != kSphereBvhInternal) {
+                uint32_t first = nd.leaf & 0xffffffu, cnt = nd.leaf >> 24;
+                for (uint32_t k = 0; k < cnt; k++) cand(sl, first + k, o, d, four_a, two_a, bt, bo, found);
+                break;
+            }
+            uint32_t l = n + 1, r = sl.nodes[n + 1].skip;
+            float tl, tr;
+            bool hl = box(l, tl), hr = box(r, tr);
+            if (hl && hr) {
+                if (tr < tl) { std::swap(l, r); std::swap(tl, tr); }
+                stack[sp] = r; st[sp++] = tr; n = l;
+            } else if (hl) n = l; else if (hr) n = r; else break;
+        }
+    }
+    return {bt, found ? (int)bo : -1};
+}
+
 static Res kernel_like(const SphereSlots& sl, V o, V d) {
     float bt = F32_MAX_;
     uint32_t bo = 0;
@@ -66,16 +114,21 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
     for (uint32_t i = 0; i < sl.n_always; i++) cand(sl, i, o, d, four_a, two_a, bt, bo, found);
     const uint32_t n = (uint32_t)sl.nodes.size();
     if (n) {
-        const float m = (getenv("MARGIN") ? (float)atof(getenv("MARGIN")) : 4.0e-3f) * (std::sqrt(dot(o, o)) + sl.extent) + (getenv("MARGIN") ? 0.0f : 1.0e-6f);
+        // the kernel's culling bounds (rt_bvh_slab.h); LAT_SCALE / SLACK_SCALE
+        // shrink them to show the check is not vacuous
+        float lateral, slack;
+        sphere_cull_bounds(std::sqrt(dot(o, o)), sl.extent, sl.r_min, sl.r_max, 1.0f / std::sqrt(a), lateral, slack);
+        if (getenv("LAT_SCALE")) lateral *= (float)atof(getenv("LAT_SCALE"));
+        if (getenv("SLACK_SCALE")) slack *= (float)atof(getenv("SLACK_SCALE"));
         V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-        const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);  // the kernel's slab test
+        const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);  // the kernel's slab test
         uint32_t node = 0;
         while (node < n) {
             g_nodes++;
             const SphereBvhNode& nd = sl.nodes[node];
             float near_t, far_t;
             slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], near_t, far_t);
-            bool hit = near_t <= far_t && far_t >= 0.0f && near_t <= bt * 1.00001f;
+            bool hit = near_t <= far_t && far_t >= -slack && near_t <= bt * 1.00001f + slack;
             if (hit && nd.leaf != kSphereBvhInternal) {
                 uint32_t first = nd.leaf & 0xffffffu, cnt = nd.leaf >> 24;
                 for (uint32_t k = 0; k < cnt; k++) cand(sl, first + k, o, d, four_a, two_a, bt, bo, found);
@@ -100,7 +153,7 @@ static int replay(const char* rays_path, const char* sph_path) {
     g_tests = 0;
     while (fread(q, sizeof(q), 1, f) == 1) {
         V o{q[0], q[1], q[2]}, d{q[3], q[4], q[5]};
-        Res a = brute(s, o, d), b = kernel_like(sl, o, d);
+        Res a = brute(s, o, d), b = getenv("ORDERED") ? ordered_like(sl, o, d) : kernel_like(sl, o, d);
         uint32_t ta, tb;
         memcpy(&ta, &a.t, 4);
         memcpy(&tb, &b.t, 4);
@@ -182,7 +235,7 @@ int main(int argc, char** argv) {
         }
         float scale = 0.5f + 2.0f * U(rng);  // non-unit directions (jitter breaks unit length, :219)
         d = {d.x * scale, d.y * scale, d.z * scale};
-        Res a = brute(s, o, d), b = kernel_like(sl, o, d);
+        Res a = brute(s, o, d), b = getenv("ORDERED") ? ordered_like(sl, o, d) : kernel_like(sl, o, d);
         uint32_t ta, tb;
         memcpy(&ta, &a.t, 4);
         memcpy(&tb, &b.t, 4);

@@ -40,12 +40,21 @@ def main():
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     rays_dirs = scene.camera.recalculate_ray_directions()
     rs = []
-    for p in args.libs:
+    import os
+    for spec in args.libs:
+        # "path.so" or "path.so:KNOB=V,KNOB2=V": env knobs are read when the context is created
+        p, _, knobs = spec.partition(":")
+        saved = dict(os.environ)
+        for kv in filter(None, knobs.split(",")):
+            k, _, v = kv.partition("=")
+            os.environ[k] = v
         lib = N.load_library(Path(p).resolve())
         if args.device_rays:
             rs.append(Renderer(scene, lib=lib, device_rays=True))
         else:
             rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib))
+        os.environ.clear()
+        os.environ.update(saved)
     for r in rs:  # warmup
         r.compute_frame(bounces)
         r.synchronize()
