@@ -238,6 +238,19 @@ RT_API int rt_synchronize(rt_ctx* ctx);
 RT_API int rt_read_output(rt_ctx* ctx, uint32_t* rgba8_out);
 RT_API int rt_read_accumulation(rt_ctx* ctx, float* rgba_f32_out);
 
+/* Display readback (Renderer::update_texture + calculate_bytes_per_row,
+ * src/renderer.rs:254-295): the packed RGBA8 output (byte order R, G, B, A:
+ * the Rgba8Unorm texel the reference copies into its display texture) written
+ * row by row into `dst`, each row `bytes_per_row` bytes apart (>= 4*width; the
+ * reference's wgpu copy needs a multiple of 256, which is what forces its
+ * window width to a multiple of 64 pixels, src/main.rs:51-53 -- any pitch
+ * works here). Padding bytes are left untouched. Synchronous. */
+RT_API int rt_read_output_pitched(rt_ctx* ctx, uint8_t* dst, uint32_t bytes_per_row);
+
+/* calculate_bytes_per_row (src/renderer.rs:285-295): 4*width rounded up to
+ * `alignment` (a power of two; the reference uses wgpu's 256). 0 on bad input. */
+RT_API uint32_t rt_bytes_per_row(uint32_t width, uint32_t alignment);
+
 /* Counted ray segments (every trace_ray call: primary + bounce, a path that
  * escapes to the environment stops counting), summed over all dispatches
  * since creation or the last rt_reset_ray_count. Synchronous. */

@@ -107,6 +107,8 @@ SIGNATURES = {
     "rt_synchronize": (ctypes.c_int, [_P]),
     "rt_read_output": (ctypes.c_int, [_P, _P]),
     "rt_read_accumulation": (ctypes.c_int, [_P, _P]),
+    "rt_read_output_pitched": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_bytes_per_row": (_U32, [_U32, _U32]),
     "rt_ray_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_reset_ray_count": (ctypes.c_int, [_P]),
     "rt_accumulation_index": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),

@@ -985,10 +985,13 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 // the size with the most resident waves up to a cap (rt_pathtrace_pick_config).
 // Sphere-only scenes get kernels without the triangle side (fewer live scalar
 // registers: the kernel arguments of the triangle path no longer spill).
+#ifndef RT_EXTRA_CONFIGS  // experiment builds add instances here, e.g. -DRT_EXTRA_CONFIGS(X)="X(1, 640, false)"
+#define RT_EXTRA_CONFIGS(X)
+#endif
 #define RT_FOR_EACH_CONFIG(X)                                                                                   \
     X(0, 256, true) X(0, 512, true) X(0, 1024, true) X(1, 256, true) X(1, 512, true) X(1, 1024, true)           \
     X(2, 256, true) X(2, 512, true) X(2, 1024, true) X(0, 256, false) X(0, 512, false) X(0, 1024, false)        \
-    X(1, 256, false) X(1, 512, false) X(1, 1024, false)
+    X(1, 256, false) X(1, 512, false) X(1, 1024, false) RT_EXTRA_CONFIGS(X)
 
 namespace {
 // Dynamic LDS above 64 KiB must be opted into per kernel.

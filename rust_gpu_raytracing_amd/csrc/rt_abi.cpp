@@ -868,6 +868,23 @@ int rt_read_output(rt_ctx* ctx, uint32_t* out) {
     return RT_OK;
 }
 
+int rt_read_output_pitched(rt_ctx* ctx, uint8_t* dst, uint32_t bytes_per_row) {
+    RT_ENTER(ctx);
+    if (!dst) return fail(ctx, RT_E_INVALID, "dst is NULL");
+    if ((uint64_t)bytes_per_row < 4ull * ctx->width) return fail(ctx, RT_E_INVALID, "bytes_per_row < 4 * width");
+    RT_HIP(ctx, hipMemcpy2DAsync(dst, bytes_per_row, ctx->d_out, 4ull * ctx->width, 4ull * ctx->width, ctx->height,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+uint32_t rt_bytes_per_row(uint32_t width, uint32_t alignment) {
+    if (alignment == 0 || (alignment & (alignment - 1)) != 0) return 0;
+    const uint64_t v = 4ull * width;
+    const uint64_t r = (v + alignment - 1) & ~(uint64_t)(alignment - 1);
+    return r > 0xffffffffull ? 0u : (uint32_t)r;
+}
+
 int rt_read_accumulation(rt_ctx* ctx, float* out) {
     RT_ENTER(ctx);
     if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");

@@ -164,6 +164,22 @@ class Renderer:
         self._call("rt_read_accumulation", N.ptr(out))
         return out
 
+    def update_texture(self, alignment: int = 256) -> np.ndarray:
+        """``Renderer::update_texture`` (src/renderer.rs:254-283), headless: the
+        packed output as the Rgba8Unorm display texture the reference copies it
+        into, one row every ``calculate_bytes_per_row`` bytes (:285-295). Returns
+        the (height, bytes_per_row) u8 staging image; ``image()`` strips the pitch."""
+        bpr = int(self._lib.rt_bytes_per_row(self.width, alignment))
+        if bpr == 0:
+            raise ValueError(f"alignment {alignment} must be a power of two")
+        out = np.zeros((self.height, bpr), np.uint8)
+        self._call("rt_read_output_pitched", N.ptr(out), bpr)
+        return out
+
+    def image(self) -> np.ndarray:
+        """The displayed frame as an (height, width, 4) RGBA8 array (R first)."""
+        return np.ascontiguousarray(self.update_texture()[:, : 4 * self.width].reshape(self.height, self.width, 4))
+
     def ray_count(self) -> int:
         v = ctypes.c_uint64()
         self._call("rt_ray_count", ctypes.byref(v))
