@@ -312,6 +312,71 @@ RT_API void* rt_stream(rt_ctx* ctx);
  * texels with (IEC 61966-2-1, rounded to f32). For tests. */
 RT_API int rt_srgb_table(float out[256]);
 
+/* ---- scene build and edit: src/triangle_object.rs -----
+ *
+ * Host-side restatement of SceneObject (STL file -> placed triangles -> 7-triangle
+ * sub-objects) in f32 with glam's operation order, plus the device-side
+ * rebuild that Renderer::update_scene (src/renderer.rs:153-199) runs after an
+ * edit. Vertices are 9 floats per triangle (a, b, c), in triangle order.
+ * Calls without a context report errors through rt_last_error(NULL). */
+
+/* The edit state of one object (SceneObject::rotation / scale /
+ * transformation, src/triangle_object.rs:39-52): rotation in degrees about
+ * x, y, z (applied as Rz * Ry * Rx, :253-269). 32 bytes. */
+typedef struct rt_object_transform {
+    float rotation[3];
+    float scale;
+    float transformation[3];
+    uint32_t _padding;
+} rt_object_transform;
+
+/* stl_io::read_stl (src/triangle_object.rs:69): binary or ASCII STL bytes.
+ * rt_stl_triangle_count gives the facet count; rt_stl_read writes 9 floats per
+ * facet (normals are ignored, as in the reference). */
+RT_API int rt_stl_triangle_count(const uint8_t* data, size_t size, uint32_t* count);
+RT_API int rt_stl_read(const uint8_t* data, size_t size, float* vertices, uint32_t capacity);
+
+/* SceneObject::new (src/triangle_object.rs:55-127): rotate, normalise to unit
+ * diagonal, scale, drop onto the y = 0 surface, translate to `coordinates`.
+ * Outputs: the normalised points the edit path starts from (9 floats per
+ * triangle), the triangles (SceneTriangle::new), the ObjectInfo (bounds,
+ * material; sub-object fields 0) and the initial edit state (scale 1,
+ * rotation 0, transformation = coordinates + surface drop). */
+RT_API int rt_scene_object_new(const float* stl_vertices, uint32_t triangle_count, float scale,
+                               const float coordinates[3], const float rotation[3], uint32_t material_index,
+                               float* normalized_points, rt_scene_triangle* triangles, rt_object_info* info,
+                               rt_object_transform* state);
+
+/* SceneObject::create_sub_objects (:160-197): chunks of 7 triangles with their
+ * AABBs; `sub_objects` has room for ceil(triangle_count / 7). Sets the
+ * object's first_sub_object_index / sub_object_count. */
+RT_API int rt_scene_object_create_sub_objects(const rt_scene_triangle* triangles, uint32_t triangle_count,
+                                              uint32_t first_sub_object_index, uint32_t first_triangle_index,
+                                              rt_object_info* info, rt_sub_object_info* sub_objects);
+
+/* SceneObject::update_triangles + update_sub_objects (:129-150, :199-220) on
+ * the host: triangles and bounds from the normalised points and `state`.
+ * `sub_objects` holds info->sub_object_count records (bounds rewritten). */
+RT_API int rt_scene_object_update(const float* normalized_points, uint32_t triangle_count,
+                                  const rt_object_transform* state, rt_object_info* info,
+                                  rt_scene_triangle* triangles, rt_sub_object_info* sub_objects);
+
+/* Device-side edit path. rt_set_object_models uploads every object's normalised
+ * points (9 floats per triangle, in the triangle buffer's order; the objects
+ * and sub-objects last set on the context say which triangles belong to which
+ * object). rt_update_objects then runs update_triangles + update_sub_objects
+ * for objects [0, count) on the device -- triangles, sub-object bounds,
+ * object bounds -- and refits the triangle accelerator there, stream-ordered
+ * before the next frame: no host round trip. Asynchronous. */
+RT_API int rt_set_object_models(rt_ctx* ctx, const float* normalized_points, uint32_t triangle_count);
+RT_API int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32_t count);
+
+/* Readback of the scene geometry the kernel sees (after host or device
+ * updates). Triangles come back as full 112-byte records. Synchronous. */
+RT_API int rt_read_triangles(rt_ctx* ctx, rt_scene_triangle* out, uint32_t count);
+RT_API int rt_read_object_info(rt_ctx* ctx, rt_object_info* out, uint32_t count);
+RT_API int rt_read_sub_object_info(rt_ctx* ctx, rt_sub_object_info* out, uint32_t count);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

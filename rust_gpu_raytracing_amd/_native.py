@@ -124,6 +124,16 @@ SIGNATURES = {
     "rt_math_selftest": (ctypes.c_int, [_U32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     "rt_stream": (_P, [_P]),
     "rt_srgb_table": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
+    "rt_stl_triangle_count": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_stl_read": (ctypes.c_int, [_P, ctypes.c_size_t, _P, _U32]),
+    "rt_scene_object_new": (ctypes.c_int, [_P, _U32, ctypes.c_float, _P, _P, _U32, _P, _P, _P, _P]),
+    "rt_scene_object_create_sub_objects": (ctypes.c_int, [_P, _U32, _U32, _U32, _P, _P]),
+    "rt_scene_object_update": (ctypes.c_int, [_P, _U32, _P, _P, _P, _P]),
+    "rt_set_object_models": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_update_objects": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_read_triangles": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_read_object_info": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_read_sub_object_info": (ctypes.c_int, [_P, _P, _U32]),
 }
 
 _lib = None

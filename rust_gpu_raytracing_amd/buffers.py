@@ -85,9 +85,15 @@ SUB_OBJECT_INFO = np.dtype(
     ]
 )
 
+# include/rt_abi.h rt_object_transform -- SceneObject's edit state
+# (rotation in degrees, scale, transformation; src/triangle_object.rs:39-52), 32 B
+OBJECT_TRANSFORM = np.dtype(
+    [("rotation", "<f4", 3), ("scale", "<f4"), ("transformation", "<f4", 3), ("_padding", "<u4")]
+)
+
 for _dt, _size in (
     (PARAMS, 48), (RAY_CAMERA, 16), (RAY, 16), (SPHERE, 32), (TRIANGLE, 112),
-    (MATERIAL, 32), (OBJECT_INFO, 48), (SUB_OBJECT_INFO, 32),
+    (MATERIAL, 32), (OBJECT_INFO, 48), (SUB_OBJECT_INFO, 32), (OBJECT_TRANSFORM, 32),
 ):
     assert _dt.itemsize == _size, (_dt, _size)
 
@@ -134,8 +140,12 @@ def scene_triangles(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
     out["edge_ac"] = edge_ac
     out["calc_normal"] = calc_normal
     out["face_normal"] = normalize_f32(calc_normal)
-    out["min_bounds"] = np.minimum(np.minimum(a, b), c)
-    out["max_bounds"] = np.maximum(np.maximum(a, b), c)
+    # Vec3A::min/max (SSE minps/maxps: `x < y ? x : y`, the second operand on
+    # ties and NaN), chained as a.min(b).min(c)
+    mn = np.where(a < b, a, b)
+    out["min_bounds"] = np.where(mn < c, mn, c)
+    mx = np.where(a > b, a, b)
+    out["max_bounds"] = np.where(mx > c, mx, c)
     return out
 
 

@@ -54,6 +54,7 @@ struct SceneView {
     const float* srgb;        // LDS, 256 entries
     const float4* tri_nodes;  // triangle accelerator nodes (LDS in mode 2, else global)
     const uint4* tri_prims;   // triangle accelerator leaves: object, sub-object, sweep position
+    float tri_extent;         // triangle margin scale (device memory: a device refit updates it)
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -232,11 +233,12 @@ __device__ __forceinline__ float prune_limit(const TraceState& ts) {
 
 // Slab constants and depth bounds of a BVH walk. The triangle walk culls by
 // box only: no slack, no distance limit.
-__device__ __forceinline__ void phase_setup(const KernelArgs& ka, f3 o, float a, uint32_t phase, TraceState& ts) {
+__device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArgs& ka, f3 o, float a, uint32_t phase,
+                                            TraceState& ts) {
     const float r = sqrt_rn(dot(o, o));
     float m;
     if (phase == 0) {
-        m = kTriMarginScale * (r + ka.tri_extent) + 1.0e-30f;
+        m = kTriMarginScale * (r + sv.tri_extent) + 1.0e-30f;
         ts.slack = 0.0f;
     } else {
         sphere_cull_bounds(r, ka.sphere_extent, ka.sphere_rmin, ka.sphere_rmax, __builtin_amdgcn_rsqf(a), m,
@@ -280,7 +282,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
         ts.phase = ka.tri_nodes != 0 ? 0u : 1u;
     }
     if (ts.phase == 1 && ka.sphere_nodes == 0) ts.phase = 2;
-    phase_setup(ka, o, a, ts.phase, ts);
+    phase_setup(sv, ka, o, a, ts.phase, ts);
 }
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
@@ -332,7 +334,7 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
         if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
         ts.node = 0;
         ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
-        phase_setup(ka, o, ts.a2 * 0.5f, 1, ts);
+        phase_setup(sv, ka, o, ts.a2 * 0.5f, 1, ts);
     } else if (ts.node >= ka.sphere_nodes) {
         ts.phase = 2;
     }
@@ -700,7 +702,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     const uint32_t tid = threadIdx.x;
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, ka.objects,
-                 l_srgb,          ka.tri_bvh,     ka.tri_prims};
+                 l_srgb,          ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f};
     if (tid == 0) block_rays = 0;
     if constexpr (kMode >= 1) {
         float4* l_sph = reinterpret_cast<float4*>(lds);

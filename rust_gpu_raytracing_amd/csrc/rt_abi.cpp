@@ -20,6 +20,7 @@
 
 #include "rt_abi.h"
 #include "rt_kernel_args.h"
+#include "rt_scene_math.h"
 #include "sphere_bvh.h"
 
 hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
@@ -28,6 +29,13 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32
                                hipStream_t stream);
 hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
                                     uint32_t* threads, int* blocks_per_cu);
+hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const uint32_t* sub_object,
+                          const uint2* object_tris, const rt_scene::Placement* place, uint32_t object_count,
+                          uint32_t n_tri, uint32_t n_sub, RtTriangleHot* tris, float4* bounds, RtSubObject* subs,
+                          RtObject* objects, hipStream_t stream);
+hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
+                           const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
+                           hipStream_t stream);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
@@ -66,7 +74,13 @@ constexpr uint32_t kQueueStride = 64;
 // traversing (pathtrace.hip, step 4 of the kernel loop).
 constexpr uint32_t kDefaultTravThreshold = 8;
 
+}  // namespace
+
+// The last error of a call without a context (rt_create, the scene builders).
 thread_local std::string g_create_error;
+void rt_set_global_error(const std::string& msg) { g_create_error = msg; }
+
+namespace {
 
 struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
@@ -130,7 +144,21 @@ struct rt_ctx {
     uint32_t tri_count_built = 0xffffffffu;
     bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
     uint32_t tri_nodes = 0, tri_prim_count = 0;
-    float tri_extent = 0.0f;
+    float* d_tri_extent = nullptr;   // margin extent, in device memory (refit updates it)
+    uint32_t* d_tri_order = nullptr; // node indices by depth, deepest level first (refit)
+    uint32_t* d_tri_level_off = nullptr;
+    size_t tri_order_cap = 0, tri_level_cap = 0;
+    uint32_t tri_levels = 0;
+    // device-side edit path (scene_edit.hip): normalised points per triangle,
+    // triangle/sub-object -> object maps, per-object triangle ranges, placements
+    float* d_model = nullptr;
+    uint32_t model_tris = 0;
+    uint32_t* d_tri_object = nullptr;
+    uint32_t* d_sub_object = nullptr;
+    uint2* d_object_tris = nullptr;
+    rt_scene::Placement* d_place = nullptr;
+    float4* d_tri_bounds = nullptr;   // per-triangle min/max (SceneTriangle's host-only fields)
+    bool geom_on_device = false;      // device edits are newer than h_obj / h_sub
     RtMaterial* d_mat = nullptr;
     RtObject* d_obj = nullptr;
     RtSubObject* d_sub = nullptr;
@@ -264,11 +292,29 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     return RT_OK;
 }
 
+// After device-side edits (rt_update_objects) the host copies of the object and
+// sub-object records are stale; read them back before anything host-side uses
+// their bounds.
+int sync_host_geometry(rt_ctx* ctx) {
+    if (!ctx->geom_on_device) return RT_OK;
+    if (!ctx->h_obj.empty())
+        RT_HIP(ctx, hipMemcpyAsync(ctx->h_obj.data(), ctx->d_obj, ctx->h_obj.size() * 48, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    if (!ctx->h_sub.empty())
+        RT_HIP(ctx, hipMemcpyAsync(ctx->h_sub.data(), ctx->d_sub, ctx->h_sub.size() * 32, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->geom_on_device = false;
+    return RT_OK;
+}
+
 // Rebuild the triangle accelerator for the first `object_count` objects when
 // objects or sub-objects changed (the boxes it culls with are theirs).
 int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
     if (!ctx->use_tri_bvh || object_count == 0) return RT_OK;
     if (!ctx->tri_dirty && ctx->tri_count_built == object_count) return RT_OK;
+    int rc0 = sync_host_geometry(ctx);
+    if (rc0) return rc0;
     TriangleAccel acc;
     build_triangle_accel(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(), &acc);
     auto ensure = [&](void** p, size_t* cap, size_t bytes) -> int {
@@ -291,7 +337,28 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         return rc;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
     ctx->tri_prim_count = (uint32_t)acc.prims.size();
-    ctx->tri_extent = acc.extent;
+    // depth levels for the device refit (preorder: a node precedes its children)
+    std::vector<uint32_t> depth(acc.nodes.size(), 0);
+    uint32_t max_depth = 0;
+    for (size_t i = 0; i < acc.nodes.size(); i++) {
+        max_depth = std::max(max_depth, depth[i]);
+        if (acc.nodes[i].leaf == kSphereBvhInternal) {
+            depth[i + 1] = depth[i] + 1;
+            depth[acc.nodes[i + 1].skip] = depth[i] + 1;
+        }
+    }
+    std::vector<uint32_t> off(max_depth + 2, 0), order(acc.nodes.size());
+    for (uint32_t d : depth) off[max_depth - d + 1]++;  // deepest level first
+    for (size_t l = 1; l < off.size(); l++) off[l] += off[l - 1];
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (size_t i = 0; i < acc.nodes.size(); i++) order[fill[max_depth - depth[i]]++] = (uint32_t)i;
+    if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_order), &ctx->tri_order_cap, order.size() * 4)) ||
+        (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_level_off), &ctx->tri_level_cap, off.size() * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_tri_order, order.data(), order.size() * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_tri_level_off, off.data(), off.size() * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_tri_extent, &acc.extent, 4)))
+        return rc;
+    ctx->tri_levels = max_depth + 1;
     ctx->tri_dirty = false;
     ctx->tri_count_built = object_count;
     return RT_OK;
@@ -311,7 +378,16 @@ int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
         hot[i].calc_normal = make_float4(s.calc_normal[0], s.calc_normal[1], s.calc_normal[2], 0.f);
         hot[i].face_normal = make_float4(s.face_normal[0], s.face_normal[1], s.face_normal[2], 0.f);
     }
-    return staged_copy(ctx, ctx->d_tri, (size_t)n * sizeof(RtTriangleHot));
+    if ((rc = staged_copy(ctx, ctx->d_tri, (size_t)n * sizeof(RtTriangleHot))) ||
+        (rc = staging(ctx, (size_t)n * 32, &p)))
+        return rc;
+    float4* b = static_cast<float4*>(p);
+    for (uint32_t i = 0; i < n; i++) {
+        const rt_scene_triangle& s = t[i];
+        b[2 * i] = make_float4(s.min_bounds[0], s.min_bounds[1], s.min_bounds[2], 0.f);
+        b[2 * i + 1] = make_float4(s.max_bounds[0], s.max_bounds[1], s.max_bounds[2], 0.f);
+    }
+    return staged_copy(ctx, ctx->d_tri_bounds, (size_t)n * 32);
 }
 
 // Index ranges the kernel walks must lie inside the buffers (the reference's
@@ -494,6 +570,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         (rc = dev_alloc(ctx, &ctx->d_bvh, 2 * (size_t)info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
+        (rc = dev_alloc(ctx, &ctx->d_tri_bounds, 2 * (size_t)ctx->n_tri_dev)) ||
+        (rc = dev_alloc(ctx, &ctx->d_tri_extent, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_srgb, 256)) || (rc = dev_alloc(ctx, &ctx->d_tex, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_env, 1)))
         return bail(rc);
@@ -524,7 +602,8 @@ void rt_destroy(rt_ctx* ctx) {
     void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_queue, ctx->d_slot_sph,
                     ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
-                    ctx->d_srgb};
+                    ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
+                    ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -641,6 +720,8 @@ int rt_update_object_info(rt_ctx* ctx, const rt_object_info* objects, uint32_t c
     RT_ENTER(ctx);
     if (count && !objects) return fail(ctx, RT_E_INVALID, "objects is NULL");
     if (count > ctx->cap_obj) return fail(ctx, RT_E_CAPACITY, "more objects than the buffer holds");
+    int rc0 = sync_host_geometry(ctx);
+    if (rc0) return rc0;
     std::vector<rt_object_info> saved = ctx->h_obj;
     std::copy(objects, objects + count, ctx->h_obj.begin());
     int rc = validate_ranges(ctx);
@@ -656,6 +737,8 @@ int rt_update_sub_object_info(rt_ctx* ctx, const rt_sub_object_info* sub_objects
     RT_ENTER(ctx);
     if (count && !sub_objects) return fail(ctx, RT_E_INVALID, "sub_objects is NULL");
     if (count > ctx->cap_sub) return fail(ctx, RT_E_CAPACITY, "more sub-objects than the buffer holds");
+    int rc0 = sync_host_geometry(ctx);
+    if (rc0) return rc0;
     std::vector<rt_sub_object_info> saved = ctx->h_sub;
     std::copy(sub_objects, sub_objects + count, ctx->h_sub.begin());
     int rc = validate_ranges(ctx);
@@ -711,7 +794,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tri_accel = (ctx->use_tri_bvh && p.object_count != 0) ? 1u : 0u;
     ka.tri_nodes = ka.tri_accel ? ctx->tri_nodes : 0u;
     ka.tri_prim_count = ka.tri_accel ? ctx->tri_prim_count : 0u;
-    ka.tri_extent = ctx->tri_extent;
+    ka.tri_extent = ctx->d_tri_extent;
     ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
     ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);
     ka.materials = ctx->d_mat;
@@ -883,6 +966,125 @@ uint32_t rt_bytes_per_row(uint32_t width, uint32_t alignment) {
     const uint64_t v = 4ull * width;
     const uint64_t r = (v + alignment - 1) & ~(uint64_t)(alignment - 1);
     return r > 0xffffffffull ? 0u : (uint32_t)r;
+}
+
+// ---- device-side edit path (scene_edit.hip) --------------------------------
+
+int rt_set_object_models(rt_ctx* ctx, const float* points, uint32_t triangle_count) {
+    RT_ENTER(ctx);
+    if (triangle_count && !points) return fail(ctx, RT_E_INVALID, "normalized_points is NULL");
+    if (triangle_count > ctx->cap_tri) return fail(ctx, RT_E_CAPACITY, "more triangles than the buffer holds");
+    int rc = sync_host_geometry(ctx);
+    if (rc) return rc;
+    // triangle -> object and sub-object -> object maps, per-object triangle ranges
+    const uint32_t n_obj = (uint32_t)ctx->h_obj.size(), n_sub = (uint32_t)ctx->h_sub.size();
+    std::vector<uint32_t> tri_obj(std::max<uint32_t>(triangle_count, 1), 0xffffffffu);
+    std::vector<uint32_t> sub_obj(std::max<uint32_t>(n_sub, 1), 0xffffffffu);
+    std::vector<uint2> obj_tris(std::max<uint32_t>(n_obj, 1), make_uint2(0, 0));
+    for (uint32_t o = 0; o < n_obj; o++) {
+        const rt_object_info& ob = ctx->h_obj[o];
+        uint32_t first = 0, count = 0;
+        for (uint32_t i = 0; i < ob.sub_object_count; i++) {
+            const uint32_t si = ob.first_sub_object_index + i;
+            const rt_sub_object_info& so = ctx->h_sub[si];
+            if (count == 0) first = so.first_triangle_index;
+            if (so.triangle_count && so.first_triangle_index != first + count)
+                return fail(ctx, RT_E_INVALID, "object " + std::to_string(o) + ": sub-object triangles not contiguous");
+            if ((uint64_t)so.first_triangle_index + so.triangle_count > triangle_count)
+                return fail(ctx, RT_E_INVALID, "object " + std::to_string(o) + " has triangles without model points");
+            sub_obj[si] = o;
+            for (uint32_t t = 0; t < so.triangle_count; t++) tri_obj[so.first_triangle_index + t] = o;
+            count += so.triangle_count;
+        }
+        obj_tris[o] = make_uint2(first, count);
+    }
+    auto alloc = [&](auto** p, size_t count) -> int {
+        if (*p) return RT_OK;
+        return dev_alloc(ctx, p, count);
+    };
+    if ((rc = alloc(&ctx->d_model, 9 * (size_t)ctx->n_tri_dev)) || (rc = alloc(&ctx->d_tri_object, ctx->n_tri_dev)) ||
+        (rc = alloc(&ctx->d_sub_object, ctx->n_sub_dev)) || (rc = alloc(&ctx->d_object_tris, std::max(ctx->cap_obj, 1u))) ||
+        (rc = alloc(&ctx->d_place, std::max(ctx->cap_obj, 1u))) ||
+        (rc = upload_raw(ctx, ctx->d_model, points, (size_t)triangle_count * 36)) ||
+        (rc = upload_raw(ctx, ctx->d_tri_object, tri_obj.data(), (size_t)triangle_count * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_sub_object, sub_obj.data(), (size_t)n_sub * 4)) ||
+        (rc = upload_raw(ctx, ctx->d_object_tris, obj_tris.data(), (size_t)n_obj * 8)))
+        return rc;
+    ctx->model_tris = triangle_count;
+    return RT_OK;
+}
+
+int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !transforms) return fail(ctx, RT_E_INVALID, "transforms is NULL");
+    if (count > ctx->h_obj.size()) return fail(ctx, RT_E_CAPACITY, "more transforms than objects");
+    if (count == 0) return RT_OK;
+    if (!ctx->d_model) return fail(ctx, RT_E_INVALID, "rt_set_object_models has not been called");
+    void* p;
+    int rc = staging(ctx, (size_t)count * sizeof(rt_scene::Placement), &p);
+    if (rc) return rc;
+    rt_scene::Placement* pl = static_cast<rt_scene::Placement*>(p);
+    for (uint32_t o = 0; o < count; o++)
+        rt_scene::placement(*reinterpret_cast<const rt_scene::ObjectTransform*>(&transforms[o]), pl[o]);
+    if ((rc = staged_copy(ctx, ctx->d_place, (size_t)count * sizeof(rt_scene::Placement)))) return rc;
+    RT_HIP(ctx, rt_launch_edit(ctx->d_model, ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place,
+                               count, ctx->model_tris, (uint32_t)ctx->h_sub.size(), ctx->d_tri, ctx->d_tri_bounds,
+                               ctx->d_sub, ctx->d_obj, ctx->stream));
+    ctx->geom_on_device = true;
+    // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds
+    if (ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty)
+        RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,
+                                    ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
+    return RT_OK;
+}
+
+int rt_read_triangles(rt_ctx* ctx, rt_scene_triangle* out, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    if (count > ctx->cap_tri) return fail(ctx, RT_E_CAPACITY, "more triangles than the buffer holds");
+    if (count == 0) return RT_OK;
+    std::vector<RtTriangleHot> hot(count);
+    std::vector<float4> b(2 * (size_t)count);
+    RT_HIP(ctx, hipMemcpyAsync(hot.data(), ctx->d_tri, (size_t)count * 80, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipMemcpyAsync(b.data(), ctx->d_tri_bounds, (size_t)count * 32, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    auto put = [](float* dst, const float4& v) {
+        dst[0] = v.x;
+        dst[1] = v.y;
+        dst[2] = v.z;
+    };
+    for (uint32_t i = 0; i < count; i++) {
+        rt_scene_triangle& t = out[i];
+        std::memset(&t, 0, sizeof(t));
+        put(t.a, hot[i].a);
+        put(t.edge_ab, hot[i].edge_ab);
+        put(t.edge_ac, hot[i].edge_ac);
+        put(t.calc_normal, hot[i].calc_normal);
+        put(t.face_normal, hot[i].face_normal);
+        put(t.min_bounds, b[2 * i]);
+        put(t.max_bounds, b[2 * i + 1]);
+    }
+    return RT_OK;
+}
+
+int rt_read_object_info(rt_ctx* ctx, rt_object_info* out, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    if (count > ctx->cap_obj) return fail(ctx, RT_E_CAPACITY, "more objects than the buffer holds");
+    if (count == 0) return RT_OK;
+    RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_obj, (size_t)count * 48, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_read_sub_object_info(rt_ctx* ctx, rt_sub_object_info* out, uint32_t count) {
+    RT_ENTER(ctx);
+    if (count && !out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    if (count > ctx->cap_sub) return fail(ctx, RT_E_CAPACITY, "more sub-objects than the buffer holds");
+    if (count == 0) return RT_OK;
+    RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_sub, (size_t)count * 32, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
 }
 
 int rt_read_accumulation(rt_ctx* ctx, float* out) {

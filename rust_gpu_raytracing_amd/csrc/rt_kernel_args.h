@@ -101,7 +101,7 @@ struct KernelArgs {
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)
     uint32_t tri_prim_count;  // triangle BVH leaves
     uint32_t tri_accel;       // 1: use the triangle BVH, 0: the reference's sweep
-    float tri_extent;         // max |coordinate| over sub-object boxes (margin scale)
+    const float* __restrict__ tri_extent;  // max |coordinate| over sub-object boxes (margin scale), device memory
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     uint32_t texture_width;

@@ -9,7 +9,8 @@ reference (src/renderer.rs)                  here
 ``Renderer::new`` :42-101                    ``Renderer(scene, ...)`` -> ``rt_create`` +
                                              ``rt_upload_textures`` + ``rt_upload_env_map``
 ``reset_accumulation`` :131-151              ``reset_accumulation()`` -> ``rt_reset_accumulation``
-``update_scene`` :153-199                    ``update_scene()`` -> ``rt_update_*``
+``update_scene`` :153-199                    ``update_scene()`` -> ``rt_update_*``, or
+                                             ``update_scene(device=True)`` -> ``rt_update_objects``
 ``compute_frame`` :201-252                   ``compute_frame(bounces)`` -> ``rt_compute_frame``
 ``on_update`` (camera moved) :109-129        ``update_camera(camera)``
 (no readback in the reference)               ``read_output`` / ``read_accumulation``
@@ -108,19 +109,63 @@ class Renderer:
         p = N.params_struct(self._params(accumulation_index=1))
         self._call("rt_reset_accumulation", ctypes.byref(p))
 
-    def update_scene(self) -> None:
-        """src/renderer.rs:153-199: reset, then re-upload spheres, textures, env map,
-        triangles, objects, sub-objects and materials."""
+    def update_scene(self, device: bool = False) -> None:
+        """src/renderer.rs:153-199: reset, re-upload spheres, rebuild every object's
+        triangles from its edit state (update_triangles + update_sub_objects,
+        src/triangle_object.rs:129-150, :199-220), re-upload textures, env map,
+        triangles, objects, sub-objects and materials.
+
+        ``device=False`` rebuilds the objects on the host (native builder,
+        bit-identical to scene.py) and uploads them, as the reference does.
+        ``device=True`` runs the rebuild on the GPU instead (``update_objects``):
+        nothing but the 32-B edit state per object crosses PCIe, and the host
+        ``scene.objects`` records are left as they were."""
+        from . import builder
+
         self.reset_accumulation()
         s = self.scene
         self._call("rt_update_spheres", N.ptr(s.spheres), s.spheres.shape[0])
         self._upload_textures()
-        objs, subs, tris = s.flatten()
-        self._keep[3:6] = [tris, objs, subs]
-        self._call("rt_update_triangles", N.ptr(tris), tris.shape[0])
-        self._call("rt_update_object_info", N.ptr(objs), objs.shape[0])
-        self._call("rt_update_sub_object_info", N.ptr(subs), subs.shape[0])
+        if device:
+            self.update_objects()
+        else:
+            for o in s.objects:
+                builder.update_object(o, lib=self._lib)
+            objs, subs, tris = s.flatten()
+            self._keep[3:6] = [tris, objs, subs]
+            self._call("rt_update_triangles", N.ptr(tris), tris.shape[0])
+            self._call("rt_update_object_info", N.ptr(objs), objs.shape[0])
+            self._call("rt_update_sub_object_info", N.ptr(subs), subs.shape[0])
         self._call("rt_update_materials", N.ptr(s.materials), s.materials.shape[0])
+
+    def upload_object_models(self) -> None:
+        """The objects' normalised points (rt_set_object_models), once, for device-side edits."""
+        pts = [np.asarray(o.normalized_points, np.float32).reshape(-1, 9) for o in self.scene.objects]
+        self._models = np.ascontiguousarray(np.concatenate(pts) if pts else np.zeros((0, 9), np.float32))
+        self._call("rt_set_object_models", N.ptr(self._models), self._models.shape[0])
+
+    def update_objects(self) -> None:
+        """update_triangles + update_sub_objects for every object, on the device
+        (rt_update_objects): triangles, object and sub-object bounds rebuilt and
+        the triangle accelerator refitted, stream-ordered before the next frame."""
+        from . import builder
+
+        if getattr(self, "_models", None) is None:
+            self.upload_object_models()
+        t = np.ascontiguousarray(np.stack([builder.transform_of(o) for o in self.scene.objects])) \
+            if self.scene.objects else np.zeros(0, B.OBJECT_TRANSFORM)
+        self._call("rt_update_objects", N.ptr(t), t.shape[0])
+
+    def read_geometry(self):
+        """(objects, sub-objects, triangles) as the device holds them (rt_read_*)."""
+        objs, subs, tris = self.scene.flatten()
+        o = np.zeros(objs.shape[0], B.OBJECT_INFO)
+        so = np.zeros(subs.shape[0], B.SUB_OBJECT_INFO)
+        t = np.zeros(tris.shape[0], B.TRIANGLE)
+        self._call("rt_read_object_info", N.ptr(o), o.shape[0])
+        self._call("rt_read_sub_object_info", N.ptr(so), so.shape[0])
+        self._call("rt_read_triangles", N.ptr(t), t.shape[0])
+        return o, so, t
 
     def _set_camera_matrices(self, camera) -> None:
         self._inv = [np.ascontiguousarray(camera.inverse_projection, np.float32).reshape(16),

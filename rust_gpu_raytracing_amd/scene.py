@@ -78,12 +78,26 @@ def rotation_matrix(rotation_deg) -> np.ndarray:
     return _mat3_mul(_mat3_mul(mz, my), mx)
 
 
+_F32_MAX = np.float32(np.finfo(np.float32).max)
+
+
+def _sequential_extreme(col: np.ndarray, lower: bool) -> np.float32:
+    """One axis of get_bounding_box's scan: start at +-f32::MAX and replace on a
+    strict `<` (`>`), so NaN and values beyond the start never win and of equal
+    values (+0 / -0) the first one in point order is kept."""
+    cand = col[col < _F32_MAX] if lower else col[col > -_F32_MAX]
+    if cand.size == 0:
+        return _F32_MAX if lower else -_F32_MAX
+    m = cand.min() if lower else cand.max()
+    return cand[np.argmax(cand == m)]
+
+
 def bounding_box(points: np.ndarray):
-    """``get_bounding_box`` (src/triangle_object.rs:292-321)."""
-    if points.shape[0] == 0:
-        big = np.finfo(np.float32).max
-        return np.full(3, big, np.float32), np.full(3, -big, np.float32)
-    return points.min(axis=0).astype(np.float32), points.max(axis=0).astype(np.float32)
+    """``get_bounding_box`` (src/triangle_object.rs:292-321), bit for bit."""
+    pts = np.asarray(points, np.float32).reshape(-1, 3)
+    mn = np.array([_sequential_extreme(pts[:, k], True) for k in range(3)], np.float32)
+    mx = np.array([_sequential_extreme(pts[:, k], False) for k in range(3)], np.float32)
+    return mn, mx
 
 
 # --------------------------------------------------------------------------- objects
@@ -91,11 +105,23 @@ def bounding_box(points: np.ndarray):
 
 @dataclass
 class SceneObject:
-    """src/triangle_object.rs:39-52 (only what the GPU buffers need)."""
+    """src/triangle_object.rs:39-52.
+
+    ``normalized_points`` are the model's vertices after normalize_model and
+    scale_model (before the drop to the surface), one (3, 3) block per triangle
+    in triangle order (the reference keeps a deduplicated vertex list plus
+    ``point_indexes``; the vertices are the same). ``rotation`` (degrees),
+    ``scale`` and ``transformation`` are the edit state that
+    ``update_triangles`` applies (:129-150)."""
 
     object_info: np.ndarray  # OBJECT_INFO record
     triangles: np.ndarray  # TRIANGLE records
     sub_object_info: np.ndarray = field(default_factory=lambda: np.zeros(0, B.SUB_OBJECT_INFO))
+    normalized_points: np.ndarray = field(default_factory=lambda: np.zeros((0, 3), np.float32))
+    rotation: np.ndarray = field(default_factory=lambda: np.zeros(3, np.float32))
+    scale: np.float32 = np.float32(1.0)
+    transformation: np.ndarray = field(default_factory=lambda: np.zeros(3, np.float32))
+    n_sub_object_triangles: int = SUB_OBJECT_TRIANGLES
 
     @classmethod
     def from_triangles(cls, tri_vertices: np.ndarray, scale: float, coordinates, rotation, material_index: int):
@@ -112,9 +138,10 @@ class SceneObject:
         pts = (pts * s - average * s).astype(np.float32)
         # scale_model, :278-283
         pts = (pts * f32(scale)).astype(np.float32)
+        scaled = pts.copy()
         mn, mx = bounding_box(pts)
         # transform_points_to_surface, :323-331
-        surface = np.array([0.0, -mx[1], 0.0], np.float32)
+        surface = ((-mx) * np.array([0, 1, 0], np.float32)).astype(np.float32)  # -max * Vec3A::Y
         pts = (pts + surface).astype(np.float32)
         coords = np.asarray(coordinates, np.float32)
         pts = (pts + coords).astype(np.float32)
@@ -127,7 +154,40 @@ class SceneObject:
         info["min_bounds"] = mn
         info["max_bounds"] = mx
         info["material_index"] = material_index
-        return cls(info, tris)
+        # :114-126: scale 1, rotation 0, transformation = coordinates + surface drop
+        return cls(info, tris, normalized_points=scaled, scale=f32(1.0), rotation=np.zeros(3, np.float32),
+                   transformation=(coords + surface).astype(np.float32))
+
+    def update_triangles(self):
+        """src/triangle_object.rs:129-150: rotate the normalised points to
+        ``rotation``, scale, translate; new object bounds and triangles."""
+        pts = _mat3_mul_vec(rotation_matrix(self.rotation), self.normalized_points)
+        pts = (pts * f32(self.scale)).astype(np.float32)
+        pts = (pts + np.asarray(self.transformation, np.float32)).astype(np.float32)
+        mn, mx = bounding_box(pts)
+        self.object_info["min_bounds"] = mn
+        self.object_info["max_bounds"] = mx
+        v = pts.reshape(-1, 3, 3)
+        self.triangles = B.scene_triangles(v[:, 0], v[:, 1], v[:, 2])
+
+    def update_sub_objects(self):
+        """src/triangle_object.rs:199-220: sub-object AABBs from the current triangles."""
+        n = self.n_sub_object_triangles
+        for k in range(self.sub_object_info.shape[0]):
+            chunk = self.triangles[k * n:(k + 1) * n]
+            allb = np.stack([chunk["min_bounds"], chunk["max_bounds"]], axis=1).reshape(-1, 3)
+            mn, mx = bounding_box(allb)
+            self.sub_object_info[k]["min_bounds"] = mn
+            self.sub_object_info[k]["max_bounds"] = mx
+
+    def set_model_to_surface(self):
+        """src/triangle_object.rs:149-154 (``max_bounds * Vec3A::Y``, elementwise in f32)."""
+        y = (np.asarray(self.object_info["max_bounds"], np.float32) * np.array([0, 1, 0], np.float32)).astype(np.float32)
+        self.transformation = (np.asarray(self.transformation, np.float32) - y).astype(np.float32)
+
+    def reset_rotation(self):
+        """src/triangle_object.rs:156-158."""
+        self.rotation = np.zeros(3, np.float32)
 
     def create_sub_objects(self, start_sub: int, start_tri: int, n: int = SUB_OBJECT_TRIANGLES):
         """src/triangle_object.rs:160-197: chunks of ``n`` triangles with their AABBs."""
@@ -136,7 +196,8 @@ class SceneObject:
         subs = np.zeros(n_sub, B.SUB_OBJECT_INFO)
         for k in range(n_sub):
             chunk = self.triangles[k * n:(k + 1) * n]
-            allb = np.concatenate([chunk["min_bounds"], chunk["max_bounds"]])
+            # the reference interleaves [min0, max0, min1, max1, ...] (:171-174)
+            allb = np.stack([chunk["min_bounds"], chunk["max_bounds"]], axis=1).reshape(-1, 3)
             mn, mx = bounding_box(allb)
             subs[k]["min_bounds"] = mn
             subs[k]["max_bounds"] = mx
@@ -453,7 +514,9 @@ def scene_heightfield(width=1920, height=1080, nx=1000, nz=500, seed=7) -> Rende
     info["min_bounds"] = mn
     info["max_bounds"] = mx
     info["material_index"] = 0
-    obj = SceneObject(info, tris)
+    # editable like an STL object: its vertices are its "normalised points" at
+    # scale 1, rotation 0, no translation (update_triangles reproduces them)
+    obj = SceneObject(info, tris, normalized_points=np.stack([a, b, c], axis=1).reshape(-1, 3))
     obj.create_sub_objects(0, 0)
     mats = np.stack([_material(0, 0.9, 0.0, 0.1, 1.0, 0.0, 1.0), _material(1, 0.3, 0.0, 0.8, 0.05, 0.0, 1.0)])
     tex = np.stack([solid_color_image([0.3, 0.6, 0.3], (2, 2)), solid_color_image([0.9, 0.9, 0.9], (2, 2))])

@@ -164,6 +164,86 @@ def test_gpu_update_scene_and_reset(gpu, oracle_lib):
     assert_same(acc, out, rays, acc_o, out_o, rays_o)
 
 
+@pytest.mark.parametrize("config,kw", [
+    ("c3_chess", dict(width=96, height=64, env_size=(512, 256))),
+    ("c5_heightfield", dict(width=64, height=48, nx=60, nz=30)),
+])
+def test_gpu_device_scene_edit(gpu, oracle_lib, config, kw):
+    """update_scene on the device: every object rotated, scaled and
+    moved; triangles, object and sub-object bounds rebuilt by scene_edit.hip and
+    the accelerator refitted. Geometry must equal the host rebuild bit for bit
+    (update_triangles + update_sub_objects, src/triangle_object.rs:129-150,
+    :199-220) and the frames must equal the oracle's on the edited scene."""
+    from rust_gpu_raytracing_amd import builder
+
+    scene, bounces = build_config(config, **kw)
+    rng = np.random.default_rng(5)
+    with Renderer(scene) as r:
+        r.compute_frame(bounces)
+        for step in range(2):  # two edits in a row: the second refits a refitted tree
+            for o in scene.objects:
+                o.rotation = (rng.random(3) * 40 - 20).astype(np.float32)
+                o.scale = np.float32(0.8 + 0.4 * rng.random())
+                o.transformation = (np.asarray(o.transformation) + rng.random(3) - 0.5).astype(np.float32)
+            r.update_scene(device=True)
+            r.compute_frame(bounces)
+        geo = r.read_geometry()
+        r.reset_accumulation()
+        r.reset_ray_count()
+        for _ in range(2):
+            r.compute_frame(bounces)
+        acc, out, rays = r.read_accumulation(), r.read_output(), r.ray_count()
+    for o in scene.objects:
+        builder.update_object(o)
+    objs, subs, tris = scene.flatten()
+    assert geo[0].tobytes() == objs.tobytes()
+    assert geo[1].tobytes() == subs.tobytes()
+    assert geo[2].tobytes() == tris.tobytes()
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
+    assert_same(acc, out, rays, acc_o, out_o, rays_o)
+
+
+def test_gpu_device_edit_then_host_rebuild(gpu, oracle_lib):
+    """A device edit followed by a change that forces the host to rebuild the
+    accelerator (fewer objects in Params): the host reads the device geometry
+    back first."""
+    from rust_gpu_raytracing_amd import builder
+
+    scene, bounces = build_config("c3_chess", width=64, height=48, env_size=(512, 256))
+    with Renderer(scene) as r:
+        for o in scene.objects[:5]:
+            o.rotation = np.array([0.0, 30.0, 0.0], np.float32)
+        r.update_scene(device=True)
+        scene.objects = scene.objects[:20]  # Params.object_count 34 -> 20
+        r.reset_accumulation()
+        r.reset_ray_count()
+        r.compute_frame(bounces)
+        acc, out, rays = r.read_accumulation(), r.read_output(), r.ray_count()
+    for o in scene.objects:
+        builder.update_object(o)
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 1)
+    assert_same(acc, out, rays, acc_o, out_o, rays_o)
+
+
+def test_gpu_device_edit_full_size_heightfield(gpu):
+    """C5 at full size (1M triangles): the device rebuild equals the host one bit for bit."""
+    from rust_gpu_raytracing_amd import builder
+
+    scene, _ = build_config("c5_heightfield", width=64, height=32)
+    o = scene.objects[0]
+    o.rotation = np.array([3.0, -7.0, 11.0], np.float32)
+    o.scale = np.float32(1.5)
+    o.transformation = np.array([0.25, -1.0, 2.0], np.float32)
+    with Renderer(scene) as r:
+        r.update_objects()
+        geo = r.read_geometry()
+    builder.update_object(o)
+    objs, subs, tris = scene.flatten()
+    assert geo[0].tobytes() == objs.tobytes()
+    assert geo[1].tobytes() == subs.tobytes()
+    assert geo[2].tobytes() == tris.tobytes()
+
+
 def test_gpu_camera_move(gpu, oracle_lib):
     from rust_gpu_raytracing_amd.camera import Camera
 
