@@ -257,6 +257,25 @@ RT_API uint32_t rt_bytes_per_row(uint32_t width, uint32_t alignment);
 RT_API int rt_ray_count(rt_ctx* ctx, uint64_t* out);
 RT_API int rt_reset_ray_count(rt_ctx* ctx);
 
+/* Tile claim order (new; the reference dispatches a plain grid,
+ * src/renderer.rs:238-249). 0 = tile index order. 1 = cost-ordered (the
+ * default): every launch records the rays each of its tiles took, and the
+ * first workgroup of a launch to run out of tiles sorts the previous launch's
+ * costs (most rays first) into the claim order of the next launch, while the
+ * rest of the grid drains its last paths. Launches then end on cheap tiles
+ * rather than on long paths. Active for launches in which every wave takes
+ * at least 4 tiles on average (else the order cannot matter and the sort
+ * would lengthen a short launch). Pixels are independent, so the image is
+ * bit-identical under any order. Setting a schedule discards recorded costs
+ * and orders (the next two launches run in index order). Asynchronous. */
+RT_API int rt_set_tile_schedule(rt_ctx* ctx, uint32_t schedule);
+/* The claim order the next launch uses (order[q] = local tile claimed at
+ * queue position q; the identity when none is sorted yet) and the rays per
+ * tile recorded by the last launch (zero once a later launch sorted them).
+ * Either pointer may be NULL; each holds the rank's owned tile count
+ * (rt_owned_pixel_count / 64). Synchronous. */
+RT_API int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs);
+
 /* Current accumulation counter k (the value the next rt_compute_frame uses). */
 RT_API int rt_accumulation_index(const rt_ctx* ctx, uint32_t* out);
 

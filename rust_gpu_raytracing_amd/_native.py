@@ -112,6 +112,8 @@ SIGNATURES = {
     "rt_ray_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_reset_ray_count": (ctypes.c_int, [_P]),
     "rt_accumulation_index": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_set_tile_schedule": (ctypes.c_int, [_P, _U32]),
+    "rt_tile_schedule_state": (ctypes.c_int, [_P, _P, _P]),
     "rt_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "rt_last_dispatch_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_dispatch_time_total": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),

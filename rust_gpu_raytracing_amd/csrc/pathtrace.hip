@@ -617,6 +617,10 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 // visible). Lane 0 does the memory operations; results are wave-uniform.
 constexpr uint32_t kQueueStride = 64;  // u32 between stripe counters (256 B)
 
+// The cost-ordered schedule's device state (KernelArgs::sched).
+__device__ __forceinline__ uint32_t* sched_orders(const KernelArgs& ka) { return ka.sched + 2u * ka.owned_tiles; }
+__device__ __forceinline__ uint32_t* sched_flags(const KernelArgs& ka) { return ka.sched + 4u * ka.owned_tiles; }
+
 __device__ __forceinline__ uint32_t xcc_id() {
     return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
 }
@@ -642,12 +646,114 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka, TileQueue& 
             uint32_t old = 0;
             if (leader) old = atomicAdd(ctr, 1u);
             old = __builtin_amdgcn_readlane(old, 0);
-            if (old < count) return old * n_str + q.stripe;
+            if (old < count) {  // queue position -> local tile (identity unless cost-ordered)
+                const uint32_t pos = old * n_str + q.stripe;
+                return ka.tile_order ? ka.tile_order[pos] : pos;
+            }
         }
         q.stripe = q.stripe + 1u == n_str ? 0u : q.stripe + 1u;
         q.tried += 1;
     }
     return 0xffffffffu;
+}
+
+// Cost-ordered schedule support: adds the rays of the pixels this wave just
+// finished to their tiles' counters. Finished lanes almost always share one or
+// two tiles, so this is one wave reduction and one atomic per distinct tile.
+__device__ __forceinline__ void record_tile_cost(uint32_t* cost, bool fin, uint32_t tile, uint32_t n) {
+    uint64_t m = __ballot(fin);
+    while (m) {
+        const uint32_t t = __builtin_amdgcn_readlane(tile, (uint32_t)__builtin_ctzll(m));
+        const bool mine = fin && tile == t;
+        uint32_t v = mine ? n : 0u;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63u) == 0) atomicAdd(cost + t, v);
+        m &= ~__ballot(mine);
+    }
+}
+
+// The cost-ordered schedule's sort: the tiles of one launch ordered by the
+// rays they took, most expensive first, for a later launch to claim in that
+// order, so that launches end on cheap tiles (sky) instead of on the long paths
+// of expensive ones (paths progress one bounce per wave iteration, so the
+// paths in flight when the queue runs dry decide how long the last waves run
+// on nearly empty lanes). A stable counting sort into kOrderBuckets buckets
+// between 0 and the largest cost. No atomics on shared counters: each wave
+// counts its tiles per bucket with ballots, a scan over (bucket, wave) gives
+// every wave its slots, and the wave scatters in tile order -- so the result
+// is deterministic (and any order renders the same image: pixels are
+// independent). No costs recorded: tile index order. Zeroes the costs for
+// their next recording. Run by one whole workgroup; `scratch` holds
+// kOrderBuckets * 16 + 1 words of LDS (kLdsTailBytes, rt_kernel_args.h).
+
+template <uint32_t kThreads>
+__device__ void sort_tiles_by_cost(uint32_t* __restrict__ cost, uint32_t* __restrict__ order, uint32_t n,
+                                   uint32_t* scratch) {
+    constexpr uint32_t kWaves = kThreads / 64;
+    static_assert(kWaves <= 16 && kOrderBuckets * kWaves <= kThreads, "scratch layout / one scan entry per thread");
+    uint32_t* slots = scratch;                       // [bucket][wave]: counts, then first slot
+    uint32_t* max_cost = scratch + kOrderBuckets * 16;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    if (tid == 0) *max_cost = 0;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t i = tid; i < n; i += kThreads) m = max(m, cost[i]);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o));
+    if (lane == 0) atomicMax(max_cost, m);
+    __syncthreads();
+    const uint32_t mx = *max_cost;
+    if (mx == 0) {
+        for (uint32_t i = tid; i < n; i += kThreads) order[i] = i;
+        return;
+    }
+    const uint64_t mc = (uint64_t)mx + 1u;
+    // each wave takes one contiguous range of tiles, 64 per round, so the
+    // (bucket, wave) slot order makes the sort stable
+    const uint32_t span = ((n + kWaves - 1u) / kWaves + 63u) & ~63u;
+    const uint32_t lo = min(n, wave * span), hi = min(n, lo + span);
+    auto key = [&](uint32_t i) {  // kOrderBuckets for no tile
+        return i < hi ? kOrderBuckets - 1u - (uint32_t)(((uint64_t)cost[i] * kOrderBuckets) / mc) : kOrderBuckets;
+    };
+    uint32_t cnt = 0;  // lane b < kOrderBuckets: this wave's tiles in bucket b
+    for (uint32_t base = lo; base < hi; base += 64u) {
+        const uint32_t k = key(base + lane);
+        for (uint32_t b = 0; b < kOrderBuckets; ++b) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(k == b));
+            if (lane == b) cnt += c;
+        }
+    }
+    if (lane < kOrderBuckets) slots[lane * kWaves + wave] = cnt;
+    __syncthreads();
+    // exclusive scan over (bucket, wave), bucket-major (Hillis-Steele)
+    constexpr uint32_t kEntries = kOrderBuckets * kWaves;
+    uint32_t v = tid < kEntries ? slots[tid] : 0u;
+    const uint32_t own = v;
+    for (uint32_t off = 1; off < kEntries; off <<= 1) {
+        __syncthreads();
+        const uint32_t add = (tid < kEntries && tid >= off) ? slots[tid - off] : 0u;
+        __syncthreads();
+        v += add;
+        if (tid < kEntries) slots[tid] = v;
+    }
+    __syncthreads();
+    if (tid < kEntries) slots[tid] = v - own;
+    __syncthreads();
+    uint32_t next = lane < kOrderBuckets ? slots[lane * kWaves + wave] : 0u;  // lane b: next slot of bucket b
+    for (uint32_t base = lo; base < hi; base += 64u) {
+        const uint32_t i = base + lane;
+        const uint32_t k = key(i);
+        uint32_t pos = 0;
+        for (uint32_t b = 0; b < kOrderBuckets; ++b) {
+            const uint64_t mb = __ballot(k == b);
+            const uint32_t first = __builtin_amdgcn_readlane(next, b);
+            if (k == b) pos = first + __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+            if (lane == b) next += (uint32_t)__popcll(mb);
+        }
+        if (i < hi) {
+            order[pos] = i;
+            cost[i] = 0;
+        }
+    }
 }
 
 #ifdef RT_DIAG_TAIL
@@ -750,6 +856,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // Lane states. A lane owns one pixel at a time and one ray of its path.
     constexpr uint32_t kIdle = 0, kSetup = 1, kTrav = 2, kDone = 3;
     uint32_t rays = 0;
+    uint32_t lane_tile = 0;  // local tile of the lane's pixel (tile costs)
     uint32_t mode = kIdle;
     uint32_t index = 0, sample = 0, frame = 0;
     float4 pix = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -831,6 +938,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 
 #ifdef RT_DIAG_TAIL
     const unsigned long long wave_t0 = realtime();
+    unsigned long long wave_dry = 0;  // when the queue first came up empty for this wave
 #endif
     if (blockIdx.x == 0 && threadIdx.x < ka.queue_stripes) ka.queue_next[threadIdx.x * kQueueStride] = 0u;
     // home stripe: this XCD's (blocks are dealt round-robin over the XCDs, so
@@ -849,14 +957,21 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         const unsigned long long ts0 = stamp();
 #endif
         // 1. Shade the lanes whose trace has finished (:228-311).
+        bool fin = false;      // a sample finished: its rays go to the tile's cost
+        uint32_t fin_rays = 0;
         if (mode == kDone) {
             const Hit h = trace_end<kTris>(sv, ka, p.o, p.d, ts);
             ++rays;
-            if (shade(sv, ka, p, h))
+            if (shade(sv, ka, p, h)) {
+                // rays of the sample: one per bounce, plus the escaping one unless the limit ended it
+                fin = true;
+                fin_rays = p.bounce + (p.bounce < ka.bounces ? 1u : 0u);
                 finish_sample();
-            else
+            } else {
                 mode = kSetup;
+            }
         }
+        if (ka.tile_cost) record_tile_cost(ka.tile_cost, fin, lane_tile, fin_rays);
 #ifdef RT_DIAG
         const unsigned long long ts1 = stamp();
         shade_cyc += ts1 - ts0;
@@ -877,6 +992,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                     const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
                     if (x < ka.width && y < ka.height) {
                         index = y * ka.width + x;  // :148
+                        lane_tile = tile;
                         sample = 0;
                         frame = 0;
                         mode = kSetup;
@@ -889,6 +1005,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             if (next == 64u) {
                 tile = claim_tile(ka, queue);
                 next = 0;
+#ifdef RT_DIAG_TAIL
+                if (tile >= ka.owned_tiles && wave_dry == 0) wave_dry = realtime();
+#endif
             }
         }
 #ifdef RT_DIAG
@@ -971,7 +1090,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         atomicMax(ka.diag + 7, wave_t1 - wave_t0);
         const uint32_t w = blockIdx.x * (kThreads / 64u) + (threadIdx.x >> 6);
         if (w < 65536u) {
-            ka.diag[8 + 2 * w] = wave_t0;
+            ka.diag[8 + 2 * w] = wave_dry ? wave_dry : wave_t1;  // queue dry (tools/tail_probe.py)
             ka.diag[8 + 2 * w + 1] = wave_t1;
         }
     }
@@ -979,6 +1098,22 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     atomicAdd(&block_rays, rays);
     __syncthreads();
     if (tid == 0 && block_rays != 0) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
+    // Cost-ordered schedule: the first workgroup out of work sorts the previous
+    // launch's tile costs into the claim order of the next launch, while the
+    // rest of the grid drains its last paths (no extra launch, off the
+    // critical path). The flags are double-buffered like the queue counters.
+    if (ka.sched) {
+        const uint32_t par = ka.sched_bits & 1u, n = ka.owned_tiles;
+        __shared__ uint32_t sorter;
+        if (tid == 0) {
+            sorter = atomicAdd(sched_flags(ka) + par, 1u);
+            if (blockIdx.x == 0) sched_flags(ka)[par ^ 1u] = 0u;
+        }
+        __syncthreads();
+        if (sorter == 0)
+            sort_tiles_by_cost<kThreads>(ka.sched + (par ^ 1u) * n, sched_orders(ka) + (par ^ 1u) * n, n,
+                                         reinterpret_cast<uint32_t*>(lds + ka.lds_srgb_offset));
+    }
 }
 
 // Instantiations: LDS mode x workgroup size x triangles present. All waves of

@@ -58,9 +58,6 @@ namespace {
 
 constexpr size_t kLdsSceneBudget = 64 * 1024;    // mode 1: spheres/materials/objects/sphere BVH per workgroup
 constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerator (one 1024-thread workgroup per CU)
-// Always staged at the end of the LDS image: the sRGB table (256 floats) and the
-// camera block (inverse projection, inverse view, aspect: 33 floats).
-constexpr size_t kLdsTailBytes = 1024 + 160;
 // Diagnostic builds (-DRT_DIAG_TAIL) record (start, end) per wave after the 8
 // counters: room for 65,536 waves.
 constexpr size_t kDiagWaveRecords = 2 * 65536;
@@ -73,6 +70,10 @@ constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
 // traversing (pathtrace.hip, step 4 of the kernel loop).
 constexpr uint32_t kDefaultTravThreshold = 8;
+// Tile claim order: 0 = tile index order, 1 = cost-ordered (most rays first,
+// sorted on the device from the previous frame's per-tile ray counts).
+constexpr uint32_t kDefaultTileSchedule = 1;
+constexpr uint64_t kSchedMinTilesPerWave = 4;
 
 }  // namespace
 
@@ -123,6 +124,12 @@ struct rt_ctx {
     uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
     uint32_t trav_threshold = kDefaultTravThreshold;  // RT_TRAV_THRESHOLD (A/B switch)
     uint32_t leaf_batch = 7;                          // RT_LEAF_BATCH, in eighths (A/B switch)
+    // cost-ordered tile schedule (rt_set_tile_schedule), double-buffered by
+    // launch parity: launch L records costs[L&1], reads order[L&1], and its
+    // first idle workgroup sorts costs[~L&1] (launch L-1's) into order[~L&1]
+    uint32_t tile_schedule = kDefaultTileSchedule;  // RT_TILE_SCHEDULE (A/B switch)
+    uint32_t* d_tile_sched = nullptr;  // costs[2][n], orders[2][n], flags[2] (n = owned tiles)
+    uint64_t sched_launches = 0;       // launches since the schedule was (re)set
     uint32_t last_blocks = 0, last_lds = 0;
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
@@ -549,6 +556,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->trav_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
         env = std::getenv("RT_LEAF_BATCH");
         if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
+        env = std::getenv("RT_TILE_SCHEDULE");
+        if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
@@ -603,7 +612,8 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
-                    ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds};
+                    ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
+                    ctx->d_tile_sched};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -898,6 +908,25 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     const uint64_t wanted = (ctx->owned_tiles + waves_per_block - 1) / waves_per_block;
     const uint32_t blocks = (uint32_t)(wanted < resident ? wanted : resident);
     if (blocks == 0) return RT_OK;
+    // Cost-ordered schedule, when each wave takes several tiles per launch (with
+    // about one tile per wave the claim order cannot shorten the drain, and the
+    // sort would sit on a short launch's critical path).
+    const bool sched = ctx->tile_schedule &&
+                       (uint64_t)ctx->owned_tiles >= kSchedMinTilesPerWave * blocks * waves_per_block;
+    if (sched) {
+        const size_t n = ctx->owned_tiles;
+        if (!ctx->d_tile_sched) {
+            int rc = dev_alloc(ctx, &ctx->d_tile_sched, 4 * n + 2);
+            if (rc) return rc;
+            RT_HIP(ctx, hipMemsetAsync(ctx->d_tile_sched, 0, (4 * n + 2) * 4, ctx->stream));
+            ctx->sched_launches = 0;
+        }
+        ka.sched = ctx->d_tile_sched;
+        // orders[parity] was written by the previous launch
+        ka.sched_bits = (uint32_t)(ctx->sched_launches & 1u);
+        ka.tile_cost = ka.sched + ka.sched_bits * (size_t)n;
+        ka.tile_order = ctx->sched_launches ? ka.sched + (2u + ka.sched_bits) * (size_t)n : nullptr;
+    }
 
     EventPair ev;
     if (ctx->timing) {
@@ -922,6 +951,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         RT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
         ctx->pending.push_back(ev);
     }
+    if (sched) ++ctx->sched_launches;
     return RT_OK;
 }
 
@@ -1102,6 +1132,36 @@ int rt_ray_count(rt_ctx* ctx, uint64_t* out) {
     RT_HIP(ctx, hipMemcpyAsync(&v, ctx->d_counter, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     *out = v;
+    return RT_OK;
+}
+
+int rt_set_tile_schedule(rt_ctx* ctx, uint32_t schedule) {
+    RT_ENTER(ctx);
+    if (schedule > 1) return fail(ctx, RT_E_INVALID, "tile schedule must be 0 (index order) or 1 (cost-ordered)");
+    ctx->tile_schedule = schedule;
+    if (ctx->d_tile_sched)
+        RT_HIP(ctx, hipMemsetAsync(ctx->d_tile_sched, 0, (4 * (size_t)ctx->owned_tiles + 2) * 4, ctx->stream));
+    ctx->sched_launches = 0;
+    return RT_OK;
+}
+
+int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
+    RT_ENTER(ctx);
+    const size_t n = ctx->owned_tiles;
+    const bool on = ctx->tile_schedule && ctx->d_tile_sched;
+    const uint32_t par = (uint32_t)(ctx->sched_launches & 1u);  // the next launch's parity
+    for (size_t i = 0; i < n && order; i++) order[i] = (uint32_t)i;
+    if (order && on && ctx->sched_launches)
+        RT_HIP(ctx, hipMemcpyAsync(order, ctx->d_tile_sched + 2 * n + par * n, n * 4, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    if (costs) {
+        if (on && ctx->sched_launches)  // what the last launch recorded
+            RT_HIP(ctx, hipMemcpyAsync(costs, ctx->d_tile_sched + (par ^ 1u) * n, n * 4, hipMemcpyDeviceToHost,
+                                       ctx->stream));
+        else
+            std::memset(costs, 0, n * 4);
+    }
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return RT_OK;
 }
 

@@ -57,6 +57,19 @@ static_assert(sizeof(RtObject) == 48, "ObjectInfo layout");
 static_assert(sizeof(RtSubObject) == 32, "SubObjectInfo layout");
 static_assert(sizeof(RtTriangleHot) == 80, "hot triangle layout");
 
+// Cost-ordered tile schedule: buckets of the counting sort (pathtrace.hip,
+// sort_tiles_by_cost), whose scratch reuses the LDS tail after the frame loop.
+#ifndef RT_ORDER_BUCKETS
+#define RT_ORDER_BUCKETS 16
+#endif
+constexpr uint32_t kOrderBuckets = RT_ORDER_BUCKETS;
+// Always staged at the end of the LDS image: the sRGB table (256 floats) and
+// the camera block (inverse projection, inverse view, aspect: 33 floats, 160 B
+// reserved). After the frame loop the sort's scratch (kOrderBuckets x 16 waves
+// + 1 words) reuses it.
+constexpr size_t kLdsTailBytes = 1024 + 160;
+static_assert(kLdsTailBytes >= (kOrderBuckets * 16 + 1) * 4, "sort scratch fits the LDS tail");
+
 struct KernelArgs {
     // framebuffer (bindings 1, 2, 6)
     const float4* __restrict__ camera_rays;
@@ -66,6 +79,14 @@ struct KernelArgs {
     unsigned long long* __restrict__ diag;          // 8 diagnostic counters (RT_DIAG builds)
     uint32_t* __restrict__ queue;       // this launch's tile-queue stripe counters (zero at launch start)
     uint32_t* __restrict__ queue_next;  // the next launch's counters, zeroed by this launch
+    // cost-ordered tile schedule (pathtrace.hip, sort_tiles_by_cost), null when
+    // off: costs[2][owned_tiles], orders[2][owned_tiles], sort flags[2]; launch
+    // parity p = sched_bits & 1 records costs[p] and claims in orders[p] (if
+    // sched_bits & 2), and its first idle workgroup sorts costs[p^1] (the
+    // previous launch's) into orders[p^1] for the next launch
+    uint32_t* __restrict__ sched;
+    const uint32_t* __restrict__ tile_order;  // = orders[p] when valid, else null (index order)
+    uint32_t* __restrict__ tile_cost;         // = costs[p]
     // scene (bindings 3, 4, 5, 7, 8, 10)
     const float4* __restrict__ sphere_slots;      // centre.xyz, radius*radius (f32), kernel order (sphere_bvh.h)
     const uint32_t* __restrict__ sphere_orig;     // slot -> original sphere index
@@ -124,6 +145,7 @@ struct KernelArgs {
     uint32_t trav_threshold;  // resume shading once at most this many lanes still traverse
     uint32_t leaf_batch;      // test deferred leaves once 8 * pending >= leaf_batch * traversing
     uint32_t queue_stripes;   // tile-queue stripes (one per XCD)
+    uint32_t sched_bits;      // cost-ordered schedule: launch parity
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;
     uint32_t lds_obj_offset;

@@ -270,6 +270,19 @@ class Renderer:
         N.check(self._ctx, self._lib.rt_debug_counters(self._ctx, v, n), self._lib)
         return list(v)
 
+    def set_tile_schedule(self, schedule: int) -> None:
+        """0: claim tiles in index order; 1: cost-ordered (most rays of an earlier launch first)."""
+        self._call("rt_set_tile_schedule", schedule)
+
+    def tile_schedule_state(self):
+        """(order, costs): the next launch's claim order over this rank's tiles and the rays recorded per tile."""
+        n = self.owned_pixel_count() // 64
+        order = np.zeros(n, np.uint32)
+        costs = np.zeros(n, np.uint32)
+        self._call("rt_tile_schedule_state", order.ctypes.data_as(ctypes.c_void_p),
+                   costs.ctypes.data_as(ctypes.c_void_p))
+        return order, costs
+
     def launch_config(self) -> dict:
         """Geometry of the last launch: workgroup threads, workgroups, LDS bytes, scene staged in LDS."""
         v = [ctypes.c_uint32() for _ in range(4)]

@@ -114,6 +114,52 @@ def test_gpu_tile_split_bitwise(gpu):
     assert np.array_equal(out, out1) and np.array_equal(acc.view(np.uint32), acc1.view(np.uint32))
 
 
+@pytest.mark.parametrize("rank,world,w,h", [(0, 1, 1920, 1080), (1, 3, 3840, 2160)])
+def test_gpu_cost_ordered_schedule(gpu, rank, world, w, h):
+    """The cost-ordered tile schedule (rt_set_tile_schedule) changes only the
+    claim order: bit-identical to index order. Each launch records every ray
+    of its tiles; the next launch's first idle workgroup sorts them into a
+    permutation, most rays first, which the launch after that claims in."""
+    scene, bounces = build_config("c2_rtiow", width=w, height=h)
+    res = []
+    for schedule in (0, 1):
+        with Renderer(scene, rank=rank, world_size=world) as r:
+            r.set_tile_schedule(schedule)
+            n_tiles = r.owned_pixel_count() // 64
+            prev_costs = None
+            for f in range(5):
+                before = r.ray_count()
+                r.compute_frame(bounces)
+                order, costs = r.tile_schedule_state()
+                assert np.array_equal(np.sort(order), np.arange(n_tiles))  # always a permutation
+                if schedule == 0:
+                    assert np.array_equal(order, np.arange(n_tiles)) and not costs.any()
+                    continue
+                assert costs.sum() == r.ray_count() - before  # every ray of this launch, by tile
+                if f == 0:
+                    assert np.array_equal(order, np.arange(n_tiles))  # nothing recorded before launch 0
+                else:  # a stable sort of the previous launch's costs into 16 buckets, most rays first
+                    c = prev_costs.astype(np.uint64)
+                    key = 15 - (c * 16) // (c.max() + 1)
+                    assert np.array_equal(order, np.argsort(key, kind="stable"))
+                prev_costs = costs
+            res.append((r.read_accumulation(), r.read_output(), r.ray_count()))
+    (a0, o0, n0), (a1, o1, n1) = res
+    assert n0 == n1
+    assert np.array_equal(o0, o1) and np.array_equal(a0.view(np.uint32), a1.view(np.uint32))
+
+
+def test_gpu_cost_ordered_schedule_inactive_on_small_frames(gpu):
+    """With about one tile per resident wave the schedule stays off: index order, nothing recorded."""
+    scene, bounces = build_config("c1_four_spheres", width=320, height=184)
+    with Renderer(scene) as r:
+        r.set_tile_schedule(1)
+        for _ in range(3):
+            r.compute_frame(bounces)
+        order, costs = r.tile_schedule_state()
+        assert np.array_equal(order, np.arange(order.size)) and not costs.any()
+
+
 def test_gpu_pack_unpack_gather(gpu):
     """The multi-GPU readback path on one device: ranks pack their tiles into device
     buffers, rank 0 unpacks them; the assembled accumulation equals a 1-GPU render."""

@@ -8,6 +8,7 @@ builds produce bit-identical accumulations.
 import argparse
 import json
 import statistics
+import time
 import sys
 from pathlib import Path
 
@@ -59,15 +60,19 @@ def main():
         r.compute_frame(bounces)
         r.synchronize()
     times = {p: [] for p in args.libs}
+    walls = {p: [] for p in args.libs}
     rays = {}
     for _ in range(args.rounds):
         for p, r in zip(args.libs, rs):
             r.reset_timing()
             r.reset_ray_count()
             r.set_timing(True)
+            r.synchronize()
+            t0 = time.perf_counter()
             for _ in range(args.frames):
                 r.compute_frame(bounces)
             r.synchronize()
+            walls[p].append((time.perf_counter() - t0) * 1e3 / args.frames)
             r.set_timing(False)
             ms, n = r.dispatch_time_total()
             times[p].append(ms / n)
@@ -78,6 +83,7 @@ def main():
     for (p, t), s in zip(times.items(), same):
         med = statistics.median(t)
         out.append({"lib": Path(p).name, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+                    "wall_ms": round(statistics.median(walls[p]), 4),
                     "mray_s": round(rays[p] / med / 1e3, 1), "bit_identical_to_first": s,
                     "launch": launch_of(rs[list(times).index(p)])})
     print(json.dumps({"config": args.config, "bounces": bounces, "results": out}, indent=1))

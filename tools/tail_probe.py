@@ -2,7 +2,8 @@
 
 usage: RT_LIB=build/ab/lib_tail.so python tools/tail_probe.py [config ...]
 Per launch: first wave start -> mean/last wave start (ramp), mean/last wave end
-(tail), in microseconds of the device's 100 MHz real-time clock.
+(tail), when waves first found the tile queue empty (dry) and how long they ran
+after that (drain), in microseconds of the device's 100 MHz real-time clock.
 """
 import json
 import sys
@@ -31,13 +32,15 @@ for name in sys.argv[1:] or ["c2_rtiow"]:
             kern_ms, _ = r.dispatch_time_total()
             c = r.debug_counters(8 + 2 * 65536)
             waves = np.array(c[8:8 + 2 * c[3]], np.float64).reshape(-1, 2)
-            dur = (waves[:, 1] - waves[:, 0]) / 100.0
-            ends = (waves[:, 1] - waves[:, 0].min()) / 100.0
-            n = c[3]
             t_first = (~np.uint64(c[2])).item()  # stored as the max of ~start
+            dry = (waves[:, 0] - t_first) / 100.0   # when the wave first found the queue empty
+            dur = (waves[:, 1] - waves[:, 0]) / 100.0  # its drain: queue dry -> wave end
+            ends = (waves[:, 1] - t_first) / 100.0
+            n = c[3]
             res.append({"waves": n, "ramp_mean_us": (c[4] / n - t_first) / 100, "ramp_last_us": (c[5] - t_first) / 100,
                         "end_mean_us": (c[0] / n - t_first) / 100, "end_last_us": (c[1] - t_first) / 100,
                         "nan_fallbacks": c[6], "longest_wave_us": c[7] / 100, "kernel_us": kern_ms * 1e3,
-                        "wave_dur_pct": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 99, 100)],
+                        "dry_pct": [round(float(np.percentile(dry, q)), 1) for q in (0, 10, 50, 90, 100)],
+                        "drain_pct": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 99, 100)],
                         "end_pct": [round(float(np.percentile(ends, q)), 1) for q in (10, 50, 90, 99, 100)]})
         print(json.dumps({"config": name, "runs": res[1:]}))
