@@ -356,6 +356,11 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
 template <bool kTris>
 constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
 
+// Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
+// is read from global memory (LDS modes 0 and 1).
+template <int kMode, bool kTris>
+constexpr bool kDrainDecouple = kTris && kMode < 2;
+
 template <bool kTris>
 __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     const bool tri = kTris && ts.phase == 0;
@@ -1031,16 +1036,37 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         // 4. Traverse. Lanes whose trace finishes wait (kDone) until fewer than
         // `trav_threshold` lanes are still traversing; then the wave goes back
         // to shade and refill them together, so neither the traversal tail nor
-        // the shading runs on a nearly empty wave. With no tiles left, traverse
-        // to the end.
-        const uint32_t thresh = tile >= ka.owned_tiles ? 0u : ka.trav_threshold;
+        // the shading runs on a nearly empty wave. With no tiles left (the
+        // drain) the wave cannot refill, and by default traverses to the end.
+        // Instances whose triangle accelerator stays in global memory (long
+        // traces: hundreds of dependent loads) decouple the drain instead:
+        // after at least `drain_min_steps` steps the wave goes back to
+        // shading once at most `drain_threshold` lanes still traverse and
+        // some lane is done, so a few very long traces do not hold up the
+        // other paths' next bounces (C5: 72 -> 53 ms). Where traces are short
+        // an extra shading pass costs more than the wait (C2, C3: measured).
+        const bool draining = tile >= ka.owned_tiles;
+        uint32_t thresh = draining ? 0u : ka.trav_threshold;
+        uint32_t n_active = 64u, min_steps = 0u;
+        if constexpr (kDrainDecouple<kMode, kTris>) {
+            if (draining) {
+                thresh = ka.drain_threshold;
+                n_active = (uint32_t)__popcll(__ballot(mode == kTrav || mode == kDone));
+                min_steps = ka.drain_min_steps;
+            }
+        }
 #ifdef RT_DIAG
         const unsigned long long t0 = stamp();
 #endif
         while (true) {
             const uint64_t trav = __ballot(mode == kTrav);
             const uint32_t n_trav = (uint32_t)__popcll(trav);
-            if (n_trav <= thresh || trav == 0) break;
+            if constexpr (kDrainDecouple<kMode, kTris>) {
+                if (trav == 0 || (n_trav <= thresh && n_trav < n_active && min_steps == 0)) break;
+                min_steps -= min_steps != 0;
+            } else {
+                if (n_trav <= thresh || trav == 0) break;
+            }
 #ifdef RT_DIAG
             ++steps;
             step_lanes += (unsigned long long)n_trav;

@@ -70,6 +70,12 @@ constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
 // traversing (pathtrace.hip, step 4 of the kernel loop).
 constexpr uint32_t kDefaultTravThreshold = 8;
+// Instances with the triangle accelerator in global memory: the same once the
+// tile queue is empty, when the wave goes back to shading only if some lane
+// has finished and after at least kDefaultDrainMinSteps traversal steps
+// (threshold 0: traverse to the end, as the other instances do).
+constexpr uint32_t kDefaultDrainThreshold = 32;
+constexpr uint32_t kDefaultDrainMinSteps = 64;
 // Tile claim order: 0 = tile index order, 1 = cost-ordered (most rays first,
 // sorted on the device from the previous frame's per-tile ray counts).
 constexpr uint32_t kDefaultTileSchedule = 1;
@@ -123,6 +129,8 @@ struct rt_ctx {
     uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
     uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
     uint32_t trav_threshold = kDefaultTravThreshold;  // RT_TRAV_THRESHOLD (A/B switch)
+    uint32_t drain_threshold = kDefaultDrainThreshold;  // RT_DRAIN_THRESHOLD (A/B switch)
+    uint32_t drain_min_steps = kDefaultDrainMinSteps;   // RT_DRAIN_MIN_STEPS (A/B switch)
     uint32_t leaf_batch = 7;                          // RT_LEAF_BATCH, in eighths (A/B switch)
     // cost-ordered tile schedule (rt_set_tile_schedule), double-buffered by
     // launch parity: launch L records costs[L&1], reads order[L&1], and its
@@ -554,6 +562,10 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TRAV_THRESHOLD");
         if (env) ctx->trav_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
+        env = std::getenv("RT_DRAIN_THRESHOLD");
+        if (env) ctx->drain_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
+        env = std::getenv("RT_DRAIN_MIN_STEPS");
+        if (env) ctx->drain_min_steps = (uint32_t)std::strtoul(env, nullptr, 10);
         env = std::getenv("RT_LEAF_BATCH");
         if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TILE_SCHEDULE");
@@ -847,6 +859,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.rank = ctx->rank;
     ka.world_size = ctx->world;
     ka.trav_threshold = ctx->trav_threshold;
+    ka.drain_threshold = ctx->drain_threshold;
+    ka.drain_min_steps = ctx->drain_min_steps;
     ka.leaf_batch = ctx->leaf_batch;
     ka.frames = frames;
 

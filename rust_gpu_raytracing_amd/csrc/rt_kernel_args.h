@@ -143,6 +143,8 @@ struct KernelArgs {
     uint32_t rank;
     uint32_t world_size;
     uint32_t trav_threshold;  // resume shading once at most this many lanes still traverse
+    uint32_t drain_threshold; // decoupled drain (triangle BVH in global memory): the same once the tile
+    uint32_t drain_min_steps; // queue is empty and some lane is done, after at least this many steps
     uint32_t leaf_batch;      // test deferred leaves once 8 * pending >= leaf_batch * traversing
     uint32_t queue_stripes;   // tile-queue stripes (one per XCD)
     uint32_t sched_bits;      // cost-ordered schedule: launch parity
