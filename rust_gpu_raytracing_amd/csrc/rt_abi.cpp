@@ -68,8 +68,14 @@ constexpr uint32_t kQueueStripes = 32;
 constexpr uint32_t kQueueStripesMax = 64;
 constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
-// traversing (pathtrace.hip, step 4 of the kernel loop).
-constexpr uint32_t kDefaultTravThreshold = 8;
+// traversing (pathtrace.hip, step 4 of the kernel loop). The longer a trace is
+// against a shading pass, the earlier it pays to shade the finished lanes
+// (measured: sphere scenes 8, C2 slower at 12+; triangle accelerator in LDS
+// 24, C3/C4 -2%; in global memory 32, C5 -10%).
+uint32_t trav_threshold_for(int lds_mode, bool tris) {
+    if (!tris) return 8;
+    return lds_mode == 2 ? 24 : 32;
+}
 // Instances with the triangle accelerator in global memory: the same once the
 // tile queue is empty, when the wave goes back to shading only if some lane
 // has finished and after at least kDefaultDrainMinSteps traversal steps
@@ -128,7 +134,7 @@ struct rt_ctx {
     uint32_t occ_threads = 0;
     uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
     uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
-    uint32_t trav_threshold = kDefaultTravThreshold;  // RT_TRAV_THRESHOLD (A/B switch)
+    uint32_t trav_threshold = 0;  // RT_TRAV_THRESHOLD (A/B switch); 0 = by scene (trav_threshold_for)
     uint32_t drain_threshold = kDefaultDrainThreshold;  // RT_DRAIN_THRESHOLD (A/B switch)
     uint32_t drain_min_steps = kDefaultDrainMinSteps;   // RT_DRAIN_MIN_STEPS (A/B switch)
     uint32_t leaf_batch = 7;                          // RT_LEAF_BATCH, in eighths (A/B switch)
@@ -858,7 +864,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.owned_tiles = ctx->owned_tiles;
     ka.rank = ctx->rank;
     ka.world_size = ctx->world;
-    ka.trav_threshold = ctx->trav_threshold;
     ka.drain_threshold = ctx->drain_threshold;
     ka.drain_min_steps = ctx->drain_min_steps;
     ka.leaf_batch = ctx->leaf_batch;
@@ -891,6 +896,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         else if (mode1_bytes <= kLdsSceneBudget && ctx->max_lds_mode >= 1)
             mode = 1;
     }
+    ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
