@@ -71,6 +71,16 @@ def pmc_traffic(workload: str):
     return float(e["fetch_bytes_x2"] + e["write_bytes"]), e.get("source")
 
 
+def pmc_issue(workload: str):
+    """VALU issue and lane utilisation of the same committed PMC run (SQ counters): the
+    resource this branchy f32 path is actually bound by, or None."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    e = json.loads(f.read_text()).get(workload) if f.exists() else None
+    if not e or e.get("valu_issue_util") is None:
+        return None
+    return {"valu_issue_util": e["valu_issue_util"], "valu_lane_util": e["valu_lane_util"], "source": e.get("source")}
+
+
 def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
     """The CPU oracle (scalar C restatement, OpenMP over the host cores) on a bounded
     sample of the same workload: the tiles t % sample_world == 0, frames k = 1, 2, ...
@@ -267,6 +277,7 @@ def main() -> int:
                 "launch": launch,
                 "bytes_per_launch": b_launch,
                 "note": "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction",
+                "valu": pmc_issue(workload) if world == 1 else None,
             },
         }
         if gather_ms is not None:

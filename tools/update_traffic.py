@@ -31,7 +31,8 @@ def main(prof_dir, dest):
     f = ROOT / "profiles" / "pmc_traffic.json"
     table = json.loads(f.read_text()) if f.exists() else {}
     table[workload] = {"fetch_bytes_x2": summ["fetch_bytes_x2"], "write_bytes": summ["write_bytes"],
-                       "avg_ns": summ.get("avg_ns"), "source": str(dest.relative_to(ROOT))}
+                       "avg_ns": summ.get("avg_ns"), "valu_issue_util": summ.get("valu_issue_util"),
+                       "valu_lane_util": summ.get("valu_lane_util"), "source": str(dest.relative_to(ROOT))}
     f.write_text(json.dumps(table, indent=1, sort_keys=True) + "\n")
     print(json.dumps(table[workload]))
 
