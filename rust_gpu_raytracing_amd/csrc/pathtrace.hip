@@ -355,6 +355,16 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
 #endif
 template <bool kTris>
 constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
+// Node steps per wave-wide check of the traversal loop (the ballots of the
+// threshold and leaf-batch tests, exec-mask updates). Lanes that finish inside
+// the group idle for its remaining steps; the visit order is unchanged.
+// Measured (RT_TRAV_UNROLL / _TRI = 1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%.
+#ifndef RT_TRAV_UNROLL
+#define RT_TRAV_UNROLL 3
+#endif
+#ifndef RT_TRAV_UNROLL_TRI
+#define RT_TRAV_UNROLL_TRI 3
+#endif
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
@@ -1068,6 +1078,17 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                     node_step<kTris>(sv, ka, p.o, p.d, ts);
                 phase_end<kTris>(sv, ka, p.o, p.d, ts);
                 if (ts.phase == 2) mode = kDone;
+                if (!(kDeferLeaves<kTris> && leaves)) {
+                    // further node steps before the next wave-wide check (RT_TRAV_UNROLL)
+#pragma unroll
+                    for (int k = 1; k < (kTris ? RT_TRAV_UNROLL_TRI : RT_TRAV_UNROLL); ++k) {
+                        if (mode == kTrav) {
+                            node_step<kTris>(sv, ka, p.o, p.d, ts);
+                            phase_end<kTris>(sv, ka, p.o, p.d, ts);
+                            if (ts.phase == 2) mode = kDone;
+                        }
+                    }
+                }
             }
         }
 #ifdef RT_DIAG
