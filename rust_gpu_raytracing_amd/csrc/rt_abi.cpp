@@ -76,6 +76,11 @@ uint32_t trav_threshold_for(int lds_mode, bool tris) {
     if (!tris) return 8;
     return lds_mode == 2 ? 24 : 32;
 }
+// Triangle scenes test deferred leaves once this many eighths of the
+// traversing lanes hold one (pathtrace.hip, leaf_step): later for an LDS
+// accelerator (C3: 7 beats 6 and 8), earlier when the leaf's loads go to global
+// memory anyway (C5: 6 is 4% faster than 7).
+uint32_t leaf_batch_for(int lds_mode) { return lds_mode == 2 ? 7 : 6; }
 // Instances with the triangle accelerator in global memory: the same once the
 // tile queue is empty, when the wave goes back to shading only if some lane
 // has finished and after at least kDefaultDrainMinSteps traversal steps
@@ -137,7 +142,7 @@ struct rt_ctx {
     uint32_t trav_threshold = 0;  // RT_TRAV_THRESHOLD (A/B switch); 0 = by scene (trav_threshold_for)
     uint32_t drain_threshold = kDefaultDrainThreshold;  // RT_DRAIN_THRESHOLD (A/B switch)
     uint32_t drain_min_steps = kDefaultDrainMinSteps;   // RT_DRAIN_MIN_STEPS (A/B switch)
-    uint32_t leaf_batch = 7;                          // RT_LEAF_BATCH, in eighths (A/B switch)
+    uint32_t leaf_batch = 0;  // RT_LEAF_BATCH, in eighths (A/B switch); 0 = by scene (leaf_batch_for)
     // cost-ordered tile schedule (rt_set_tile_schedule), double-buffered by
     // launch parity: launch L records costs[L&1], reads order[L&1], and its
     // first idle workgroup sorts costs[~L&1] (launch L-1's) into order[~L&1]
@@ -866,7 +871,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.world_size = ctx->world;
     ka.drain_threshold = ctx->drain_threshold;
     ka.drain_min_steps = ctx->drain_min_steps;
-    ka.leaf_batch = ctx->leaf_batch;
     ka.frames = frames;
 
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
@@ -897,6 +901,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             mode = 1;
     }
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
+    ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
