@@ -428,9 +428,12 @@ __device__ __forceinline__ Hit trace_end(const SceneView& sv, const KernelArgs& 
         h.n = ts.tri.front ? fn : -fn;
         h.t = ts.tri.t;
         h.p = o + d * ts.tri.t;
-        // object_texture_coords, :568-578 (uv from the OBJECT bounds)
-        h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
-        h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
+        // object_texture_coords, :568-578 (uv from the OBJECT bounds); unused
+        // with 1x1 texture layers, as for spheres below
+        if (ka.tex_w != 1u || ka.tex_h != 1u) {
+            h.u = (h.p.x - ob.min_bounds[0]) / (ob.max_bounds[0] - ob.min_bounds[0]);
+            h.v = (h.p.z - ob.min_bounds[2]) / (ob.max_bounds[2] - ob.min_bounds[2]);
+        }
         h.material_index = ob.material_index;
     }
     if (ts.sph.t < h.t) {  // no sphere -> F32_MAX
@@ -439,12 +442,17 @@ __device__ __forceinline__ Hit trace_end(const SceneView& sv, const KernelArgs& 
         const float t = ts.sph.t;
         const f3 p = o + d * t;
         const f3 outward = normalize(p - ld3(s));
-        const float theta = acosf_c(-outward.y);
-        const float phi = atan2f_c(-outward.z, outward.x) + kWgslPi;
         h.t = t;
         h.p = p;
-        h.u = div_const(phi, kTwoPiWgsl, kInvTwoPiWgsl);  // exact: rt_math_selftest
-        h.v = div_const(theta, kWgslPi, kInvWgslPi);
+        // uv feeds only the texel fetch, and with 1x1 texture layers every uv
+        // maps to texel (0, 0) (texel_coord clamps to [0, size-1]): the
+        // acos/atan2 are then skipped (bit-identical; 4% of a C2 frame)
+        if (ka.tex_w != 1u || ka.tex_h != 1u) {
+            const float theta = acosf_c(-outward.y);
+            const float phi = atan2f_c(-outward.z, outward.x) + kWgslPi;
+            h.u = div_const(phi, kTwoPiWgsl, kInvTwoPiWgsl);  // exact: rt_math_selftest
+            h.v = div_const(theta, kWgslPi, kInvWgslPi);
+        }
         h.front_face = dot(d, outward) < 0.0f;
         h.n = h.front_face ? outward : -outward;
         h.material_index = sv.sph_mat[ts.sph.orig];

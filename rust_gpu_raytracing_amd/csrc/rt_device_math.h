@@ -250,8 +250,13 @@ __device__ __forceinline__ float random01(uint32_t& seed) {
 __device__ __forceinline__ float normal01(uint32_t& seed) {
     const float theta = kBoxMullerTwoPi * random01(seed);
     // -2 log(r), r in {0} U [2^-32, 1]: -0, +inf, or >= 1.1e-7 (sqrt_rn_nrm's domain)
+#ifdef RT_EXP_HW_TRANSCENDENTALS  // timing experiment only: hardware log/cos (not the contract)
+    const float rho = sqrt_rn_nrm(-2.0f * __logf(random01(seed)));
+    return rho * __cosf(theta);
+#else
     const float rho = sqrt_rn_nrm(-2.0f * logf_c(random01(seed)));
     return rho * cosf_c(theta);
+#endif
 }
 
 }  // namespace rtk
