@@ -55,7 +55,7 @@ def algorithmic_bytes(owned_pixels: int, rays: float, scene_bytes: int) -> float
 
 def scene_bytes(scene) -> int:
     objs, subs, tris = scene.flatten()
-    return int(scene.spheres.nbytes + scene.materials.nbytes + objs.nbytes + subs.nbytes + tris.shape[0] * 80)
+    return int(scene.spheres.nbytes + scene.materials.nbytes + objs.nbytes + subs.nbytes + tris.shape[0] * 64)
 
 
 def pmc_traffic(workload: str):

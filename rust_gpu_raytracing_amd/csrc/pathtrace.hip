@@ -149,6 +149,16 @@ struct TriHit {
     bool front;
 };
 
+// The four vectors of a triangle the intersection test reads (the first 48 B
+// of its record; face_normal is read only for the closest hit).
+struct TriGeom {
+    f3 a, ab, ac, cn;
+};
+__device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t, uint32_t i) {
+    const float4 p0 = t[i].p0, p1 = t[i].p1, p2 = t[i].p2;
+    return TriGeom{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w)};
+}
+
 // check_triangles, compute_shader.wgsl:422-517: the reference's own sweep over
 // objects -> sub-objects -> triangles (first wins on equal distance, `>=`
 // rejects, :457). Used when the accelerator is off, and as the fallback for
@@ -169,17 +179,16 @@ __device__ __forceinline__ TriHit sweep_triangles(const SceneView& sv, const Ker
             if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
             for (uint32_t j = 0; j < sub.triangle_count; ++j) {
                 const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
-                const RtTriangleHot& tr = ka.triangles[ti];
-                const f3 cn = ld3(tr.calc_normal);
-                const float det = -dot(d, cn);
+                const TriGeom g = load_tri(ka.triangles, ti);
+                const float det = -dot(d, g.cn);
                 const float inv_det = 1.0f / det;
-                const f3 ao = o - ld3(tr.a);
-                const float dist = dot(ao, cn) * inv_det;
+                const f3 ao = o - g.a;
+                const float dist = dot(ao, g.cn) * inv_det;
                 if (dist < 0.0f || dist >= closest) continue;
                 const f3 dao = cross(ao, d);
-                const float v = -dot(ld3(tr.edge_ab), dao) * inv_det;
+                const float v = -dot(g.ab, dao) * inv_det;
                 if (v < 0.0f) continue;
-                const float u = dot(ld3(tr.edge_ac), dao) * inv_det;
+                const float u = dot(g.ac, dao) * inv_det;
                 if (u < 0.0f) continue;
                 const float w = 1.0f - u - v;
                 if (w < 0.0f) continue;
@@ -298,19 +307,18 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     for (uint32_t j = 0; j < sub.triangle_count; ++j) {
         const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
         const uint32_t seq = pr.z + j;
-        const RtTriangleHot& tr = ka.triangles[ti];
-        const f3 cn = ld3(tr.calc_normal);
-        const float det = -dot(d, cn);
+        const TriGeom g = load_tri(ka.triangles, ti);
+        const float det = -dot(d, g.cn);
         const float inv_det = 1.0f / det;
-        const f3 ao = o - ld3(tr.a);
-        const float dist = dot(ao, cn) * inv_det;
+        const f3 ao = o - g.a;
+        const float dist = dot(ao, g.cn) * inv_det;
         const bool nan_dist = dist != dist;
         if (dist < 0.0f) continue;
         if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) continue;
         const f3 dao = cross(ao, d);
-        const float v = -dot(ld3(tr.edge_ab), dao) * inv_det;
+        const float v = -dot(g.ab, dao) * inv_det;
         if (v < 0.0f) continue;
-        const float u = dot(ld3(tr.edge_ac), dao) * inv_det;
+        const float u = dot(g.ac, dao) * inv_det;
         if (u < 0.0f) continue;
         const float w = 1.0f - u - v;
         if (w < 0.0f) continue;
@@ -423,7 +431,7 @@ __device__ __forceinline__ Hit trace_end(const SceneView& sv, const KernelArgs& 
     h.v = 0.f;
     if (kTris && ts.tri.t != kF32Max) {  // found (the sweep can accept a NaN distance, :457)
         const RtObject& ob = sv.obj[ts.tri.obj];
-        const f3 fn = ld3(ka.triangles[ts.tri.tri].face_normal);
+        const f3 fn = ld3(ka.triangles[ts.tri.tri].fn);
         h.front_face = ts.tri.front;
         h.n = ts.tri.front ? fn : -fn;
         h.t = ts.tri.t;

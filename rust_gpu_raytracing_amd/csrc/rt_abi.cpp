@@ -398,11 +398,7 @@ int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     RtTriangleHot* hot = static_cast<RtTriangleHot*>(p);
     for (uint32_t i = 0; i < n; i++) {
         const rt_scene_triangle& s = t[i];
-        hot[i].a = make_float4(s.a[0], s.a[1], s.a[2], 0.f);
-        hot[i].edge_ab = make_float4(s.edge_ab[0], s.edge_ab[1], s.edge_ab[2], 0.f);
-        hot[i].edge_ac = make_float4(s.edge_ac[0], s.edge_ac[1], s.edge_ac[2], 0.f);
-        hot[i].calc_normal = make_float4(s.calc_normal[0], s.calc_normal[1], s.calc_normal[2], 0.f);
-        hot[i].face_normal = make_float4(s.face_normal[0], s.face_normal[1], s.face_normal[2], 0.f);
+        hot[i] = pack_triangle(s.a, s.edge_ab, s.edge_ac, s.calc_normal, s.face_normal);
     }
     if ((rc = staged_copy(ctx, ctx->d_tri, (size_t)n * sizeof(RtTriangleHot))) ||
         (rc = staging(ctx, (size_t)n * 32, &p)))
@@ -1100,7 +1096,7 @@ int rt_read_triangles(rt_ctx* ctx, rt_scene_triangle* out, uint32_t count) {
     if (count == 0) return RT_OK;
     std::vector<RtTriangleHot> hot(count);
     std::vector<float4> b(2 * (size_t)count);
-    RT_HIP(ctx, hipMemcpyAsync(hot.data(), ctx->d_tri, (size_t)count * 80, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipMemcpyAsync(hot.data(), ctx->d_tri, (size_t)count * sizeof(RtTriangleHot), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipMemcpyAsync(b.data(), ctx->d_tri_bounds, (size_t)count * 32, hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     auto put = [](float* dst, const float4& v) {
@@ -1111,11 +1107,7 @@ int rt_read_triangles(rt_ctx* ctx, rt_scene_triangle* out, uint32_t count) {
     for (uint32_t i = 0; i < count; i++) {
         rt_scene_triangle& t = out[i];
         std::memset(&t, 0, sizeof(t));
-        put(t.a, hot[i].a);
-        put(t.edge_ab, hot[i].edge_ab);
-        put(t.edge_ac, hot[i].edge_ac);
-        put(t.calc_normal, hot[i].calc_normal);
-        put(t.face_normal, hot[i].face_normal);
+        unpack_triangle(hot[i], t.a, t.edge_ab, t.edge_ac, t.calc_normal, t.face_normal);
         put(t.min_bounds, b[2 * i]);
         put(t.max_bounds, b[2 * i + 1]);
     }

@@ -2,7 +2,7 @@
 //
 // The records are the reference's GPU layouts (src/buffers.rs:7-129,
 // compute_shader.wgsl:43-126) except the triangle, which is repacked on upload
-// to the 80 bytes the kernel reads (the reference's 112-byte SceneTriangle
+// to the 64 bytes the kernel reads (the reference's 112-byte SceneTriangle
 // carries per-triangle bounds the shader never touches).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -43,19 +43,41 @@ struct RtSubObject {  // src/buffers.rs:124-129, 32 B
     uint32_t triangle_count;
 };
 
-struct RtTriangleHot {  // the 80 B of SceneTriangle (src/buffers.rs:49-64) the kernel reads
-    float4 a;
-    float4 edge_ab;
-    float4 edge_ac;
-    float4 calc_normal;
-    float4 face_normal;
+// The SceneTriangle fields the kernel reads (src/buffers.rs:49-64), 64 B: the
+// four vectors of the intersection test packed into the first 48 B (three
+// 16-B loads), face_normal (read only for the closest hit) last. A record never
+// straddles a 128-B line, and a sub-object's 7 triangles span 448 B.
+struct RtTriangleHot {
+    float4 p0;  // a.x a.y a.z edge_ab.x
+    float4 p1;  // edge_ab.y edge_ab.z edge_ac.x edge_ac.y
+    float4 p2;  // edge_ac.z calc_normal.x calc_normal.y calc_normal.z
+    float4 fn;  // face_normal.x face_normal.y face_normal.z 0
 };
+
+__host__ __device__ inline RtTriangleHot pack_triangle(const float* a, const float* ab, const float* ac,
+                                                       const float* cn, const float* fn) {
+    RtTriangleHot h;
+    h.p0 = make_float4(a[0], a[1], a[2], ab[0]);
+    h.p1 = make_float4(ab[1], ab[2], ac[0], ac[1]);
+    h.p2 = make_float4(ac[2], cn[0], cn[1], cn[2]);
+    h.fn = make_float4(fn[0], fn[1], fn[2], 0.f);
+    return h;
+}
+
+__host__ __device__ inline void unpack_triangle(const RtTriangleHot& h, float* a, float* ab, float* ac, float* cn,
+                                                float* fn) {
+    a[0] = h.p0.x, a[1] = h.p0.y, a[2] = h.p0.z;
+    ab[0] = h.p0.w, ab[1] = h.p1.x, ab[2] = h.p1.y;
+    ac[0] = h.p1.z, ac[1] = h.p1.w, ac[2] = h.p2.x;
+    cn[0] = h.p2.y, cn[1] = h.p2.z, cn[2] = h.p2.w;
+    fn[0] = h.fn.x, fn[1] = h.fn.y, fn[2] = h.fn.z;
+}
 
 static_assert(sizeof(RtSphere) == 32, "SceneSphere layout");
 static_assert(sizeof(RtMaterial) == 32, "SceneMaterial layout");
 static_assert(sizeof(RtObject) == 48, "ObjectInfo layout");
 static_assert(sizeof(RtSubObject) == 32, "SubObjectInfo layout");
-static_assert(sizeof(RtTriangleHot) == 80, "hot triangle layout");
+static_assert(sizeof(RtTriangleHot) == 64, "hot triangle layout");
 
 // Cost-ordered tile schedule: buckets of the counting sort (pathtrace.hip,
 // sort_tiles_by_cost), whose scratch reuses the LDS tail after the frame loop.

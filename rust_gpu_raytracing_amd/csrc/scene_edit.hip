@@ -9,7 +9,7 @@
 // edit costs a few small launches and no host round trip:
 //
 //   rt_edit_triangles_kernel   one thread per triangle: place its 3 points,
-//                              SceneTriangle::new -> the 80-B record the path
+//                              SceneTriangle::new -> the 64-B record the path
 //                              tracer reads + the per-triangle bounds
 //   rt_edit_sub_objects_kernel one thread per sub-object: get_bounding_box over
 //                              [min0, max0, min1, max1, ...] of its triangles
@@ -71,13 +71,7 @@ extern "C" __global__ void __launch_bounds__(256) rt_edit_triangles_kernel(
     place_point(pl, v, c);
     TriangleRecord r;
     scene_triangle(a, b, c, r);
-    RtTriangleHot h;
-    h.a = make_float4(a[0], a[1], a[2], 0.f);
-    h.edge_ab = make_float4(r.ab[0], r.ab[1], r.ab[2], 0.f);
-    h.edge_ac = make_float4(r.ac[0], r.ac[1], r.ac[2], 0.f);
-    h.calc_normal = make_float4(r.calc_normal[0], r.calc_normal[1], r.calc_normal[2], 0.f);
-    h.face_normal = make_float4(r.face_normal[0], r.face_normal[1], r.face_normal[2], 0.f);
-    tris[t] = h;
+    tris[t] = pack_triangle(a, r.ab, r.ac, r.calc_normal, r.face_normal);
     bounds[2 * (size_t)t] = make_float4(r.mn[0], r.mn[1], r.mn[2], 0.f);
     bounds[2 * (size_t)t + 1] = make_float4(r.mx[0], r.mx[1], r.mx[2], 0.f);
 }
