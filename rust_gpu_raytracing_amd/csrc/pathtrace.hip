@@ -255,6 +255,11 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
     }
     ts.slab = slab_ray(o.x, o.y, o.z, ts.inv.x, ts.inv.y, ts.inv.z, m);
     ts.limit = phase == 0 ? __builtin_inff() : prune_limit(ts);
+    if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
+        const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
+                             ((__float_as_uint(ts.inv.z) >> 31) << 2);
+        ts.node = oct * ka.sphere_octant_stride;
+    }
 }
 
 // kTris: the scene has objects (triangles); false compiles the triangle side out.

@@ -158,6 +158,7 @@ struct rt_ctx {
     bool slots_dirty = true;
     uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
     bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
+    bool sphere_octants = true;          // RT_SPHERE_OCTANTS=0: one BVH layout (A/B switch)
     uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
     uint32_t n_always = 0, n_nodes = 0, n_slots = 0;
     float sphere_extent = 0.0f;
@@ -301,11 +302,13 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     build_sphere_slots(ctx->h_sph.data(), count, ctx->use_bvh, &sl, ctx->sphere_leaf_max);
     std::vector<uint32_t> mat(count);
     for (uint32_t i = 0; i < count; i++) mat[i] = ctx->h_sph[i].material_index;
+    std::vector<SphereBvhNode> oct;  // 8 direction-ordered copies; layout 0 alone is a complete walk too
+    order_bvh_by_octant(sl.nodes, &oct);
     int rc;
     if ((rc = upload_raw(ctx, ctx->d_slot_sph, sl.slot_sph.data(), sl.slot_sph.size() * 4)) ||
         (rc = upload_raw(ctx, ctx->d_slot_orig, sl.slot_orig.data(), sl.slot_orig.size() * 4)) ||
         (rc = upload_raw(ctx, ctx->d_sph_mat, mat.data(), mat.size() * 4)) ||
-        (rc = upload_raw(ctx, ctx->d_bvh, sl.nodes.data(), sl.nodes.size() * sizeof(SphereBvhNode))))
+        (rc = upload_raw(ctx, ctx->d_bvh, oct.data(), oct.size() * sizeof(SphereBvhNode))))
         return rc;
     ctx->n_always = sl.n_always;
     ctx->n_slots = (uint32_t)sl.slot_orig.size();
@@ -565,6 +568,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
         ctx->use_bvh = !(env && env[0] == '0');
+        env = std::getenv("RT_SPHERE_OCTANTS");
+        ctx->sphere_octants = !(env && env[0] == '0');
         env = std::getenv("RT_QUEUE_STRIPES");
         if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TRAV_THRESHOLD");
@@ -595,7 +600,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         (rc = dev_alloc(ctx, &ctx->d_slot_sph, 4 * (size_t)info->sphere_count + 4)) ||  // padded groups
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
-        (rc = dev_alloc(ctx, &ctx->d_bvh, 2 * (size_t)info->sphere_count)) ||
+        (rc = dev_alloc(ctx, &ctx->d_bvh, 16 * (size_t)info->sphere_count + 8)) ||  // 8 ordered layouts
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
         (rc = dev_alloc(ctx, &ctx->d_tri_bounds, 2 * (size_t)ctx->n_tri_dev)) ||
@@ -871,31 +876,45 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
 
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
-    size_t off = al16((size_t)ctx->n_slots * 16);
-    ka.lds_mat_offset = (uint32_t)off;
-    off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
-    ka.lds_obj_offset = (uint32_t)off;
-    off = al16(off + (size_t)p.object_count * sizeof(RtObject));
-    ka.lds_orig_offset = (uint32_t)off;
-    off = al16(off + (size_t)ctx->n_slots * 4);
-    ka.lds_smat_offset = (uint32_t)off;
-    off = al16(off + (size_t)p.sphere_count * 4);
-    ka.lds_nodes_offset = (uint32_t)off;
-    off = al16(off + (size_t)ctx->n_nodes * sizeof(SphereBvhNode));
-    const size_t mode1_bytes = off + kLdsTailBytes;
-    ka.lds_tri_nodes_offset = (uint32_t)off;
-    off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
-    ka.lds_tri_prims_offset = (uint32_t)off;
-    off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
-    const size_t mode2_bytes = off + kLdsTailBytes;
-    int mode = 0;
     const bool tris = p.object_count != 0;  // else the sphere-only kernels
-    if (!ctx->force_global_scene) {
-        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes <= kLdsAccelBudget && ctx->max_lds_mode >= 2)
-            mode = 2;
-        else if (mode1_bytes <= kLdsSceneBudget && ctx->max_lds_mode >= 1)
-            mode = 1;
+    size_t mode1_bytes = 0, mode2_bytes = 0;
+    // lays out the LDS image for `layouts` sphere BVH layouts and returns the LDS mode it fits
+    auto carve = [&](uint32_t layouts, size_t mode1_budget) -> int {
+        size_t off = al16((size_t)ctx->n_slots * 16);
+        ka.lds_mat_offset = (uint32_t)off;
+        off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
+        ka.lds_obj_offset = (uint32_t)off;
+        off = al16(off + (size_t)p.object_count * sizeof(RtObject));
+        ka.lds_orig_offset = (uint32_t)off;
+        off = al16(off + (size_t)ctx->n_slots * 4);
+        ka.lds_smat_offset = (uint32_t)off;
+        off = al16(off + (size_t)p.sphere_count * 4);
+        ka.lds_nodes_offset = (uint32_t)off;
+        off = al16(off + (size_t)layouts * ctx->n_nodes * sizeof(SphereBvhNode));
+        mode1_bytes = off + kLdsTailBytes;
+        ka.lds_tri_nodes_offset = (uint32_t)off;
+        off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
+        ka.lds_tri_prims_offset = (uint32_t)off;
+        off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
+        mode2_bytes = off + kLdsTailBytes;
+        if (ctx->force_global_scene) return 0;
+        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes <= kLdsAccelBudget && ctx->max_lds_mode >= 2) return 2;
+        if (mode1_bytes <= mode1_budget && ctx->max_lds_mode >= 1) return 1;
+        return 0;
+    };
+    // Direction-ordered sphere BVH layouts (order_bvh_by_octant) when all eight
+    // fit the LDS mode that one layout gets (up to the mode-2 budget, in fewer,
+    // larger workgroups); otherwise layout 0 alone.
+    int mode = carve(1, kLdsSceneBudget);
+    uint32_t layouts = 1;
+    if (ctx->sphere_octants && ctx->n_nodes != 0) {
+        if (carve(8, kLdsAccelBudget) == mode)
+            layouts = 8;
+        else
+            carve(1, kLdsSceneBudget);
     }
+    ka.sphere_nodes = layouts * ctx->n_nodes;
+    ka.sphere_octant_stride = layouts == 8 ? ctx->n_nodes : 0u;
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
     ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);
     size_t lds_bytes;

@@ -1,3 +1,4 @@
+#include <functional>
 // sphere_bvh.cpp — binned-SAH BVH over spheres, flattened depth-first with
 // skip links for stackless traversal on the GPU.
 #include "sphere_bvh.h"
@@ -134,6 +135,43 @@ void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, u
     Builder b{prims, *nodes, {}, leaf_max};
     b.build(0, (uint32_t)n);
     *leaf_order = std::move(b.leaf_order);
+}
+
+void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out) {
+    out->clear();
+    const uint32_t n = (uint32_t)in.size();
+    if (n == 0) return;
+    out->reserve(8 * (size_t)n);
+    const uint32_t end_all = 8u * n;
+    for (uint32_t oct = 0; oct < 8; oct++) {
+        const uint32_t base = (uint32_t)out->size();
+        // pre-order re-emission (recursion depth = tree depth)
+        std::function<void(uint32_t)> emit = [&](uint32_t src) {
+            const uint32_t at = (uint32_t)out->size();
+            out->push_back(in[src]);
+            if (in[src].leaf == kSphereBvhInternal) {
+                uint32_t a = src + 1, b = in[src + 1].skip;  // left child, right child
+                int axis = 0;
+                double best = -1.0, diff = 0.0;
+                for (int k = 0; k < 3; k++) {
+                    const double ca = 0.5 * ((double)in[a].bmin[k] + (double)in[a].bmax[k]);
+                    const double cb = 0.5 * ((double)in[b].bmin[k] + (double)in[b].bmax[k]);
+                    if (std::fabs(cb - ca) > best) {
+                        best = std::fabs(cb - ca);
+                        axis = k;
+                        diff = cb - ca;
+                    }
+                }
+                const bool negative = (oct >> axis) & 1u;  // this octant's rays travel towards -axis
+                if ((diff < 0.0) != negative) std::swap(a, b);  // a: met first along the travel direction
+                emit(a);
+                emit(b);
+            }
+            const uint32_t after = (uint32_t)out->size();
+            (*out)[at].skip = after == base + n ? end_all : after;
+        };
+        emit(0);
+    }
 }
 
 void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, const rt_sub_object_info* subs,

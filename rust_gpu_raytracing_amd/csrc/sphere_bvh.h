@@ -50,6 +50,17 @@ struct SphereSlots {
 void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use_bvh, SphereSlots* out,
                         uint32_t leaf_max = kSphereBvhLeafMax);
 
+// Direction-ordered copies of a depth-first BVH (same boxes and leaves): layout
+// k (k = octant of the ray direction: bit 0 set if d.x < 0, bit 1 d.y, bit 2 d.z)
+// lists, at every internal node, first the child that a ray of that octant
+// reaches first along the axis that separates the two children's centres
+// most, so the stackless skip walk visits near children first and its
+// distance pruning starts early. The 8 layouts are concatenated (node indices
+// and skips absolute); a skip that leaves a layout is 8 * nodes.size(), so
+// "node >= total" ends every walk. Visiting order does not change the result
+// (the lexicographic minimum, conservative pruning).
+void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out);
+
 // Generic builder: binned-SAH BVH over axis-aligned boxes (lo/hi, 3 floats each
 // per primitive), leaves of at most `leaf_max` primitives. Returns depth-first
 // nodes (same layout as SphereBvhNode; leaf = first | count << 24 indexing

@@ -106,6 +106,10 @@ static Res ordered_like(const SphereSlots& sl, V o, V d) {
     return {bt, found ? (int)bo : -1};
 }
 
+// The kernel walks the direction-ordered layouts (order_bvh_by_octant) unless
+// SINGLE_LAYOUT is set: g_oct holds them for the scene under test.
+static std::vector<SphereBvhNode> g_oct;
+
 static Res kernel_like(const SphereSlots& sl, V o, V d) {
     float bt = F32_MAX_;
     uint32_t bo = 0;
@@ -122,10 +126,16 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
         if (getenv("SLACK_SCALE")) slack *= (float)atof(getenv("SLACK_SCALE"));
         V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
         const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);  // the kernel's slab test
-        uint32_t node = 0;
-        while (node < n) {
+        const bool oct = !getenv("SINGLE_LAYOUT");
+        if (oct && g_oct.size() != 8 * (size_t)n) order_bvh_by_octant(sl.nodes, &g_oct);
+        const SphereBvhNode* nodes = oct ? g_oct.data() : sl.nodes.data();
+        const uint32_t total = oct ? 8 * n : n;
+        uint32_t node = oct ? n * ((std::signbit(inv.x) ? 1u : 0u) | (std::signbit(inv.y) ? 2u : 0u) |
+                                   (std::signbit(inv.z) ? 4u : 0u))
+                            : 0u;
+        while (node < total) {
             g_nodes++;
-            const SphereBvhNode& nd = sl.nodes[node];
+            const SphereBvhNode& nd = nodes[node];
             float near_t, far_t;
             slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], near_t, far_t);
             bool hit = near_t <= far_t && far_t >= -slack && near_t <= bt * 1.00001f + slack;
