@@ -319,7 +319,8 @@ RT_API int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
 /* Device self-check of the kernel's fast exact-arithmetic helpers against the
  * IEEE operations they replace, over every f32 input (current device):
  * which 0 = sqrt on {+-0} U [2^-96, inf], 1..4 = x / 2pi, x / pi, x / 255,
- * x / 10. *mismatches = number of differing results (0 = bit-exact),
+ * x / 10; 5: the Box-Muller log, 6: its cos, on every value random01 returns.
+ * *mismatches = number of differing results (0 = bit-exact),
  * *first_bad = smallest differing input's bit pattern (0xffffffff if none). */
 RT_API int rt_math_selftest(uint32_t which, uint64_t* mismatches, uint32_t* first_bad);
 

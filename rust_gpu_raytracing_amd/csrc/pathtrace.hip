@@ -1320,9 +1320,20 @@ extern "C" __global__ void __launch_bounds__(256) rt_math_selftest_kernel(uint32
         } else if (which == 3) {
             got = div_const(x, 255.0f, kInv255);
             want = x / 255.0f;
-        } else {
+        } else if (which == 4) {
             got = div_const(x, 10.0f, kInv10);
             want = x / 10.0f;
+        } else {
+            // every value random01 returns: its seed word / 2^32 (the seed is any u32)
+            const float u = (float)bits / 4294967296.0f;
+            if (which == 5) {
+                got = logf_u01(u);
+                want = logf_c(u);
+            } else {
+                const float theta = kBoxMullerTwoPi * u;
+                got = cosf_box(theta);
+                want = cosf_c(theta);
+            }
         }
         const bool same = __float_as_uint(got) == __float_as_uint(want) || (got != got && want != want);
         if (!same) {

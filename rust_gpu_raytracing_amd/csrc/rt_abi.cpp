@@ -1302,7 +1302,7 @@ void* rt_stream(rt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 }  // extern "C"
 
 int rt_math_selftest(uint32_t which, uint64_t* mismatches, uint32_t* first_bad) {
-    if (!mismatches || !first_bad || which > 4) return RT_E_INVALID;
+    if (!mismatches || !first_bad || which > 6) return RT_E_INVALID;
     unsigned long long* d_bad = nullptr;
     uint32_t* d_first = nullptr;
     hipError_t e = hipMalloc(&d_bad, sizeof(unsigned long long));

@@ -237,6 +237,61 @@ __device__ __forceinline__ float pow5(float x) {
     return (x2 * x2) * x;
 }
 
+// logf_c and cosf_c restricted to what normal01 feeds them: r = random01() in
+// {0} U [2^-32, 1] (never NaN, negative, infinite or denormal) and
+// theta = kBoxMullerTwoPi * r in [0, 2*pi]. Same operations on that domain,
+// without the special-value branches and with both polynomials evaluated and
+// selected (branch-free: the lanes of a wave disagree on the octant anyway).
+// rt_math_selftest (which 5, 6) compares them bit for bit with logf_c / cosf_c
+// over all 2^32 values random01 can return.
+__device__ __forceinline__ float logf_u01(float x) {
+    const uint32_t b = __float_as_uint(x);
+    int e = (int)((b >> 23) & 0xffu) - 126;
+    float m = __uint_as_float((b & 0x007fffffu) | 0x3f000000u);  // [0.5, 1)
+    const bool lo = m < 0.70710678118654752f;
+    e = lo ? e - 1 : e;
+    m = lo ? m + m - 1.0f : m - 1.0f;
+    const float z = m * m;
+    float y = 7.0376836292e-2f;
+    y = y * m - 1.1514610310e-1f;
+    y = y * m + 1.1676998740e-1f;
+    y = y * m - 1.2420140846e-1f;
+    y = y * m + 1.4249322787e-1f;
+    y = y * m - 1.6668057665e-1f;
+    y = y * m + 2.0000714765e-1f;
+    y = y * m - 2.4999993993e-1f;
+    y = y * m + 3.3333331174e-1f;
+    y = y * m * z;
+    const float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    const float r = m + y;
+    return x == 0.0f ? -__builtin_inff() : r + 0.693359375f * fe;
+}
+
+__device__ __forceinline__ float cosf_box(float x) {
+    int j = (int)(1.27323954473516f * x);
+    float y = (float)j;
+    const bool odd = (j & 1) != 0;
+    j = odd ? j + 1 : j;
+    y = odd ? y + 1.0f : y;
+    j &= 7;
+    const bool neg = (j > 3) != ((j & 3) > 1);
+    j &= 3;
+    const float r = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    const float z = r * r;
+    float ps = -1.9515295891e-4f;
+    ps = ps * z + 8.3321608736e-3f;
+    ps = ps * z - 1.6666654611e-1f;
+    const float s_res = ps * z * r + r;
+    float pc = 2.443315711809948e-5f;
+    pc = pc * z - 1.388731625493765e-3f;
+    pc = pc * z + 4.166664568298827e-2f;
+    const float c_res = pc * z * z - 0.5f * z + 1.0f;
+    const float res = (j == 1 || j == 2) ? s_res : c_res;
+    return neg ? -res : res;
+}
+
 // PCG hash RNG, compute_shader.wgsl:587-599 + normalize_u32 :630-632.
 __device__ __forceinline__ float random01(uint32_t& seed) {
     const uint32_t state = seed * 747796405u + 2891336453u;
@@ -254,8 +309,8 @@ __device__ __forceinline__ float normal01(uint32_t& seed) {
     const float rho = sqrt_rn_nrm(-2.0f * __logf(random01(seed)));
     return rho * __cosf(theta);
 #else
-    const float rho = sqrt_rn_nrm(-2.0f * logf_c(random01(seed)));
-    return rho * cosf_c(theta);
+    const float rho = sqrt_rn_nrm(-2.0f * logf_u01(random01(seed)));
+    return rho * cosf_box(theta);
 #endif
 }
 

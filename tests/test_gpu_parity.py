@@ -477,7 +477,8 @@ def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib):
 
 
 @pytest.mark.parametrize("which,name", [(0, "sqrt on {0} U [2^-96, inf]"), (1, "x / 2pi"), (2, "x / pi"),
-                                        (3, "x / 255"), (4, "x / 10")])
+                                        (3, "x / 255"), (4, "x / 10"), (5, "Box-Muller log on random01's range"),
+                                        (6, "Box-Muller cos on 2pi * random01's range")])
 def test_gpu_fast_exact_math_selftest(gpu, which, name):
     """The kernel's short correctly-rounded sqrt and constant divisions equal the IEEE
     operations bit for bit over every f32 input of their domain (exhaustive, on the device)."""
