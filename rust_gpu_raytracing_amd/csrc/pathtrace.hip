@@ -487,11 +487,18 @@ __device__ __forceinline__ uint32_t fetch_texture(const KernelArgs& ka, uint32_t
 }
 
 __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb, f3 d) {
-    // environment_map_coords, :580-585
-    const float u = 0.5f + div_const(atan2f_c(d.z, d.x), kTwoPiWgsl, kInvTwoPiWgsl);
-    const float v = 0.5f + div_const(asinf_c(d.y), kWgslPi, kInvWgslPi);
-    const int x = texel_coord(u * (float)(int32_t)ka.env_map_width, ka.env_w);
-    const int y = texel_coord(v * (float)(int32_t)ka.env_map_height, ka.env_h);
+    // environment_map_coords, :580-585. A coordinate is computed only when the
+    // texel depends on it: with every row (column) of the map one colour, any u
+    // (v) -- NaN included -- fetches the same texel as column (row) 0.
+    int x = 0, y = 0;
+    if (!(ka.env_uniform & 1u)) {
+        const float u = 0.5f + div_const(atan2f_c(d.z, d.x), kTwoPiWgsl, kInvTwoPiWgsl);
+        x = texel_coord(u * (float)(int32_t)ka.env_map_width, ka.env_w);
+    }
+    if (!(ka.env_uniform & 2u)) {
+        const float v = 0.5f + div_const(asinf_c(d.y), kWgslPi, kInvWgslPi);
+        y = texel_coord(v * (float)(int32_t)ka.env_map_height, ka.env_h);
+    }
 #ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
     return decode_texel(0xffc0a080u ^ (uint32_t)(y * ka.env_w + x), srgb);
 #else

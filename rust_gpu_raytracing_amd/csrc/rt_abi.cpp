@@ -194,6 +194,7 @@ struct rt_ctx {
     uint32_t tex_w = 0, tex_h = 0, tex_layers = 0;
     uint32_t* d_env = nullptr;
     uint32_t env_w = 0, env_h = 0;
+    uint32_t env_uniform = 3;  // bit 0: every row one colour, bit 1: every column (sample_env skips u / v)
     float* d_srgb = nullptr;
 
     // host-side copies used for validation of index ranges
@@ -691,6 +692,23 @@ int rt_upload_env_map(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_
     }
     ctx->env_w = width;
     ctx->env_h = height;
+    // A map whose rows (columns) are each one colour returns the same texel for
+    // any u (v): the kernel then skips that coordinate's atan2 (asin).
+    const uint32_t* t = reinterpret_cast<const uint32_t*>(rgba8);
+    bool rows = true, cols = true;
+    for (size_t y = 0; y < height && rows; y++)
+        for (size_t x = 1; x < width; x++)
+            if (t[y * width + x] != t[y * width]) {
+                rows = false;
+                break;
+            }
+    for (size_t y = 1; y < height && cols; y++)
+        for (size_t x = 0; x < width; x++)
+            if (t[y * width + x] != t[x]) {
+                cols = false;
+                break;
+            }
+    ctx->env_uniform = (rows ? 1u : 0u) | (cols ? 2u : 0u);
     return upload_raw(ctx, ctx->d_env, rgba8, texels * 4);
 }
 
@@ -860,6 +878,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tex_layers = ctx->tex_layers;
     ka.env_w = ctx->env_w;
     ka.env_h = ctx->env_h;
+    ka.env_uniform = ctx->env_uniform;
     ka.height = ctx->height;
     ka.gen_rays = ctx->gen_rays ? 1u : 0u;
     ka.aspect = (float)ctx->width / (float)ctx->height;  // src/camera.rs:142

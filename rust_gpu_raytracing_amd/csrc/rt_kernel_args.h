@@ -158,6 +158,7 @@ struct KernelArgs {
     uint32_t triangle_count;
     uint32_t tex_w, tex_h, tex_layers;
     uint32_t env_w, env_h;
+    uint32_t env_uniform;  // bit 0: env map rows uniform (u unused), bit 1: columns uniform (v unused)
     // launch geometry
     uint32_t height;
     uint32_t bounces;

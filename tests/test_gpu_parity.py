@@ -61,6 +61,31 @@ def test_gpu_matches_oracle_full_frame(gpu, oracle_lib, config, w, h, frames, kw
     assert_same(acc, out, rays, acc_o, out_o, rays_o)
 
 
+@pytest.mark.parametrize("kind", ["cols_uniform", "rows_uniform", "both_uniform", "one_texel_off", "random"])
+def test_gpu_env_map_uniform_rows_columns(gpu, oracle_lib, kind):
+    """sample_env skips u (v) when every row (column) of the env map is one colour
+    (rt_upload_env_map detects it): each case, and a map one texel away from
+    uniform rows, must equal the oracle, which always computes both coordinates."""
+    scene, bounces = build_config("c2_rtiow", width=160, height=96)
+    rng = np.random.default_rng(11)
+    eh, ew = 64, 128
+    if kind == "cols_uniform":
+        env = np.broadcast_to(rng.integers(0, 256, (1, ew, 4), dtype=np.uint8), (eh, ew, 4))
+    elif kind in ("rows_uniform", "one_texel_off"):
+        env = np.broadcast_to(rng.integers(0, 256, (eh, 1, 4), dtype=np.uint8), (eh, ew, 4))
+    elif kind == "both_uniform":
+        env = np.broadcast_to(np.array([40, 90, 200, 255], np.uint8), (eh, ew, 4))
+    else:
+        env = rng.integers(0, 256, (eh, ew, 4), dtype=np.uint8)
+    env = np.ascontiguousarray(env)
+    if kind == "one_texel_off":
+        env[eh // 2, ew // 3, 0] ^= 0x40
+    scene.environment_map = env
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
+    acc, out, rays = gpu_render(scene, bounces, 2)
+    assert_same(acc, out, rays, acc_o, out_o, rays_o)
+
+
 @pytest.mark.parametrize("config", ["c2_rtiow", "c3_chess", "c5_heightfield"])
 def test_gpu_full_size_sampled(gpu, oracle_lib, config):
     """BASELINE size (1920x1080, 8 bounces): every GPU pixel of 2 frames is checked on a
