@@ -89,7 +89,7 @@ struct SphereHit {
 __device__ __forceinline__ void sphere_candidate(float disc, float b, float two_a, uint32_t orig, uint32_t slot,
                                                  SphereHit& best) {
     if (disc >= 0.0f) {
-        const float t = (-b - sqrt_rn(disc)) / two_a;
+        const float t = (-b - sqrt_rn_any(disc)) / two_a;
         if (t > 0.0f && (t < best.t || (t == best.t && orig < best.orig))) {
             best.t = t;
             best.orig = orig;
@@ -606,7 +606,7 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
         } else {
             // refract, :316-325
             const f3 perp = (p.d + h.n * cos_t) * ior;
-            const float len = sqrt_rn(dot(perp, perp));
+            const float len = sqrt_rn_any(dot(perp, perp));
             const float len_sq = len * len;
             // |1 - len_sq| is 0 or >= 2^-24 (exact difference near 1): sqrt_rn_nrm's domain
             const f3 refr = perp + h.n * (-sqrt_rn_nrm(__builtin_fabsf(1.0f - len_sq)));

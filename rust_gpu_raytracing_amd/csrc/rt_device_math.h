@@ -49,6 +49,9 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
 // min/max returning the non-NaN operand (v_min_f32/v_max_f32 IEEE-mode semantics).
 __device__ __forceinline__ float fmin_nn(float a, float b) { return __builtin_fminf(a, b); }
 __device__ __forceinline__ float fmax_nn(float a, float b) { return __builtin_fmaxf(a, b); }
+#ifndef RT_SQRT_SPLIT
+#define RT_SQRT_SPLIT 1
+#endif
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 
 // Correctly rounded sqrt for x in {+-0} U [2^-96, +inf] (NaN and negative x give
@@ -82,7 +85,16 @@ __device__ __forceinline__ float div_const(float x, float c, float rc) {
     const float q2 = __builtin_fmaf(r, rc, q);
     return __builtin_isinf(x) ? q : q2;
 }
-__device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / sqrt_rn(dot(v, v))); }
+// Correctly rounded sqrt for any x: the short form on its proven domain (x >=
+// 2^-96, +inf included), the IEEE expansion for zeros, tiny and denormal x,
+// negatives and NaN (a branch whose slow side is all but never taken).
+__device__ __forceinline__ float sqrt_rn_any(float x) {
+#if RT_SQRT_SPLIT
+    if (__builtin_expect(x >= 0x1p-96f, 1)) return sqrt_rn_nrm(x);
+#endif
+    return sqrt_rn(x);
+}
+__device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / sqrt_rn_any(dot(v, v))); }
 __device__ __forceinline__ f3 lerp(f3 a, f3 b, float t) { return a + (b - a) * t; }
 
 __device__ __forceinline__ float logf_c(float x) {
