@@ -46,11 +46,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(owned_pixels: int, rays: float, scene_bytes: int) -> float:
-    """B = 52 B/px (ray dir 16 + accum 16 read + 16 write + RGBA8 4)
-    + 4 B per counted ray (one RGBA8 texel: texture on hit, env map on miss)
-    + the scene arrays read once."""
-    return 52.0 * owned_pixels + 4.0 * rays + scene_bytes
+def algorithmic_bytes(owned_pixels: int, rays: float, scene_bytes: int, frames: float = 1.0) -> float:
+    """SURVEY §8d, per launch: B = 52 B/px/frame (ray dir 16 + accum 16 read + 16 write +
+    RGBA8 4) + 4 B per counted ray (one RGBA8 texel: texture on hit, env map on miss)
+    + the scene arrays read once. A launch rendering F batched frames reads each
+    pixel's accumulation once and keeps it in a register between its frames:
+    16 + 36 F B/px (F = 1: the 52 B above)."""
+    return (16.0 + 36.0 * frames) * owned_pixels + 4.0 * rays + scene_bytes
 
 
 def scene_bytes(scene) -> int:
@@ -126,6 +128,8 @@ def main() -> int:
     ap.add_argument("--cpu-sample-world", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "1")),
+                    help="frames one launch may render (rt_set_frame_batch); 1 = one launch per frame")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="N>1: weak = N frames per step (1/N of the tiles each, per-GPU work fixed); "
                          "strong = one frame per step split N ways")
@@ -169,7 +173,7 @@ def main() -> int:
         height = int(round(args.height * scale / 8.0)) * 8
     scene, default_bounces = build_config(args.config, width=width, height=height)
     bounces = args.bounces or default_bounces
-    r = Renderer(scene, device=device, rank=rank, world_size=world)
+    r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=args.frame_batch)
     owned_px = r.owned_pixel_count()
 
     def step():
@@ -233,9 +237,9 @@ def main() -> int:
 
     if rank == 0:
         avg_kernel_s = kern_ms / max(n_timed, 1) / 1e3
-        rays_per_launch = rays / max(args.steps, 1)
-        # one launch reads/writes each owned pixel's framebuffer words once, whatever its frame count
-        b_launch = algorithmic_bytes(owned_px, rays_per_launch, scene_bytes(scene))
+        frames_per_launch = args.steps / max(n_timed, 1)
+        rays_per_launch = rays / max(n_timed, 1)
+        b_launch = algorithmic_bytes(owned_px, rays_per_launch, scene_bytes(scene), frames_per_launch)
         achieved = b_launch / avg_kernel_s / 1e9
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
         traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
@@ -263,6 +267,8 @@ def main() -> int:
                 "pixels_per_gpu": owned_px,
                 "rays_per_step": rays_total / args.steps,
                 "nominal_rays_per_step": width * height * bounces,
+                "frame_batch": args.frame_batch,
+                "launches": n_timed,
             },
             "roofline": {
                 "bound": "hbm",

@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -228,6 +228,23 @@ RT_API int rt_compute_frame(rt_ctx* ctx, uint32_t bounces);
  * per step. frames >= 1. Asynchronous. */
 RT_API int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
 
+/* Frame batching (new; the reference submits one dispatch per compute_frame,
+ * src/renderer.rs:238-249, and wgpu runs it later, asynchronously). With
+ * max_frames > 1, rt_compute_frame queues its frame (Params and k advance as
+ * always) and one launch renders the queued frames once max_frames are queued,
+ * when the bounce count changes, or before ANY other call on the context
+ * (readback, update, sync, timing, destroy). Inside the launch each pixel runs
+ * its frames back to back on one lane and every frame writes its accumulation
+ * and packed output, so every observable result -- buffers, ray count, k -- is
+ * that of the single-frame dispatches; what changes is that the persistent
+ * grid's fill and drain are paid once per batch instead of once per frame.
+ * 1 (the default; env RT_FRAME_BATCH) launches each frame at once.
+ * max_frames in [1, 64]. rt_frame_batch reports the setting and the frames
+ * queued; rt_flush launches them now. */
+RT_API int rt_set_frame_batch(rt_ctx* ctx, uint32_t max_frames);
+RT_API int rt_frame_batch(const rt_ctx* ctx, uint32_t* max_frames, uint32_t* pending);
+RT_API int rt_flush(rt_ctx* ctx);
+
 /* Blocks until all work on the context's stream has finished. */
 RT_API int rt_synchronize(rt_ctx* ctx);
 
@@ -302,6 +319,11 @@ RT_API int rt_pack_owned_accumulation(rt_ctx* ctx, void* dst_device);
  * the given accumulation divisor (k*c, src/compute_shader.wgsl:166). */
 RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size,
                            uint32_t divisor);
+/* The same for the packed RGBA8 output (one u32 per pixel, rt_owned_pixel_count
+ * * 4 bytes), copied as is: the gather of a non-accumulating render
+ * (Params.accumulate == 0 never writes the accumulation, compute_shader.wgsl:171-178). */
+RT_API int rt_pack_owned_output(rt_ctx* ctx, void* dst_device);
+RT_API int rt_unpack_output(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size);
 
 /* Launch geometry of the last rt_dispatch (diagnostics): workgroup size in
  * threads, workgroups launched, dynamic LDS bytes per workgroup, and the LDS

@@ -104,6 +104,9 @@ SIGNATURES = {
     "rt_dispatch": (ctypes.c_int, [_P, _U32]),
     "rt_compute_frame": (ctypes.c_int, [_P, _U32]),
     "rt_compute_frames": (ctypes.c_int, [_P, _U32, _U32]),
+    "rt_set_frame_batch": (ctypes.c_int, [_P, _U32]),
+    "rt_frame_batch": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_flush": (ctypes.c_int, [_P]),
     "rt_synchronize": (ctypes.c_int, [_P]),
     "rt_read_output": (ctypes.c_int, [_P, _P]),
     "rt_read_accumulation": (ctypes.c_int, [_P, _P]),
@@ -121,6 +124,8 @@ SIGNATURES = {
     "rt_owned_pixel_count": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_pack_owned_accumulation": (ctypes.c_int, [_P, _P]),
     "rt_unpack_accumulation": (ctypes.c_int, [_P, _P, _U32, _U32, _U32]),
+    "rt_pack_owned_output": (ctypes.c_int, [_P, _P]),
+    "rt_unpack_output": (ctypes.c_int, [_P, _P, _U32, _U32]),
     "rt_launch_config": (ctypes.c_int, [_P] + [ctypes.POINTER(ctypes.c_uint32)] * 4),
     "rt_debug_counters": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), _U32]),
     "rt_math_selftest": (ctypes.c_int, [_U32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),

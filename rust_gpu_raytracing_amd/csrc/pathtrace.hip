@@ -925,6 +925,27 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // next sample (random_index += 1, :162), its next frame (a multi-frame
     // launch runs the frames of one pixel back to back on its lane), or its
     // final write (:164-178).
+    // The end of one frame of the pixel (:164-178): the accumulation and the
+    // packed output as that frame's dispatch leaves them. Stored where the pixel
+    // finishes (holding them back to the next traversal phase measured no
+    // faster and costs 6 VGPRs).
+    auto store_frame = [&]() {
+        float r, g, b, a;
+        if (accumulate) {
+            const float div = (float)((ka.accumulation_index + frame) * ka.compute_per_frame);
+            r = clamp01(pix.x / div);
+            g = clamp01(pix.y / div);
+            b = clamp01(pix.z / div);
+            a = clamp01(pix.w / div);
+        } else {
+            r = clamp01(p.light.x);
+            g = clamp01(p.light.y);
+            b = clamp01(p.light.z);
+            a = clamp01(p.light.w);
+        }
+        if (accumulate) ka.accum[index] = pix;      // :164
+        ka.output[index] = pack_rgba8(r, g, b, a);  // :178
+    };
     auto finish_sample = [&]() {
         sample += 1;
         if (accumulate) {
@@ -934,6 +955,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             pix.w = pix.w + p.light.w;
         }
         if (sample == samples && frame + 1u < ka.frames) {
+            // a multi-frame launch: every frame writes its result, exactly as
+            // the sequence of single-frame dispatches it stands for would
+            store_frame();
             frame += 1;
             sample = 0;
         }
@@ -941,23 +965,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, index % ka.width, index / ka.width), p);
             mode = kSetup;
         } else {
-            float r, g, b, a;
-            if (accumulate) {
-                const float div = (float)((ka.accumulation_index + frame) * ka.compute_per_frame);
-                r = clamp01(pix.x / div);
-                g = clamp01(pix.y / div);
-                b = clamp01(pix.z / div);
-                a = clamp01(pix.w / div);
-            } else {
-                r = clamp01(p.light.x);
-                g = clamp01(p.light.y);
-                b = clamp01(p.light.z);
-                a = clamp01(p.light.w);
-            }
-            // stored where the pixel finishes (holding them back to the next
-            // traversal phase measured no faster and costs 6 VGPRs)
-            if (accumulate) ka.accum[index] = pix;  // :164
-            ka.output[index] = pack_rgba8(r, g, b, a);  // :178
+            store_frame();
             mode = kIdle;
         }
     };
@@ -1279,6 +1287,38 @@ extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(const f
     accum[idx] = v;
     output[idx] = pack_rgba8(clamp01(v.x / divisor), clamp01(v.y / divisor), clamp01(v.z / divisor),
                              clamp01(v.w / divisor));
+}
+
+// The packed RGBA8 output, one u32 per pixel, both ways (non-accumulating renders).
+extern "C" __global__ void __launch_bounds__(256) rt_pack_output_kernel(const uint32_t* __restrict__ output,
+                                                                       uint32_t* __restrict__ dst, uint32_t width,
+                                                                       uint32_t height, uint32_t tiles_x,
+                                                                       uint32_t owned_tiles, uint32_t rank,
+                                                                       uint32_t world, uint32_t unpack) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t local_tile = gid >> 6;
+    if (local_tile >= owned_tiles) return;
+    const uint32_t lane = (uint32_t)(gid & 63u);
+    const uint32_t tile = (uint32_t)local_tile * world + rank;
+    const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u);
+    const uint32_t y = (tile / tiles_x) * 8u + (lane >> 3);
+    const bool inside = x < width && y < height;
+    const size_t idx = (size_t)y * width + x;
+    uint32_t* out = const_cast<uint32_t*>(output);
+    if (unpack) {
+        if (inside) out[idx] = dst[gid];
+    } else {
+        dst[gid] = inside ? output[idx] : 0u;
+    }
+}
+
+hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t width, uint32_t height, uint32_t tiles_x,
+                                 uint32_t owned_tiles, uint32_t rank, uint32_t world, bool unpack, hipStream_t stream) {
+    const uint64_t threads = (uint64_t)owned_tiles * 64u;
+    const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
+    hipLaunchKernelGGL(rt_pack_output_kernel, dim3(blocks), dim3(256), 0, stream, output, packed, width, height,
+                       tiles_x, owned_tiles, rank, world, unpack ? 1u : 0u);
+    return hipGetLastError();
 }
 
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,

@@ -36,6 +36,8 @@ hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const 
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
+hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t width, uint32_t height, uint32_t tiles_x,
+                                 uint32_t owned_tiles, uint32_t rank, uint32_t world, bool unpack, hipStream_t stream);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
@@ -91,6 +93,8 @@ constexpr uint32_t kDefaultDrainMinSteps = 64;
 // sorted on the device from the previous frame's per-tile ray counts).
 constexpr uint32_t kDefaultTileSchedule = 1;
 constexpr uint64_t kSchedMinTilesPerWave = 4;
+// Frame batching (rt_set_frame_batch): at most this many frames per launch.
+constexpr uint32_t kMaxFrameBatch = 64;
 
 }  // namespace
 
@@ -117,6 +121,10 @@ struct rt_ctx {
     rt_params params{};  // shadow of binding 0
     uint32_t k = 1;      // Renderer::accumulation_index (src/renderer.rs:37)
     rt_ray_camera camera{};
+    // frame batching (rt_set_frame_batch): queued rt_compute_frame calls
+    uint32_t frame_batch = 1;     // frames per launch at most (1: one launch per frame)
+    uint32_t pending_frames = 0;  // queued, not yet launched (their k already advanced)
+    uint32_t pending_bounces = 0;
 
     uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
     // extents the kernel clamps against (>= 1 so clamps never underflow)
@@ -180,6 +188,7 @@ struct rt_ctx {
     // triangle/sub-object -> object maps, per-object triangle ranges, placements
     float* d_model = nullptr;
     uint32_t model_tris = 0;
+    bool models_valid = false;  // rt_set_object_models since the last object / sub-object range change
     uint32_t* d_tri_object = nullptr;
     uint32_t* d_sub_object = nullptr;
     uint2* d_object_tris = nullptr;
@@ -219,6 +228,8 @@ struct rt_ctx {
 
     std::string err;
 };
+
+static int flush_frames(rt_ctx* ctx);
 
 namespace {
 
@@ -583,6 +594,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TILE_SCHEDULE");
         if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
+        env = std::getenv("RT_FRAME_BATCH");
+        if (env) ctx->frame_batch = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxFrameBatch, (uint32_t)std::strtoul(env, nullptr, 10)));
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
@@ -632,6 +645,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
 void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    (void)flush_frames(ctx);  // queued frames were submitted: they run before teardown
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_queue, ctx->d_slot_sph,
                     ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
@@ -655,12 +669,33 @@ void rt_destroy(rt_ctx* ctx) {
     delete ctx;
 }
 
-#define RT_ENTER(ctx)                                               \
+static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
+
+// Frame batching (rt_set_frame_batch): rt_compute_frame queues frames and one
+// launch renders the whole batch (each pixel's frames back to back on one lane,
+// every frame's accumulation and output written). The batch is launched when it
+// is full and before anything else touches the context, so every other entry
+// point sees exactly the state the sequence of single-frame dispatches leaves.
+static int flush_frames(rt_ctx* ctx) {
+    if (ctx->pending_frames == 0) return RT_OK;
+    const uint32_t n = ctx->pending_frames;
+    ctx->pending_frames = 0;
+    return dispatch_frames(ctx, ctx->pending_bounces, n);
+}
+
+#define RT_ENTER_NOFLUSH(ctx)                                       \
     do {                                                            \
         if (!(ctx)) return RT_E_INVALID;                            \
         (ctx)->err.clear();                                         \
         hipError_t e0_ = hipSetDevice((ctx)->device);               \
         if (e0_ != hipSuccess) return hip_fail(ctx, "hipSetDevice", e0_); \
+    } while (0)
+
+#define RT_ENTER(ctx)                                \
+    do {                                             \
+        RT_ENTER_NOFLUSH(ctx);                       \
+        const int rcf_ = flush_frames(ctx);          \
+        if (rcf_ != RT_OK) return rcf_;              \
     } while (0)
 
 int rt_upload_textures(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height, uint32_t layers) {
@@ -781,7 +816,17 @@ int rt_update_object_info(rt_ctx* ctx, const rt_object_info* objects, uint32_t c
         ctx->h_obj.swap(saved);
         return rc;
     }
-    ctx->tri_dirty = true;
+    // the accelerator culls with the object boxes and walks the sub-object
+    // ranges; the device edit path's maps follow the ranges. A change of the
+    // other fields (material_index) invalidates neither.
+    bool boxes = false, ranges = false;
+    for (uint32_t i = 0; i < count; i++) {
+        const rt_object_info &a = saved[i], &b = objects[i];
+        boxes |= std::memcmp(a.min_bounds, b.min_bounds, 12) != 0 || std::memcmp(a.max_bounds, b.max_bounds, 12) != 0;
+        ranges |= a.first_sub_object_index != b.first_sub_object_index || a.sub_object_count != b.sub_object_count;
+    }
+    if (boxes || ranges) ctx->tri_dirty = true;
+    if (ranges) ctx->models_valid = false;
     return upload_raw(ctx, ctx->d_obj, objects, (size_t)count * 48);
 }
 
@@ -798,6 +843,10 @@ int rt_update_sub_object_info(rt_ctx* ctx, const rt_sub_object_info* sub_objects
         ctx->h_sub.swap(saved);
         return rc;
     }
+    for (uint32_t i = 0; i < count; i++)
+        if (saved[i].first_triangle_index != sub_objects[i].first_triangle_index ||
+            saved[i].triangle_count != sub_objects[i].triangle_count)
+            ctx->models_valid = false;  // the device edit path's triangle maps are stale
     ctx->tri_dirty = true;
     return upload_raw(ctx, ctx->d_sub, sub_objects, (size_t)count * 32);
 }
@@ -1014,7 +1063,41 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     return RT_OK;
 }
 
-int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) { return rt_compute_frames(ctx, bounces, 1); }
+int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) {
+    if (!ctx || ctx->frame_batch <= 1) return rt_compute_frames(ctx, bounces, 1);
+    RT_ENTER_NOFLUSH(ctx);
+    if (ctx->pending_frames && bounces != ctx->pending_bounces) {
+        const int rc = flush_frames(ctx);
+        if (rc) return rc;
+    }
+    if (ctx->pending_frames == 0) {
+        ctx->pending_bounces = bounces;
+        if (ctx->params.accumulate) ctx->params.accumulation_index = ctx->k;  // src/renderer.rs:216-235
+    }
+    if (ctx->params.accumulate) ctx->k += 1;
+    ctx->pending_frames += 1;
+    return ctx->pending_frames >= ctx->frame_batch ? flush_frames(ctx) : RT_OK;
+}
+
+int rt_set_frame_batch(rt_ctx* ctx, uint32_t max_frames) {
+    RT_ENTER(ctx);
+    if (max_frames == 0 || max_frames > kMaxFrameBatch)
+        return fail(ctx, RT_E_INVALID, "frame batch must be in [1, " + std::to_string(kMaxFrameBatch) + "]");
+    ctx->frame_batch = max_frames;
+    return RT_OK;
+}
+
+int rt_frame_batch(const rt_ctx* ctx, uint32_t* max_frames, uint32_t* pending) {
+    if (!ctx || !max_frames || !pending) return RT_E_INVALID;
+    *max_frames = ctx->frame_batch;
+    *pending = ctx->pending_frames;
+    return RT_OK;
+}
+
+int rt_flush(rt_ctx* ctx) {
+    RT_ENTER(ctx);
+    return RT_OK;
+}
 
 int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     RT_ENTER(ctx);
@@ -1100,6 +1183,7 @@ int rt_set_object_models(rt_ctx* ctx, const float* points, uint32_t triangle_cou
         (rc = upload_raw(ctx, ctx->d_object_tris, obj_tris.data(), (size_t)n_obj * 8)))
         return rc;
     ctx->model_tris = triangle_count;
+    ctx->models_valid = true;
     return RT_OK;
 }
 
@@ -1108,7 +1192,9 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
     if (count && !transforms) return fail(ctx, RT_E_INVALID, "transforms is NULL");
     if (count > ctx->h_obj.size()) return fail(ctx, RT_E_CAPACITY, "more transforms than objects");
     if (count == 0) return RT_OK;
-    if (!ctx->d_model) return fail(ctx, RT_E_INVALID, "rt_set_object_models has not been called");
+    if (!ctx->d_model || !ctx->models_valid)
+        return fail(ctx, RT_E_INVALID,
+                    "object models missing or stale (object / sub-object ranges changed): call rt_set_object_models");
     void* p;
     int rc = staging(ctx, (size_t)count * sizeof(rt_scene::Placement), &p);
     if (rc) return rc;
@@ -1294,6 +1380,28 @@ int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_ran
                                     ctx->height, ctx->tiles_x, owned, src_rank, world_size, (float)divisor,
                                     ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_unpack_tiles_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_pack_owned_output(rt_ctx* ctx, void* dst_device) {
+    RT_ENTER(ctx);
+    if (!dst_device) return fail(ctx, RT_E_INVALID, "dst is NULL");
+    if (ctx->owned_tiles == 0) return RT_OK;
+    hipError_t e = rt_launch_pack_output(ctx->d_out, static_cast<uint32_t*>(dst_device), ctx->width, ctx->height,
+                                         ctx->tiles_x, ctx->owned_tiles, ctx->rank, ctx->world, false, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_pack_output_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_unpack_output(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size) {
+    RT_ENTER(ctx);
+    if (!src_device || world_size == 0 || src_rank >= world_size) return fail(ctx, RT_E_INVALID, "unpack: bad arguments");
+    const uint32_t owned = owned_tile_count(ctx->tiles_x * ctx->tiles_y, src_rank, world_size);
+    if (owned == 0) return RT_OK;
+    hipError_t e = rt_launch_pack_output(ctx->d_out, const_cast<uint32_t*>(static_cast<const uint32_t*>(src_device)),
+                                         ctx->width, ctx->height, ctx->tiles_x, owned, src_rank, world_size, true,
+                                         ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_pack_output_kernel launch", e);
     return RT_OK;
 }
 

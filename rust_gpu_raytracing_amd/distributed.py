@@ -60,7 +60,8 @@ def unpack_host(accum: np.ndarray, packed: np.ndarray, src_rank: int, world_size
 
 
 def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0):
-    """Gather every rank's packed tile buffer (torch tensor, (owned*64, 4) f32) to `dst`.
+    """Gather every rank's packed tile buffer (torch tensor, owned*64 rows: (n, 4) f32
+    accumulation or (n,) int32 RGBA8 words) to `dst`.
 
     Buffers are padded to the largest rank's size so one collective moves them
     all. Returns the list of per-rank tensors (trimmed) on `dst`, None elsewhere.
@@ -70,7 +71,7 @@ def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0
 
     cap = max_owned_tiles(n_tiles, world_size) * 64
     if packed.shape[0] < cap:
-        pad = torch.zeros((cap - packed.shape[0], 4), dtype=packed.dtype, device=packed.device)
+        pad = torch.zeros((cap - packed.shape[0], *packed.shape[1:]), dtype=packed.dtype, device=packed.device)
         packed = torch.cat([packed, pad])
     device = packed.device
     if dist.get_backend() == "gloo" and packed.is_cuda:  # gloo moves host tensors only
@@ -83,24 +84,35 @@ def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0
 
 
 def gather_accumulation(renderer, dst: int = 0):
-    """Assemble the whole accumulation (and RGBA8 output) of a tile-split render
-    on rank `dst`'s Renderer: device pack -> RCCL gather -> device unpack."""
+    """Assemble the whole frame of a tile-split render on rank `dst`'s Renderer:
+    device pack -> RCCL gather -> device unpack. Accumulating renders move the
+    RGBA32F accumulation (16 B/px) and rebuild the RGBA8 output from it with the
+    last frame's divisor k*c (compute_shader.wgsl:166); non-accumulating ones
+    (which never write the accumulation, :171-178) move the RGBA8 words as is."""
     import torch
 
     rank, world = renderer.rank, renderer.world_size
     tx_n, ty_n = tile_grid(renderer.width, renderer.height)
     n_tiles = tx_n * ty_n
     cap = max_owned_tiles(n_tiles, world) * 64
-    packed = torch.zeros((cap, 4), dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device()))
-    renderer.pack_owned_accumulation(packed.data_ptr())
+    device = torch.device("cuda", renderer.device)  # the renderer's GPU, whatever torch's current device is
+    if renderer.accumulate:
+        packed = torch.zeros((cap, 4), dtype=torch.float32, device=device)
+        renderer.pack_owned_accumulation(packed.data_ptr())
+    else:
+        packed = torch.zeros((cap,), dtype=torch.int32, device=device)
+        renderer.pack_owned_output(packed.data_ptr())
     renderer.synchronize()
     parts = gather_packed(packed, n_tiles, rank, world, dst)
     if parts is None:
         return
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(device)
     k = renderer.accumulation_index - 1  # the last frame's accumulation_index
     divisor = max(k, 1) * renderer.compute_per_frame
     for src, part in enumerate(parts):
         if src != rank and part.shape[0]:
-            renderer.unpack_accumulation(part.data_ptr(), src, world, divisor)
+            if renderer.accumulate:
+                renderer.unpack_accumulation(part.data_ptr(), src, world, divisor)
+            else:
+                renderer.unpack_output(part.data_ptr(), src, world)
     renderer.synchronize()

@@ -43,13 +43,17 @@ class Renderer:
         world_size: int = 1,
         camera_rays: np.ndarray | None = None,
         device_rays: bool | None = None,
+        frame_batch: int = 1,
         lib=None,
     ):
         """``camera_rays``: explicit per-pixel directions (the reference's ray buffer;
         default: ``scene.camera.recalculate_ray_directions()``). ``device_rays=True``
         computes them on the device from the camera's matrices instead
         (rt_update_camera_matrices; bit-identical, no ray buffer read, but measured
-        2% slower on C2 than reading the buffer, so off by default)."""
+        2% slower on C2 than reading the buffer, so off by default).
+        ``frame_batch``: frames one launch may render (rt_set_frame_batch): with
+        F > 1, ``compute_frame`` queues frames and launches F at a time (or at the
+        next readback / update / sync), each frame's results written as before."""
         self._lib = N.load_library() if lib is None else lib
         self.scene = scene
         self.accumulate = accumulate
@@ -57,6 +61,7 @@ class Renderer:
         self.width = scene.camera.viewport_width
         self.height = scene.camera.viewport_height
         self.rank, self.world_size = rank, world_size
+        self.device = device
         self._ctx = None
         rays = scene.camera.recalculate_ray_directions() if camera_rays is None else camera_rays
         self.camera_rays = np.ascontiguousarray(rays, dtype=B.RAY)
@@ -81,6 +86,8 @@ class Renderer:
         self.device_rays = bool(device_rays)
         if self.device_rays:
             self._set_camera_matrices(scene.camera)
+        if frame_batch != 1:
+            self.set_frame_batch(frame_batch)
 
     # ------------------------------------------------------------------ helpers
     def _params(self, accumulation_index: int) -> np.ndarray:
@@ -127,8 +134,12 @@ class Renderer:
         self._call("rt_update_spheres", N.ptr(s.spheres), s.spheres.shape[0])
         self._upload_textures()
         if device:
+            # the device rebuild rewrites bounds only; every other ObjectInfo field
+            # (material_index, src/renderer.rs:188-193) comes from the host records
+            self._upload_object_fields()
             self.update_objects()
         else:
+            self._models = None  # the host path may change the objects: re-upload models for device edits
             for o in s.objects:
                 builder.update_object(o, lib=self._lib)
             objs, subs, tris = s.flatten()
@@ -138,10 +149,27 @@ class Renderer:
             self._call("rt_update_sub_object_info", N.ptr(subs), subs.shape[0])
         self._call("rt_update_materials", N.ptr(s.materials), s.materials.shape[0])
 
+    def _upload_object_fields(self) -> None:
+        """The host ObjectInfo records with the device's current bounds (a device
+        edit leaves the host bounds stale): material index and sub-object range
+        reach the device without invalidating the triangle accelerator."""
+        objs = np.stack([np.asarray(o.object_info) for o in self.scene.objects]).astype(B.OBJECT_INFO) \
+            if self.scene.objects else np.zeros(0, B.OBJECT_INFO)
+        if objs.shape[0] == 0:
+            return
+        dev = np.zeros(objs.shape[0], B.OBJECT_INFO)
+        self._call("rt_read_object_info", N.ptr(dev), dev.shape[0])
+        merged = objs.copy()
+        merged["min_bounds"] = dev["min_bounds"]
+        merged["max_bounds"] = dev["max_bounds"]
+        merged = np.ascontiguousarray(merged)
+        self._call("rt_update_object_info", N.ptr(merged), merged.shape[0])
+
     def upload_object_models(self) -> None:
         """The objects' normalised points (rt_set_object_models), once, for device-side edits."""
         pts = [np.asarray(o.normalized_points, np.float32).reshape(-1, 9) for o in self.scene.objects]
         self._models = np.ascontiguousarray(np.concatenate(pts) if pts else np.zeros((0, 9), np.float32))
+        self._models_key = tuple(id(o) for o in self.scene.objects)
         self._call("rt_set_object_models", N.ptr(self._models), self._models.shape[0])
 
     def update_objects(self) -> None:
@@ -150,7 +178,8 @@ class Renderer:
         the triangle accelerator refitted, stream-ordered before the next frame."""
         from . import builder
 
-        if getattr(self, "_models", None) is None:
+        if getattr(self, "_models", None) is None or \
+                getattr(self, "_models_key", None) != tuple(id(o) for o in self.scene.objects):
             self.upload_object_models()
         t = np.ascontiguousarray(np.stack([builder.transform_of(o) for o in self.scene.objects])) \
             if self.scene.objects else np.zeros(0, B.OBJECT_TRANSFORM)
@@ -194,6 +223,20 @@ class Renderer:
         """``frames`` compute_frame calls fused into one launch (same results;
         rt_compute_frames in include/rt_abi.h). Asynchronous."""
         self._call("rt_compute_frames", bounces, frames)
+
+    def set_frame_batch(self, max_frames: int) -> None:
+        """rt_set_frame_batch: up to ``max_frames`` queued compute_frame calls per launch."""
+        self._call("rt_set_frame_batch", max_frames)
+
+    def frame_batch(self):
+        """(max frames per launch, frames queued now)."""
+        m, p = ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(self._ctx, self._lib.rt_frame_batch(self._ctx, ctypes.byref(m), ctypes.byref(p)), self._lib)
+        return m.value, p.value
+
+    def flush(self) -> None:
+        """Launch the queued frames now (rt_flush); every other call does so implicitly."""
+        self._call("rt_flush")
 
     # ------------------------------------------------------------------ readback & stats
     def synchronize(self) -> None:
@@ -263,6 +306,12 @@ class Renderer:
 
     def unpack_accumulation(self, src_device_ptr: int, src_rank: int, world_size: int, divisor: int) -> None:
         self._call("rt_unpack_accumulation", ctypes.c_void_p(src_device_ptr), src_rank, world_size, divisor)
+
+    def pack_owned_output(self, dst_device_ptr: int) -> None:
+        self._call("rt_pack_owned_output", ctypes.c_void_p(dst_device_ptr))
+
+    def unpack_output(self, src_device_ptr: int, src_rank: int, world_size: int) -> None:
+        self._call("rt_unpack_output", ctypes.c_void_p(src_device_ptr), src_rank, world_size)
 
     def debug_counters(self, n: int = 8) -> list:
         """Diagnostic builds only: the 8 counters, then per-wave stamps (include/rt_abi.h)."""

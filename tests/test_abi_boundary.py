@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.rt_abi_version() == 4
+    assert native_lib.rt_abi_version() == 5
 
 
 def test_ctypes_layouts_match_header():

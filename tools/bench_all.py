@@ -40,13 +40,14 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kw", default="{}", help="JSON builder kwargs applied to every config, e.g. '{\"env_size\": [1024, 512]}'")
     ap.add_argument("--size", default=None, help="WxH override")
+    ap.add_argument("--frame-batch", type=int, default=1, help="rt_set_frame_batch (frames per launch at most)")
     args = ap.parse_args()
     for name in args.configs:
         w, h = SIZES[name] if args.size is None else map(int, args.size.split("x"))
         t0 = time.perf_counter()
         scene, bounces = build_config(name, width=w, height=h, **json.loads(args.kw))
         t_build = time.perf_counter() - t0
-        with Renderer(scene) as r:
+        with Renderer(scene, frame_batch=args.frame_batch) as r:
             for _ in range(args.warmup):
                 r.compute_frame(bounces)
             r.synchronize()
@@ -62,15 +63,16 @@ def main():
             ms, n = r.dispatch_time_total()
             rays = r.ray_count()
             launch = r.launch_config()
-        kern_s = ms / n / 1e3
+        kern_s = ms / args.frames / 1e3  # kernel time per frame (a launch may render several)
         rpf = rays / args.frames
-        b = bench.algorithmic_bytes(w * h, rpf, bench.scene_bytes(scene))
+        fpl = args.frames / n  # frames per launch
+        b = bench.algorithmic_bytes(w * h, rpf * fpl, bench.scene_bytes(scene), fpl) / fpl  # per frame
         res = {
             "config": name, "width": w, "height": h, "bounces": bounces,
             "spheres": int(scene.spheres.shape[0]), "triangles": int(scene.flatten()[2].shape[0]),
             "gpu_mray_s": rpf / kern_s / 1e6, "gpu_mray_s_wall": rays / wall / 1e6,
-            "kernel_ms": kern_s * 1e3, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
-            "hbm_bytes_per_launch": b, "hbm_frac": b / kern_s / 8e12, "launch": launch,
+            "kernel_ms": kern_s * 1e3, "launches": n, "frame_batch": args.frame_batch, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
+            "hbm_bytes_per_frame": b, "hbm_frac": b / kern_s / 8e12, "launch": launch,
             "scene_build_s": round(t_build, 2),
         }
         if not args.no_cpu:
