@@ -1,26 +1,30 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mray/s of the path-tracing kernel, 1920x1080, 8 bounces.
 
-Workload (BASELINE.json configs[1]): the RTIOW cover scene (488 spheres),
+Workload (BASELINE.json configs[1]): the RTIOW cover scene (484 spheres),
 1920x1080, 8 bounces, 1 sample per pixel per frame, accumulation on. One
-"step" = one Renderer.compute_frame (one kernel launch over the frame). Inputs
-are resident in HBM before timing; the timed region holds exactly `--steps`
-frames bracketed by barrier + device synchronize.
+"step" = one Renderer.compute_frame (one frame: every pixel traced, its
+accumulation and RGBA8 output written). Frames are launched in batches of
+--frame-batch (rt_set_frame_batch; default 8 at N=1: the persistent grid's fill
+and drain are paid once per 8 frames; every frame is traced in full and added to
+the accumulation in the reference's order). Inputs are resident in HBM before timing; the timed region
+holds exactly `--steps` frames bracketed by barrier + device synchronize.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-the 1920x1080 image is tile-split across ranks (8x8 tile t -> rank t % N,
-SURVEY §8e). Default "--scaling weak": the same view rendered at N times the
-pixels -- (1920*sqrt(N)) x (1080*sqrt(N)) rounded to whole 8x8 tiles (N=4 is
-3840x2160) -- so every GPU owns one 1920x1080 frame's worth of tiles at every N
-and each step is still one single-frame launch per GPU (one frame of the job's
-image). "--scaling strong": the 1920x1080 frame split N ways (0.1 ms of work
-per GPU at N=8). No collective runs in the timed loop; one RCCL gather of the
-accumulated RGBA32F tiles to rank 0 runs afterwards and is reported separately
-as gather_ms.
+default "--scaling strong", the metric's config: the 1920x1080 frame is
+tile-split across ranks (8x8 tile t -> rank t % N), frame batch 8N
+(each GPU's launch holds the work of an N=1 launch), and the timed region also
+assembles the image on rank 0 once (device pack -> RCCL gather of the RGBA32F
+accumulation -> unpack), so `value` includes the gather (also reported as
+gather_ms). A secondary "weak" object measures the same view at N x the pixels
+((1920*sqrt(N)) x (1080*sqrt(N)) in whole tiles, one 1920x1080 frame's worth
+of tiles per GPU). `value` = all ranks' rays / the slowest rank's time.
 
-roofline.traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
-(profiles/pmc_traffic.json, FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE), when
-it was measured on this workload; null otherwise.
+roofline: algorithmic bytes per launch (bench.algorithmic_bytes) /
+the average launch time from HIP events on the renderer's stream. traffic and
+valu: the committed rocprofv3 PMC entry (profiles/pmc_traffic.json, FETCH_SIZE x2
+per the gfx950 note + WRITE_SIZE; SQ counters) of this workload, frame batch and
+kernel build hash; null (with the reason, and a warning) when stale.
 
 Prints ONE JSON line on rank 0.
 """
@@ -47,12 +51,12 @@ def log(*a):
 
 
 def algorithmic_bytes(owned_pixels: int, rays: float, scene_bytes: int, frames: float = 1.0) -> float:
-    """SURVEY §8d, per launch: B = 52 B/px/frame (ray dir 16 + accum 16 read + 16 write +
-    RGBA8 4) + 4 B per counted ray (one RGBA8 texel: texture on hit, env map on miss)
-    + the scene arrays read once. A launch rendering F batched frames reads each
-    pixel's accumulation once and keeps it in a register between its frames:
-    16 + 36 F B/px (F = 1: the 52 B above)."""
-    return (16.0 + 36.0 * frames) * owned_pixels + 4.0 * rays + scene_bytes
+    """SURVEY §8d's per-frame figure x the frames one launch renders: B = 52 B/px/frame
+    (ray dir 16 + accum 16 read + 16 write + RGBA8 4) + 4 B per counted ray (one RGBA8
+    texel: texture on hit, env map on miss) + the scene arrays read once. (A batched
+    launch moves less -- each pixel's accumulation once per batch, plus its lights:
+    roofline.traffic is what the counters see.)"""
+    return 52.0 * frames * owned_pixels + 4.0 * rays + scene_bytes
 
 
 def scene_bytes(scene) -> int:
@@ -60,25 +64,30 @@ def scene_bytes(scene) -> int:
     return int(scene.spheres.nbytes + scene.materials.nbytes + objs.nbytes + subs.nbytes + tris.shape[0] * 64)
 
 
-def pmc_traffic(workload: str):
-    """HBM bytes per launch measured by rocprofv3 PMC for this workload (tools/profile.sh ->
-    profiles/pmc_traffic.json), or None when no committed measurement matches."""
+def pmc_entry(key: str, build_hash: str):
+    """The committed rocprofv3 PMC measurement (tools/profile.sh -> tools/update_traffic.py ->
+    profiles/pmc_traffic.json) of this workload AND this kernel build: (entry, None), or
+    (None, reason) when there is none or it was measured on another build (stale)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None, None
-    d = json.loads(f.read_text())
-    e = d.get(workload)
+    e = json.loads(f.read_text()).get(key) if f.exists() else None
     if not e:
-        return None, None
-    return float(e["fetch_bytes_x2"] + e["write_bytes"]), e.get("source")
+        return None, f"no PMC entry for '{key}'"
+    if e.get("build_hash") != build_hash:
+        msg = f"PMC entry for '{key}' was measured on build {e.get('build_hash')}, this is {build_hash}: stale, not used"
+        log("WARNING: " + msg)
+        return None, msg
+    return e, None
 
 
-def pmc_issue(workload: str):
-    """VALU issue and lane utilisation of the same committed PMC run (SQ counters): the
-    resource this branchy f32 path is actually bound by, or None."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    e = json.loads(f.read_text()).get(workload) if f.exists() else None
-    if not e or e.get("valu_issue_util") is None:
+def pmc_traffic(e):
+    """HBM bytes per launch: FETCH_SIZE x2 (gfx950 note) + WRITE_SIZE."""
+    return None if e is None else float(e["fetch_bytes_x2"] + e["write_bytes"])
+
+
+def pmc_issue(e):
+    """VALU issue and lane utilisation of the same PMC run (SQ counters): the resource
+    this branchy f32 path is actually bound by."""
+    if e is None or e.get("valu_issue_util") is None:
         return None
     return {"valu_issue_util": e["valu_issue_util"], "valu_lane_util": e["valu_lane_util"], "source": e.get("source")}
 
@@ -115,6 +124,14 @@ def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
     }
 
 
+def default_frame_batch(world: int) -> int:
+    """Frames per launch: 8 at N=1 (the persistent grid's fill and drain paid once per
+    8 frames, DESIGN.md §5.1: C2 0.454 -> 0.365 ms/frame, C3 0.830 -> 0.383), 8N at N
+    GPUs so that each GPU's launch holds the same work as at N=1 when the frame is
+    split N ways (capped at 64)."""
+    return min(64, 8 * world)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,12 +144,14 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-sample-world", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "1")),
-                    help="frames one launch may render (rt_set_frame_batch); 1 = one launch per frame")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="N>1: weak = N frames per step (1/N of the tiles each, per-GPU work fixed); "
-                         "strong = one frame per step split N ways")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: leave the RCCL gather of the image to rank 0 out of the timed region")
+    ap.add_argument("--no-weak", action="store_true", help="N>1: skip the secondary weak-scaling measurement")
+    ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
+                    help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="N>1: strong = the 1920x1080 frame split N ways (the metric's config, `value`); "
+                         "weak = N x the pixels (per-GPU work fixed)")
     args = ap.parse_args()
 
     import torch
@@ -166,93 +185,113 @@ def main() -> int:
     if world > 1:
         dist.barrier()
 
-    width, height = args.width, args.height
-    if world > 1 and args.scaling == "weak":
-        scale = world ** 0.5  # same view, N x the pixels: per-GPU work fixed
-        width = int(round(args.width * scale / 8.0)) * 8
-        height = int(round(args.height * scale / 8.0)) * 8
-    scene, default_bounces = build_config(args.config, width=width, height=height)
-    bounces = args.bounces or default_bounces
-    r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=args.frame_batch)
-    owned_px = r.owned_pixel_count()
+    def size_for(scaling):
+        if world > 1 and scaling == "weak":
+            scale = world ** 0.5  # same view, N x the pixels: per-GPU work fixed
+            return int(round(args.width * scale / 8.0)) * 8, int(round(args.height * scale / 8.0)) * 8
+        return args.width, args.height
 
-    def step():
-        r.compute_frame(bounces)
+    def run(scaling, frame_batch):
+        """Warmup, then exactly args.steps frames between barrier + sync; with N > 1 the
+        timed region also assembles the image on rank 0 (pack -> RCCL gather -> unpack),
+        once per run (a readback after the last frame, amortised over the steps)."""
+        width, height = size_for(scaling)
+        scene, default_bounces = build_config(args.config, width=width, height=height)
+        bounces = args.bounces or default_bounces
+        r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=frame_batch)
 
-    def barrier_sync():
-        r.synchronize()
-        torch.cuda.synchronize()
+        def barrier_sync():
+            r.synchronize()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+
+        for _ in range(args.warmup):
+            r.compute_frame(bounces)
+        barrier_sync()
+        r.reset_ray_count()
+        r.reset_timing()
+        r.set_timing(True)
+        barrier_sync()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            r.compute_frame(bounces)
+            if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
+                log(f"step {i + 1}/{args.steps}")
+        barrier_sync()
+        t_render = time.perf_counter() - t0
+        r.set_timing(False)  # (reads the launch events back: outside the gather's time)
+        t1 = time.perf_counter()
+        gathered = world > 1 and not args.no_gather
+        if gathered:
+            from rust_gpu_raytracing_amd.distributed import gather_accumulation
+
+            gather_accumulation(r, dst=0)
+            barrier_sync()
+        t_gather = time.perf_counter() - t1
+        res = dict(r=r, scene=scene, bounces=bounces, width=width, height=height, rays=r.ray_count(),
+                   t_render=t_render, t_gather=t_gather, gathered=gathered, launch=r.launch_config(),
+                   timing=r.dispatch_time_total(), owned_px=r.owned_pixel_count())
+        stats = torch.tensor([t_render + t_gather, t_render, t_gather, float(res["rays"])], dtype=torch.float64,
+                             device="cuda" if backend == "nccl" else "cpu")
         if world > 1:
-            dist.barrier()
+            mx = stats[0:3].clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            tot = stats[3:4].clone()
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            stats = torch.cat([mx, tot])
+        res["t_total_max"], res["t_render_max"], res["t_gather_max"], res["rays_total"] = map(float, stats.tolist())
+        return res
 
-    for _ in range(args.warmup):
-        step()
-    barrier_sync()
-    r.reset_ray_count()
-    r.reset_timing()
-    r.set_timing(True)
-    barrier_sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step()
-        if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
-            log(f"step {i + 1}/{args.steps}")
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    r.set_timing(False)
-    launch = r.launch_config()
-    rays = r.ray_count()
-    kern_ms, n_timed = r.dispatch_time_total()
-
-    stats = torch.tensor([elapsed, float(rays)], dtype=torch.float64,
-                         device="cuda" if backend == "nccl" else "cpu")
-    if world > 1:
-        t_max = stats[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        tot = stats[1:2].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed_max, rays_total = float(t_max.item()), float(tot.item())
-    else:
-        elapsed_max, rays_total = elapsed, float(rays)
-
-    gather_ms = None
-    if world > 1 and not args.no_gather:
-        from rust_gpu_raytracing_amd.distributed import gather_accumulation
-
-        barrier_sync()
-        g0 = time.perf_counter()
-        gather_accumulation(r, dst=0)
-        barrier_sync()
-        gather_ms = (time.perf_counter() - g0) * 1e3
-        if os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
-            # the assembled tile-split image must equal a 1-GPU render of the same frames
-            with Renderer(scene, device=device) as ref:
-                for _ in range(args.warmup + args.steps):
-                    ref.compute_frame(bounces)
-                same = np.array_equal(ref.read_accumulation().view(np.uint32), r.read_accumulation().view(np.uint32))
-                same = same and np.array_equal(ref.read_output(), r.read_output())
-            log(f"gather verify: assembled image {'==' if same else '!='} 1-GPU render")
-            if not same:
-                return 3
+    fb = args.frame_batch or default_frame_batch(world)
+    main_run = run(args.scaling, fb)
+    r = main_run["r"]
+    if main_run["gathered"] and os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
+        # the assembled tile-split image must equal a 1-GPU render of the same frames
+        with Renderer(main_run["scene"], device=device) as ref:
+            for _ in range(args.warmup + args.steps):
+                ref.compute_frame(main_run["bounces"])
+            same = np.array_equal(ref.read_accumulation().view(np.uint32), r.read_accumulation().view(np.uint32))
+            same = same and np.array_equal(ref.read_output(), r.read_output())
+        log(f"gather verify: assembled image {'==' if same else '!='} 1-GPU render")
+        if not same:
+            return 3
+    r.close()
+    weak = None
+    if world > 1 and args.scaling == "strong" and not args.no_weak:
+        w_run = run("weak", args.frame_batch or default_frame_batch(1))
+        w_run["r"].close()
+        weak = {
+            "value": w_run["rays_total"] / w_run["t_total_max"] / 1e6,
+            "ms_per_step": w_run["t_total_max"] / args.steps * 1e3,
+            "render_ms_per_step": w_run["t_render_max"] / args.steps * 1e3,
+            "gather_ms": w_run["t_gather_max"] * 1e3,
+            "width": w_run["width"], "height": w_run["height"], "frame_batch": args.frame_batch or default_frame_batch(1),
+            "note": "secondary: the same view at N x the pixels, every GPU owning one 1920x1080 frame's worth of tiles",
+        }
 
     if rank == 0:
+        m = main_run
+        scene, bounces, width, height = m["scene"], m["bounces"], m["width"], m["height"]
+        kern_ms, n_timed = m["timing"]
         avg_kernel_s = kern_ms / max(n_timed, 1) / 1e3
         frames_per_launch = args.steps / max(n_timed, 1)
-        rays_per_launch = rays / max(n_timed, 1)
-        b_launch = algorithmic_bytes(owned_px, rays_per_launch, scene_bytes(scene), frames_per_launch)
+        rays_per_launch = m["rays"] / max(n_timed, 1)
+        b_launch = algorithmic_bytes(m["owned_px"], rays_per_launch, scene_bytes(scene), frames_per_launch)
         achieved = b_launch / avg_kernel_s / 1e9
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
-        traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
+        build_hash = native_build.source_hash()
+        pmc, pmc_why = pmc_entry(f"{workload} | frame_batch {fb}", build_hash) if world == 1 else (None, "N>1")
         result = {
             "metric": METRIC,
-            "value": rays_total / elapsed_max / 1e6,
+            "value": m["rays_total"] / m["t_total_max"] / 1e6,
             "unit": "Mray/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "ms_per_step": m["t_total_max"] / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if args.scaling == "weak" else "strong",
+            "scaling": args.scaling if world > 1 else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -264,10 +303,10 @@ def main() -> int:
                 "spheres": int(scene.spheres.shape[0]),
                 "triangles": int(scene.flatten()[2].shape[0]),
                 "parallelism": f"tile{world}" if world > 1 else "single",
-                "pixels_per_gpu": owned_px,
-                "rays_per_step": rays_total / args.steps,
+                "pixels_per_gpu": m["owned_px"],
+                "rays_per_step": m["rays_total"] / args.steps,
                 "nominal_rays_per_step": width * height * bounces,
-                "frame_batch": args.frame_batch,
+                "frame_batch": fb,
                 "launches": n_timed,
             },
             "roofline": {
@@ -276,23 +315,28 @@ def main() -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
+                "traffic": pmc_traffic(pmc),
+                "traffic_source": pmc["source"] if pmc else pmc_why,
                 "kernel": "rt_pathtrace_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
-                "launch": launch,
+                "frames_per_launch": frames_per_launch,
+                "launch": m["launch"],
                 "bytes_per_launch": b_launch,
                 "note": "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction",
-                "valu": pmc_issue(workload) if world == 1 else None,
+                "valu": pmc_issue(pmc),
+                "build_hash": build_hash,
             },
         }
-        if gather_ms is not None:
-            result["gather_ms"] = gather_ms
+        if world > 1:
+            result["render_ms_per_step"] = m["t_render_max"] / args.steps * 1e3
+            result["gather_ms"] = m["t_gather_max"] * 1e3
+            result["gather_in_value"] = m["gathered"]
+            if weak is not None:
+                result["weak"] = weak
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
             result["cpu_baseline"] = cpu_baseline(scene, bounces, args.cpu_seconds, args.cpu_sample_world)
         print(json.dumps(result), flush=True)
-    r.close()
     if world > 1:
         dist.destroy_process_group()
     return 0

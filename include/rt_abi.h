@@ -173,6 +173,9 @@ RT_API int rt_create(const rt_create_info* info, rt_ctx** out_ctx);
 RT_API void rt_destroy(rt_ctx* ctx);
 RT_API const char* rt_last_error(const rt_ctx* ctx); /* never NULL; "" when no error */
 RT_API int rt_abi_version(void);
+/* Identity of this build: the hash of the sources, headers and compiler flags it
+ * was compiled from (rust_gpu_raytracing_amd/build.py: source_hash). */
+RT_API const char* rt_build_hash(void);
 
 /* DataBuffers::update_texture_buffer (src/buffers.rs:479-511): `layers`
  * RGBA8 (sRGB-encoded, Rgba8UnormSrgb) images of width x height, tightly
@@ -233,11 +236,16 @@ RT_API int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
  * max_frames > 1, rt_compute_frame queues its frame (Params and k advance as
  * always) and one launch renders the queued frames once max_frames are queued,
  * when the bounce count changes, or before ANY other call on the context
- * (readback, update, sync, timing, destroy). Inside the launch each pixel runs
- * its frames back to back on one lane and every frame writes its accumulation
- * and packed output, so every observable result -- buffers, ray count, k -- is
- * that of the single-frame dispatches; what changes is that the persistent
- * grid's fill and drain are paid once per batch instead of once per frame.
+ * (readback, update, sync, timing, destroy). Every frame is traced in full.
+ * Accumulating batches are frame-parallel: each (frame, 8x8 tile) is a unit of
+ * the launch's work queue, each path's light goes to a per-(frame, sample)
+ * buffer, and a resolve pass adds them to the accumulation in the reference's
+ * order (frame k's samples, then frame k+1's: compute_shader.wgsl:156-164), so
+ * the accumulation, the packed output, the ray count and k after the batch are
+ * bit-identical to the single-frame dispatches'; what changes is that the
+ * persistent grid's fill and drain are paid once per batch, and that a tile
+ * split over N GPUs keeps N x the units per launch. Non-accumulating batches
+ * (every frame the same frame) run each pixel's frames back to back on a lane.
  * 1 (the default; env RT_FRAME_BATCH) launches each frame at once.
  * max_frames in [1, 64]. rt_frame_batch reports the setting and the frames
  * queued; rt_flush launches them now. */

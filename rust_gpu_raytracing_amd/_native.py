@@ -89,6 +89,7 @@ SIGNATURES = {
     "rt_destroy": (None, [_P]),
     "rt_last_error": (ctypes.c_char_p, [_P]),
     "rt_abi_version": (ctypes.c_int, []),
+    "rt_build_hash": (ctypes.c_char_p, []),
     "rt_upload_textures": (ctypes.c_int, [_P, _P, _U32, _U32, _U32]),
     "rt_upload_env_map": (ctypes.c_int, [_P, _P, _U32, _U32]),
     "rt_update_params": (ctypes.c_int, [_P, ctypes.POINTER(rt_params)]),

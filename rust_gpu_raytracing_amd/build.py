@@ -6,9 +6,13 @@ kernel still runs but is no longer bit-exact against the oracle.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
+import socket
 import subprocess
 import sys
+import time
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -36,7 +40,21 @@ NUMERIC_FLAGS = [
 PERF_FLAGS = ["-fno-slp-vectorize"]
 
 
-def hipcc_command(out: Path = OUT, extra: list[str] | None = None) -> list[str]:
+STAMP = PKG / "librt_pathtrace.build.json"  # what built OUT: source hash, hipcc command, host, time
+
+
+def source_hash() -> str:
+    """SHA-256 over the compiler, the flags and every source and header: the identity of
+    a build. The library embeds it (rt_build_hash) and build() rebuilds when it differs."""
+    h = hashlib.sha256()
+    h.update(" ".join([HIPCC, ARCH, *NUMERIC_FLAGS, *PERF_FLAGS]).encode())
+    for f in SOURCES + HEADERS + [Path(__file__)]:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def hipcc_command(out: Path = OUT, extra: list[str] | None = None, build_hash: str | None = None) -> list[str]:
     return [
         HIPCC,
         f"--offload-arch={ARCH}",
@@ -50,6 +68,7 @@ def hipcc_command(out: Path = OUT, extra: list[str] | None = None) -> list[str]:
         "-Wall",
         f"-I{INCLUDE}",
         f"-I{CSRC}",
+        f'-DRT_BUILD_HASH="{build_hash or source_hash()}"',
         *(extra or []),
         *map(str, SOURCES),
         "-o",
@@ -57,22 +76,39 @@ def hipcc_command(out: Path = OUT, extra: list[str] | None = None) -> list[str]:
     ]
 
 
+def build_info() -> dict:
+    """The stamp of the library on disk ({} if none) plus the current source hash."""
+    info = json.loads(STAMP.read_text()) if STAMP.exists() and OUT.exists() else {}
+    info["sources_hash"] = source_hash()
+    return info
+
+
 def up_to_date(out: Path = OUT) -> bool:
-    if not out.exists():
+    if not out.exists() or not STAMP.exists():
         return False
-    t = out.stat().st_mtime
-    return all(p.stat().st_mtime <= t for p in SOURCES + HEADERS + [Path(__file__)])
+    try:
+        return json.loads(STAMP.read_text()).get("hash") == source_hash()
+    except (ValueError, OSError):
+        return False
 
 
 def build(force: bool = False, verbose: bool = True) -> Path:
+    """Compile when the sources' hash differs from the one the library was built
+    from (content, not mtime: a copied tree with fresh timestamps does not rebuild,
+    an edited header does)."""
     if not force and up_to_date():
         return OUT
+    digest = source_hash()
     tmp = OUT.with_suffix(f".{os.getpid()}.tmp.so")
-    cmd = hipcc_command(tmp)
+    cmd = hipcc_command(tmp, build_hash=digest)
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
+    t0 = time.time()
     subprocess.run(cmd, check=True)
     os.replace(tmp, OUT)
+    STAMP.write_text(json.dumps({"hash": digest, "host": socket.gethostname(),
+                                 "built_at": time.strftime("%Y-%m-%dT%H:%M:%S"), "seconds": round(time.time() - t0, 1),
+                                 "command": " ".join(hipcc_command(OUT, build_hash=digest))}, indent=1))
     return OUT
 
 

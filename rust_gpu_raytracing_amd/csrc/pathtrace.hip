@@ -673,11 +673,13 @@ struct TileQueue {
     uint32_t tried;   // stripes found empty so far
 };
 
+// Returns the claimed queue position in [0, queue_units), or 0xffffffff when
+// the queue is empty (unit_tile maps a position to its tile and frame).
 __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka, TileQueue& q) {
     const uint32_t n_str = ka.queue_stripes;
     const bool leader = (threadIdx.x & 63u) == 0;
     while (q.tried < n_str) {
-        const uint32_t count = ka.owned_tiles > q.stripe ? (ka.owned_tiles - q.stripe + n_str - 1u) / n_str : 0u;
+        const uint32_t count = ka.queue_units > q.stripe ? (ka.queue_units - q.stripe + n_str - 1u) / n_str : 0u;
         uint32_t* ctr = ka.queue + q.stripe * kQueueStride;
         bool attempt = true;
         if (q.tried > 0) {  // stealing: skip stripes that are already drained
@@ -689,15 +691,22 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka, TileQueue& 
             uint32_t old = 0;
             if (leader) old = atomicAdd(ctr, 1u);
             old = __builtin_amdgcn_readlane(old, 0);
-            if (old < count) {  // queue position -> local tile (identity unless cost-ordered)
-                const uint32_t pos = old * n_str + q.stripe;
-                return ka.tile_order ? ka.tile_order[pos] : pos;
-            }
+            if (old < count) return old * n_str + q.stripe;
         }
         q.stripe = q.stripe + 1u == n_str ? 0u : q.stripe + 1u;
         q.tried += 1;
     }
     return 0xffffffffu;
+}
+
+// Queue position -> local tile (identity unless cost-ordered) and, in a
+// frame-parallel batch, the frame (positions are frame-major, so a launch ends
+// on the last frame's cheapest tiles). 0xffffffff (empty queue) stays so.
+__device__ __forceinline__ uint32_t unit_tile(const KernelArgs& ka, uint32_t pos, uint32_t& frame) {
+    if (pos == 0xffffffffu) return pos;
+    frame = ka.frame_light ? pos / ka.owned_tiles : 0u;
+    const uint32_t q = pos - frame * ka.owned_tiles;
+    return ka.tile_order ? ka.tile_order[q] : q;
 }
 
 // Cost-ordered schedule support: adds the rays of the pixels this wave just
@@ -900,6 +909,8 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     constexpr uint32_t kIdle = 0, kSetup = 1, kTrav = 2, kDone = 3;
     uint32_t rays = 0;
     uint32_t lane_tile = 0;  // local tile of the lane's pixel (tile costs)
+    uint32_t lane_slot = 0;  // the pixel's slot in its tile (frame-parallel light stores)
+    const bool frame_par = ka.frame_light != nullptr;
     uint32_t mode = kIdle;
     uint32_t index = 0, sample = 0, frame = 0;
     float4 pix = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -947,6 +958,22 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         ka.output[index] = pack_rgba8(r, g, b, a);  // :178
     };
     auto finish_sample = [&]() {
+        if (frame_par) {
+            // frame-parallel batch: this sample's light, added to the
+            // accumulation in order by rt_resolve_frames_kernel
+            const size_t slot = (size_t)(frame * samples + sample) * ((size_t)ka.owned_tiles * 64u) +
+                                (size_t)lane_tile * 64u + lane_slot;
+            ka.frame_light[slot] = make_float4(p.light.x, p.light.y, p.light.z, p.light.w);
+            sample += 1;
+            if (sample < samples) {
+                start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, index % ka.width, index / ka.width),
+                             p);
+                mode = kSetup;
+            } else {
+                mode = kIdle;
+            }
+            return;
+        }
         sample += 1;
         if (accumulate) {
             pix.x = pix.x + p.light.x;
@@ -978,7 +1005,8 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // home stripe: this XCD's (blocks are dealt round-robin over the XCDs, so
     // blockIdx / 8 spreads an XCD's blocks over its stripes when there are more)
     TileQueue queue{(xcc_id() + 8u * (blockIdx.x >> 3)) % ka.queue_stripes, 0u};
-    uint32_t tile = claim_tile(ka, queue);  // wave-uniform
+    uint32_t tile_frame = 0;         // frame of the claimed unit (frame-parallel batches), wave-uniform
+    uint32_t tile = unit_tile(ka, claim_tile(ka, queue), tile_frame);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
 #ifdef RT_DIAG
     unsigned long long iters = 0, trav_cyc = 0, steps = 0, step_lanes = 0, shade_cyc = 0, refill_cyc = 0,
@@ -1027,17 +1055,18 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                     if (x < ka.width && y < ka.height) {
                         index = y * ka.width + x;  // :148
                         lane_tile = tile;
+                        lane_slot = slot;
                         sample = 0;
-                        frame = 0;
+                        frame = tile_frame;
                         mode = kSetup;
-                        if (accumulate) pix = ka.accum[index];  // :156
-                        start_sample(ka, index, ka.accumulation_index, pixel_ray(ka, l_cam, index, x, y), p);
+                        if (accumulate && !frame_par) pix = ka.accum[index];  // :156
+                        start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, x, y), p);
                     }
                 }
             }
             next += min((uint32_t)__popcll(need), avail);
             if (next == 64u) {
-                tile = claim_tile(ka, queue);
+                tile = unit_tile(ka, claim_tile(ka, queue), tile_frame);
                 next = 0;
 #ifdef RT_DIAG_TAIL
                 if (tile >= ka.owned_tiles && wave_dry == 0) wave_dry = realtime();
@@ -1287,6 +1316,49 @@ extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(const f
     accum[idx] = v;
     output[idx] = pack_rgba8(clamp01(v.x / divisor), clamp01(v.y / divisor), clamp01(v.z / divisor),
                              clamp01(v.w / divisor));
+}
+
+// The end of a frame-parallel batch: for each owned pixel, the accumulation
+// plus every (frame, sample) light in the reference's order -- frame k's samples
+// k, k+1, ..., then frame k+1's (compute_shader.wgsl:156-164, src/renderer.rs:216-235)
+// -- so the sum is bit-identical to the frames rendered one after another; then
+// the accumulation and the last frame's packed output (:166-178). One thread per
+// owned pixel slot, coalesced: HBM-bound (16 + 16 * frames * samples + 20 B/px).
+extern "C" __global__ void __launch_bounds__(256) rt_resolve_frames_kernel(
+    float4* __restrict__ accum, uint32_t* __restrict__ output, const float4* __restrict__ light, uint32_t width,
+    uint32_t height, uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
+    uint32_t samples, uint32_t frames) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t owned_px = (uint64_t)owned_tiles * 64u;
+    if (gid >= owned_px) return;
+    const uint32_t lane = (uint32_t)(gid & 63u);
+    const uint32_t tile = (uint32_t)(gid >> 6) * world + rank;
+    const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u);
+    const uint32_t y = (tile / tiles_x) * 8u + (lane >> 3);
+    if (x >= width || y >= height) return;
+    const size_t idx = (size_t)y * width + x;
+    float4 pix = accum[idx];
+    const uint32_t n = frames * samples;
+    for (uint32_t i = 0; i < n; i++) {
+        const float4 l = light[(size_t)i * owned_px + gid];
+        pix.x = pix.x + l.x;
+        pix.y = pix.y + l.y;
+        pix.z = pix.z + l.z;
+        pix.w = pix.w + l.w;
+    }
+    accum[idx] = pix;
+    const float div = (float)((k0 + frames - 1u) * samples);
+    output[idx] = pack_rgba8(clamp01(pix.x / div), clamp01(pix.y / div), clamp01(pix.z / div), clamp01(pix.w / div));
+}
+
+hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
+                             uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
+                             uint32_t samples, uint32_t frames, hipStream_t stream) {
+    const uint64_t threads = (uint64_t)owned_tiles * 64u;
+    const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
+    hipLaunchKernelGGL(rt_resolve_frames_kernel, dim3(blocks), dim3(256), 0, stream, accum, output, light, width,
+                       height, tiles_x, owned_tiles, rank, world, k0, samples, frames);
+    return hipGetLastError();
 }
 
 // The packed RGBA8 output, one u32 per pixel, both ways (non-accumulating renders).

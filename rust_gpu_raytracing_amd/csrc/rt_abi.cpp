@@ -36,6 +36,9 @@ hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const 
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
+hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
+                             uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
+                             uint32_t samples, uint32_t frames, hipStream_t stream);
 hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t width, uint32_t height, uint32_t tiles_x,
                                  uint32_t owned_tiles, uint32_t rank, uint32_t world, bool unpack, hipStream_t stream);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
@@ -95,6 +98,10 @@ constexpr uint32_t kDefaultTileSchedule = 1;
 constexpr uint64_t kSchedMinTilesPerWave = 4;
 // Frame batching (rt_set_frame_batch): at most this many frames per launch.
 constexpr uint32_t kMaxFrameBatch = 64;
+// Frame-parallel batches (every (frame, tile) its own queue unit, lights resolved
+// in order afterwards) up to this many frames x samples; larger batches run each
+// pixel's frames back to back on one lane.
+constexpr uint32_t kMaxParallelLights = 64;
 
 }  // namespace
 
@@ -125,6 +132,9 @@ struct rt_ctx {
     uint32_t frame_batch = 1;     // frames per launch at most (1: one launch per frame)
     uint32_t pending_frames = 0;  // queued, not yet launched (their k already advanced)
     uint32_t pending_bounces = 0;
+    bool frame_parallel = true;     // RT_FRAME_PARALLEL=0: batches run frames back to back per lane (A/B switch)
+    float4* d_frame_light = nullptr;  // frame-parallel batch lights, owned px x frames x samples
+    size_t frame_light_cap = 0;       // float4 entries
 
     uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
     // extents the kernel clamps against (>= 1 so clamps never underflow)
@@ -503,6 +513,11 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+#ifndef RT_BUILD_HASH
+#define RT_BUILD_HASH "unknown"
+#endif
+const char* rt_build_hash(void) { return RT_BUILD_HASH; }
+
 const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int rt_srgb_table(float out[256]) {
@@ -594,6 +609,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TILE_SCHEDULE");
         if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
+        env = std::getenv("RT_FRAME_PARALLEL");
+        if (env) ctx->frame_parallel = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
         if (env) ctx->frame_batch = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxFrameBatch, (uint32_t)std::strtoul(env, nullptr, 10)));
     }
@@ -652,7 +669,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
-                    ctx->d_tile_sched};
+                    ctx->d_tile_sched, ctx->d_frame_light};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -941,6 +958,32 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.drain_threshold = ctx->drain_threshold;
     ka.drain_min_steps = ctx->drain_min_steps;
     ka.frames = frames;
+    // Frame-parallel batch: one queue unit per (frame, tile), lights resolved in order
+    // by rt_resolve_frames_kernel (accumulating renders; non-accumulating frames are
+    // all the same frame and keep the per-lane sequence).
+    const uint64_t owned_px = (uint64_t)ctx->owned_tiles * 64u;
+    const bool frame_par = frames > 1 && p.accumulate == 1u && ctx->frame_parallel &&
+                           (uint64_t)frames * p.compute_per_frame <= kMaxParallelLights && p.compute_per_frame > 0;
+    ka.frame_light = nullptr;
+    ka.queue_units = ctx->owned_tiles;
+    if (frame_par) {
+        const size_t need = (size_t)owned_px * frames * p.compute_per_frame;
+        if (need > ctx->frame_light_cap) {
+            // sized for the configured batch too, so a short first batch (a warmup)
+            // does not leave a reallocation for a later, timed launch
+            const size_t want = std::max<size_t>(
+                need, (size_t)owned_px * std::min<uint64_t>((uint64_t)ctx->frame_batch * p.compute_per_frame,
+                                                            kMaxParallelLights));
+            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->d_frame_light) RT_HIP(ctx, hipFree(ctx->d_frame_light));
+            ctx->d_frame_light = nullptr;
+            ctx->frame_light_cap = 0;
+            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_frame_light), want * sizeof(float4)));
+            ctx->frame_light_cap = want;
+        }
+        ka.frame_light = ctx->d_frame_light;
+        ka.queue_units = ctx->owned_tiles * frames;
+    }
 
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
@@ -1013,14 +1056,14 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
-    const uint64_t wanted = (ctx->owned_tiles + waves_per_block - 1) / waves_per_block;
+    const uint64_t wanted = ((uint64_t)ka.queue_units + waves_per_block - 1) / waves_per_block;
     const uint32_t blocks = (uint32_t)(wanted < resident ? wanted : resident);
     if (blocks == 0) return RT_OK;
     // Cost-ordered schedule, when each wave takes several tiles per launch (with
     // about one tile per wave the claim order cannot shorten the drain, and the
     // sort would sit on a short launch's critical path).
     const bool sched = ctx->tile_schedule &&
-                       (uint64_t)ctx->owned_tiles >= kSchedMinTilesPerWave * blocks * waves_per_block;
+                       (uint64_t)ka.queue_units >= kSchedMinTilesPerWave * blocks * waves_per_block;
     if (sched) {
         const size_t n = ctx->owned_tiles;
         if (!ctx->d_tile_sched) {
@@ -1053,6 +1096,12 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ctx->last_blocks = blocks;
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
+    if (frame_par) {
+        e = rt_launch_resolve(ctx->d_accum, ctx->d_out, ctx->d_frame_light, ctx->width, ctx->height, ctx->tiles_x,
+                              ctx->owned_tiles, ctx->rank, ctx->world, p.accumulation_index, p.compute_per_frame,
+                              frames, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, "rt_resolve_frames_kernel launch", e);
+    }
     // every tile is claimed once and every wave makes one final failing claim
     ctx->queue_parity ^= 1u;  // this launch zeroes the other half for the next one
     if (ctx->timing) {

@@ -148,6 +148,13 @@ struct KernelArgs {
     const float* __restrict__ tri_extent;  // max |coordinate| over sub-object boxes (margin scale), device memory
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
+    // Frame-parallel batch (frames > 1, accumulating): the queue holds one unit per
+    // (frame, tile) -- queue_units = frames * owned_tiles -- and a finished sample
+    // stores its path light to frame_light[(frame * compute_per_frame + sample) *
+    // owned_px + local pixel]; rt_resolve_frames_kernel then adds them to the
+    // accumulation in the reference's order. Null / owned_tiles otherwise.
+    float4* __restrict__ frame_light;
+    uint32_t queue_units;
     uint32_t texture_width;
     uint32_t texture_height;
     uint32_t env_map_width;

@@ -9,6 +9,20 @@ if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
 
 
+def pytest_report_header(config):
+    """Which native build the run loads: the hash embedded in the library against the
+    sources' hash, and where / with which hipcc command it was compiled."""
+    try:
+        from rust_gpu_raytracing_amd import build as nb
+
+        info = nb.build_info()
+        return [f"rt_pathtrace build: hash {info.get('hash')} (sources {info['sources_hash']}), "
+                f"host {info.get('host')}, at {info.get('built_at')}",
+                f"rt_pathtrace hipcc: {info.get('command')}"]
+    except Exception as e:  # the header must never break collection
+        return [f"rt_pathtrace build: unavailable ({e})"]
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the HIP kernel)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

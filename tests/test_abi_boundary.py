@@ -44,6 +44,14 @@ def test_abi_version(native_lib):
     assert native_lib.rt_abi_version() == 5
 
 
+def test_library_built_from_these_sources(native_lib):
+    """The loaded library embeds the hash of the sources + flags it was compiled from
+    (build.py: content-gated, not mtime-gated): it must be this tree's."""
+    from rust_gpu_raytracing_amd import build as nb
+
+    assert native_lib.rt_build_hash().decode() == nb.source_hash() == nb.build_info()["hash"]
+
+
 def test_ctypes_layouts_match_header():
     assert ctypes.sizeof(N.rt_params) == B.PARAMS.itemsize == 48
     # rt_create_info: 4 u32, camera 16 B, rays pointer, then 5 (pointer, u32 count + pad) pairs

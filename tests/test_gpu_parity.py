@@ -259,16 +259,21 @@ def test_gpu_pack_unpack_gather(gpu, accumulate):
             r.close()
 
 
-@pytest.mark.parametrize("config,spp,accumulate,batch,kw", [
-    ("c2_rtiow", 1, 1, 4, {}),
-    ("c3_chess", 2, 1, 3, dict(env_size=(512, 256))),
-    ("c1_four_spheres", 1, 0, 4, {}),
-    ("c5_heightfield", 1, 1, 2, dict(nx=80, nz=40)),
+@pytest.mark.parametrize("config,spp,accumulate,batch,parallel,kw", [
+    ("c2_rtiow", 1, 1, 4, "1", {}),
+    ("c2_rtiow", 1, 1, 4, "0", {}),
+    ("c3_chess", 2, 1, 3, "1", dict(env_size=(512, 256))),
+    ("c3_chess", 2, 1, 3, "0", dict(env_size=(512, 256))),
+    ("c1_four_spheres", 1, 0, 4, "1", {}),
+    ("c5_heightfield", 1, 1, 2, "1", dict(nx=80, nz=40)),
 ])
-def test_gpu_frame_batch(gpu, oracle_lib, config, spp, accumulate, batch, kw):
+def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, batch, parallel, kw):
     """rt_set_frame_batch: queued frames launched F at a time give, after every
     observable point, exactly the single-frame sequence (the oracle's): a readback
-    in the middle of a batch, a bounce change, and a tail shorter than F."""
+    in the middle of a batch, a bounce change, and a tail shorter than F. Both batch
+    kernels: frame-parallel (a queue unit per (frame, tile), lights resolved in order,
+    the default) and RT_FRAME_PARALLEL=0 (each pixel's frames back to back on a lane)."""
+    monkeypatch.setenv("RT_FRAME_PARALLEL", parallel)
     scene, bounces = build_config(config, width=96, height=56, **kw)
     rays = scene.camera.recalculate_ray_directions()
     with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp, camera_rays=rays,

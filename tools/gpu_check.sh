@@ -5,7 +5,7 @@
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -e -o pipefail
 TAG=${1:-r01}; shift || true
-STEPS=${*:-tests smoke bench all prof multi}
+STEPS=${*:-tests smoke bench all prof multi strong}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -13,13 +13,14 @@ python3 -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1
 for s in $STEPS; do
   echo "== $s $(date +%T)"
   case $s in
-    tests) timeout -k 10 600 python3 -m pytest tests -m gpu -x -q > "$OUT/tests.log" 2>&1 ;;
+    tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1 ;;
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
-    all)   timeout -k 10 600 python3 tools/bench_all.py --no-cpu > "$OUT/bench_all.jsonl" 2> "$OUT/bench_all.err" ;;
+    all)   timeout -k 10 600 python3 tools/bench_all.py --no-cpu --frames 16 --frame-batch 8 > "$OUT/bench_all.jsonl" 2> "$OUT/bench_all.err" ;;
+    strong) timeout -k 10 300 python3 tools/strong_probe.py > "$OUT/strong_probe.jsonl" 2> "$OUT/strong_probe.err" ;;
     prof)  bash tools/profile.sh "$TAG" ;;  # then locally: python tools/update_traffic.py gpurun_out/prof_<tag> profiles/<tag>
     multi) # N-rank rehearsal on the one GPU of the box (gloo; the real run is RCCL, one GPU per rank)
-           for n in 2 4; do
+           for n in 2 4 8; do
              RT_BENCH_ONE_DEVICE=1 RT_DIST_BACKEND=gloo RT_BENCH_VERIFY_GATHER=1 timeout -k 10 300 \
                python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
                --master-port $((29500 + n)) bench.py --gpus $n --steps 10 --warmup 2 > "$OUT/multi_$n.json" 2> "$OUT/multi_$n.err"

@@ -1,0 +1,85 @@
+"""Predict the strong-scaling curve of bench.py from one GPU.
+
+On an N-GPU node every rank renders only its own 8x8 tiles (tile t -> rank t % N)
+with no communication until the final gather, so a rank's timed loop on its own
+GPU is the same program whether or not the other ranks exist. This tool runs
+each rank's share of the bench workload alone on the one GPU of the box, in
+turn, with the bench's settings (bench.default_frame_batch(N), same steps), and reports per N:
+the slowest rank's render time per frame, the predicted whole-job Mray/s (all
+ranks' rays / the slowest rank's time, as bench.py computes `value`), and the
+predicted parallel efficiency against N=1 without and with a measured estimate
+of the gather (pack + the bytes rank 0 receives, priced at --link-gbs).
+
+usage: python tools/strong_probe.py [--steps 20] [--warmup 3] [--ns 1 2 4 8]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import bench  # noqa: E402
+from rust_gpu_raytracing_amd import Renderer  # noqa: E402
+from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
+
+
+def time_rank(scene, bounces, rank, world, steps, warmup, fb):
+    import torch
+
+    with Renderer(scene, rank=rank, world_size=world, frame_batch=fb) as r:
+        for _ in range(warmup):
+            r.compute_frame(bounces)
+        r.synchronize()
+        r.reset_ray_count()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r.compute_frame(bounces)
+        r.synchronize()
+        t = time.perf_counter() - t0
+        rays = r.ray_count()
+        # the device half of the gather: pack this rank's accumulation
+        n = r.owned_pixel_count()
+        buf = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+        r.synchronize()
+        p0 = time.perf_counter()
+        r.pack_owned_accumulation(buf.data_ptr())
+        r.synchronize()
+        t_pack = time.perf_counter() - p0
+    return t, rays, t_pack, n * 16
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2_rtiow")
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ns", type=int, nargs="*", default=[1, 2, 4, 8])
+    ap.add_argument("--link-gbs", type=float, default=50.0,
+                    help="xGMI bandwidth one peer achieves into rank 0 (GB/s, per link; 7 links)")
+    args = ap.parse_args()
+    scene, bounces = build_config(args.config)
+    base = None
+    for n in args.ns:
+        fb = bench.default_frame_batch(n)
+        per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb) for r in range(n)]
+        t_max = max(p[0] for p in per)
+        rays = sum(p[1] for p in per)
+        # gather estimate: packs run in parallel (max), rank 0 receives N-1 blocks over N-1 links
+        t_gather = (max(p[2] for p in per) + (max(p[3] for p in per) / (args.link_gbs * 1e9)) + 2 * 50e-6) if n > 1 else 0.0
+        v = rays / t_max / 1e6
+        vg = rays / (t_max + t_gather) / 1e6
+        if base is None:
+            base = v
+        print(json.dumps({
+            "n": n, "frame_batch": fb, "ms_per_frame_slowest_rank": t_max / args.steps * 1e3,
+            "ms_per_frame_per_rank": [round(p[0] / args.steps * 1e3, 4) for p in per],
+            "pred_mray_s": v, "pred_eff": v / (n * base),
+            "gather_est_ms": t_gather * 1e3, "pred_mray_s_with_gather": vg, "pred_eff_with_gather": vg / (n * base),
+            "steps": args.steps,
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -27,14 +27,15 @@ def main(prof_dir, dest):
         shutil.copy(ks, dest / "kernel_stats.csv")
     bench_line = json.loads((prof_dir / "trace_bench.json").read_text().strip().splitlines()[-1])
     shutil.copy(prof_dir / "trace_bench.json", dest / "trace_bench.json")
-    workload = bench_line["config"]["workload"]
+    key = f'{bench_line["config"]["workload"]} | frame_batch {bench_line["config"]["frame_batch"]}'
     f = ROOT / "profiles" / "pmc_traffic.json"
     table = json.loads(f.read_text()) if f.exists() else {}
-    table[workload] = {"fetch_bytes_x2": summ["fetch_bytes_x2"], "write_bytes": summ["write_bytes"],
-                       "avg_ns": summ.get("avg_ns"), "valu_issue_util": summ.get("valu_issue_util"),
-                       "valu_lane_util": summ.get("valu_lane_util"), "source": str(dest.relative_to(ROOT))}
+    table[key] = {"fetch_bytes_x2": summ["fetch_bytes_x2"], "write_bytes": summ["write_bytes"],
+                  "avg_ns": summ.get("avg_ns"), "valu_issue_util": summ.get("valu_issue_util"),
+                  "valu_lane_util": summ.get("valu_lane_util"), "source": str(dest.relative_to(ROOT)),
+                  "build_hash": bench_line["roofline"]["build_hash"]}  # the kernel build the counters came from
     f.write_text(json.dumps(table, indent=1, sort_keys=True) + "\n")
-    print(json.dumps(table[workload]))
+    print(json.dumps(table[key]))
 
 
 if __name__ == "__main__":
