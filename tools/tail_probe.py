@@ -1,6 +1,7 @@
 """Ramp and tail of the persistent grid, from an RT_DIAG_TAIL build.
 
-usage: RT_LIB=build/ab/lib_tail.so python tools/tail_probe.py [config ...]
+usage: RT_LIB=build/variants/lib_tail.so python tools/tail_probe.py [--frame-batch F] [config ...]
+With --frame-batch F each probed launch renders a batch of F frames (rt_set_frame_batch).
 Per launch: first wave start -> mean/last wave start (ramp), mean/last wave end
 (tail), when waves first found the tile queue empty (dry) and how long they ran
 after that (drain), in microseconds of the device's 100 MHz real-time clock.
@@ -16,17 +17,23 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from rust_gpu_raytracing_amd import Renderer  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
-for name in sys.argv[1:] or ["c2_rtiow"]:
+argv = sys.argv[1:]
+fb = 1
+if argv[:1] == ["--frame-batch"]:
+    fb, argv = int(argv[1]), argv[2:]
+for name in argv or ["c2_rtiow"]:
     scene, bounces = build_config(name)
-    with Renderer(scene) as r:
-        r.compute_frame(bounces)
+    with Renderer(scene, frame_batch=fb) as r:
+        for _ in range(fb):
+            r.compute_frame(bounces)
         r.synchronize()
         res = []
         for _ in range(5):
             r.reset_ray_count()  # zeroes the diag counters too
             r.reset_timing()
             r.set_timing(True)
-            r.compute_frame(bounces)
+            for _ in range(fb):
+                r.compute_frame(bounces)
             r.synchronize()
             r.set_timing(False)
             kern_ms, _ = r.dispatch_time_total()
@@ -43,4 +50,4 @@ for name in sys.argv[1:] or ["c2_rtiow"]:
                         "dry_pct": [round(float(np.percentile(dry, q)), 1) for q in (0, 10, 50, 90, 100)],
                         "drain_pct": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 99, 100)],
                         "end_pct": [round(float(np.percentile(ends, q)), 1) for q in (10, 50, 90, 99, 100)]})
-        print(json.dumps({"config": name, "runs": res[1:]}))
+        print(json.dumps({"config": name, "frame_batch": fb, "runs": res[1:]}))
