@@ -133,8 +133,17 @@ struct rt_ctx {
     uint32_t pending_frames = 0;  // queued, not yet launched (their k already advanced)
     uint32_t pending_bounces = 0;
     bool frame_parallel = true;     // RT_FRAME_PARALLEL=0: batches run frames back to back per lane (A/B switch)
-    float4* d_frame_light = nullptr;  // frame-parallel batch lights, owned px x frames x samples
-    size_t frame_light_cap = 0;       // float4 entries
+    float4* d_frame_light[2] = {};    // frame-parallel batch lights (by batch parity), owned px x frames x samples
+    size_t frame_light_cap = 0;       // float4 entries, each
+    // overlapped batches (dispatch_frames): batch i runs on streams[i % 2]
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_resolved[2] = {};   // after batch i's resolve (i % 2)
+    hipEvent_t ev_aux_done = nullptr; // after the last work issued on aux_stream
+    hipEvent_t ev_primary = nullptr;  // a point of the primary stream an aux batch waits for
+    bool aux_outstanding = false;     // aux work the primary stream has not been ordered after yet
+    bool primary_dirty = true;        // primary-stream work since then that an aux batch must follow
+    uint64_t batches = 0;             // frame-parallel batches launched
+    bool batch_overlap = true;        // RT_BATCH_OVERLAP=0: every batch on the primary stream (A/B switch)
 
     uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
     // extents the kernel clamps against (>= 1 so clamps never underflow)
@@ -144,8 +153,8 @@ struct rt_ctx {
     float4* d_accum = nullptr;
     uint32_t* d_out = nullptr;
     unsigned long long* d_counter = nullptr;
-    uint32_t* d_queue = nullptr;  // 2 x kQueueStripes tile-queue counters, kQueueStride apart
-    uint32_t queue_parity = 0;    // which half the next launch uses (the launch zeroes the other)
+    uint32_t* d_queue = nullptr;  // [stream][2] x kQueueStripesMax tile-queue counters, kQueueStride apart
+    uint32_t queue_parity[2] = {0, 0};  // per stream: which half its next launch uses (the launch zeroes the other)
     uint32_t queue_stripes = kQueueStripes;  // RT_QUEUE_STRIPES (A/B switch)
     int n_cu = 0;
     bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
@@ -165,8 +174,9 @@ struct rt_ctx {
     // launch parity: launch L records costs[L&1], reads order[L&1], and its
     // first idle workgroup sorts costs[~L&1] (launch L-1's) into order[~L&1]
     uint32_t tile_schedule = kDefaultTileSchedule;  // RT_TILE_SCHEDULE (A/B switch)
-    uint32_t* d_tile_sched = nullptr;  // costs[2][n], orders[2][n], flags[2] (n = owned tiles)
-    uint64_t sched_launches = 0;       // launches since the schedule was (re)set
+    // per stream (launches on the auxiliary stream keep their own history):
+    uint32_t* d_tile_sched[2] = {};    // costs[2][n], orders[2][n], flags[2] (n = owned tiles)
+    uint64_t sched_launches[2] = {};   // launches since the schedule was (re)set
     uint32_t last_blocks = 0, last_lds = 0;
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
@@ -241,6 +251,14 @@ struct rt_ctx {
 
 static int flush_frames(rt_ctx* ctx);
 
+// Orders the primary stream after everything issued on the auxiliary stream
+// (overlapped batches): every call other than rt_compute_frame runs this first.
+static hipError_t join_aux(rt_ctx* ctx) {
+    if (!ctx->aux_outstanding) return hipSuccess;
+    ctx->aux_outstanding = false;
+    return hipStreamWaitEvent(ctx->stream, ctx->ev_aux_done, 0);
+}
+
 namespace {
 
 int fail(rt_ctx* ctx, int code, const std::string& msg) {
@@ -296,6 +314,7 @@ int staged_copy(rt_ctx* ctx, void* dst, size_t bytes) {
     if (bytes == 0) return RT_OK;
     RT_HIP(ctx, hipMemcpyAsync(dst, ctx->pinned, bytes, hipMemcpyHostToDevice, ctx->stream));
     RT_HIP(ctx, hipEventRecord(ctx->staging_done, ctx->stream));
+    ctx->primary_dirty = true;  // an overlapped batch issued later must follow this copy
     ctx->staging_busy = true;
     return RT_OK;
 }
@@ -470,6 +489,7 @@ int dev_alloc(rt_ctx* ctx, T** p, size_t count) {
     if (e != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
     e = hipMemsetAsync(*p, 0, bytes, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "hipMemsetAsync", e);
+    ctx->primary_dirty = true;
     return RT_OK;
 }
 
@@ -613,11 +633,18 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->frame_parallel = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
         if (env) ctx->frame_batch = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxFrameBatch, (uint32_t)std::strtoul(env, nullptr, 10)));
+        env = std::getenv("RT_BATCH_OVERLAP");
+        if (env) ctx->batch_overlap = env[0] != '0';
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
-    e = hipEventCreateWithFlags(&ctx->staging_done, hipEventDisableTiming);
-    if (e != hipSuccess) return bail(hip_fail(ctx, "hipEventCreate", e));
+    e = hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate (aux)", e));
+    for (hipEvent_t* ev : {&ctx->staging_done, &ctx->ev_resolved[0], &ctx->ev_resolved[1], &ctx->ev_aux_done,
+                           &ctx->ev_primary}) {
+        e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+        if (e != hipSuccess) return bail(hip_fail(ctx, "hipEventCreate", e));
+    }
 
     int rc;
     if ((rc = check_params(ctx, &info->params))) return bail(rc);
@@ -627,7 +654,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
 
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
         (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9 + kDiagWaveRecords)) ||
-        (rc = dev_alloc(ctx, &ctx->d_queue, 2 * kQueueStripesMax * kQueueStride)) ||
+        (rc = dev_alloc(ctx, &ctx->d_queue, 4 * kQueueStripesMax * kQueueStride)) ||  // 2 streams x 2 halves
         (rc = dev_alloc(ctx, &ctx->d_slot_sph, 4 * (size_t)info->sphere_count + 4)) ||  // padded groups
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
@@ -664,12 +691,13 @@ void rt_destroy(rt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)flush_frames(ctx);  // queued frames were submitted: they run before teardown
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
     void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_queue, ctx->d_slot_sph,
                     ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
-                    ctx->d_tile_sched, ctx->d_frame_light};
+                    ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1]};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -681,8 +709,11 @@ void rt_destroy(rt_ctx* ctx) {
         (void)hipEventDestroy(ev.start);
         (void)hipEventDestroy(ev.stop);
     }
-    if (ctx->staging_done) (void)hipEventDestroy(ctx->staging_done);
+    for (hipEvent_t ev : {ctx->staging_done, ctx->ev_resolved[0], ctx->ev_resolved[1], ctx->ev_aux_done,
+                          ctx->ev_primary})
+        if (ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     delete ctx;
 }
 
@@ -708,11 +739,17 @@ static int flush_frames(rt_ctx* ctx) {
         if (e0_ != hipSuccess) return hip_fail(ctx, "hipSetDevice", e0_); \
     } while (0)
 
-#define RT_ENTER(ctx)                                \
-    do {                                             \
-        RT_ENTER_NOFLUSH(ctx);                       \
-        const int rcf_ = flush_frames(ctx);          \
-        if (rcf_ != RT_OK) return rcf_;              \
+// Every entry point but rt_compute_frame: launch the queued frames, order the
+// primary stream after the auxiliary one, and note that primary-stream work may
+// follow (a later overlapped batch then waits for it).
+#define RT_ENTER(ctx)                                                   \
+    do {                                                                \
+        RT_ENTER_NOFLUSH(ctx);                                          \
+        const int rcf_ = flush_frames(ctx);                             \
+        if (rcf_ != RT_OK) return rcf_;                                 \
+        const hipError_t ej_ = join_aux(ctx);                           \
+        if (ej_ != hipSuccess) return hip_fail(ctx, "join_aux", ej_);   \
+        (ctx)->primary_dirty = true;                                    \
     } while (0)
 
 int rt_upload_textures(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height, uint32_t layers) {
@@ -897,9 +934,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.output = ctx->d_out;
     ka.ray_counter = ctx->d_counter;
     ka.diag = ctx->d_counter + 1;
-    ka.queue = ctx->d_queue + (size_t)ctx->queue_parity * kQueueStripesMax * kQueueStride;
-    ka.queue_next = ctx->d_queue + (size_t)(ctx->queue_parity ^ 1u) * kQueueStripesMax * kQueueStride;
-    ka.queue_stripes = ctx->queue_stripes;
+    ka.queue_stripes = ctx->queue_stripes;  // (queue counters: per stream, set at launch)
     ka.sphere_slots = ctx->d_slot_sph;
     ka.sphere_orig = ctx->d_slot_orig;
     ka.sphere_material = ctx->d_sph_mat;
@@ -970,18 +1005,22 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         const size_t need = (size_t)owned_px * frames * p.compute_per_frame;
         if (need > ctx->frame_light_cap) {
             // sized for the configured batch too, so a short first batch (a warmup)
-            // does not leave a reallocation for a later, timed launch
+            // does not leave a reallocation for a later, timed launch; two buffers,
+            // one per batch parity (overlapped batches)
             const size_t want = std::max<size_t>(
                 need, (size_t)owned_px * std::min<uint64_t>((uint64_t)ctx->frame_batch * p.compute_per_frame,
                                                             kMaxParallelLights));
+            RT_HIP(ctx, join_aux(ctx));
             RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            if (ctx->d_frame_light) RT_HIP(ctx, hipFree(ctx->d_frame_light));
-            ctx->d_frame_light = nullptr;
+            for (float4*& b : ctx->d_frame_light) {
+                if (b) RT_HIP(ctx, hipFree(b));
+                b = nullptr;
+            }
             ctx->frame_light_cap = 0;
-            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_frame_light), want * sizeof(float4)));
+            for (float4*& b : ctx->d_frame_light)
+                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&b), want * sizeof(float4)));
             ctx->frame_light_cap = want;
         }
-        ka.frame_light = ctx->d_frame_light;
         ka.queue_units = ctx->owned_tiles * frames;
     }
 
@@ -1064,19 +1103,41 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // sort would sit on a short launch's critical path).
     const bool sched = ctx->tile_schedule &&
                        (uint64_t)ka.queue_units >= kSchedMinTilesPerWave * blocks * waves_per_block;
+    // Overlapped batches: frame-parallel batches alternate between
+    // the primary and the auxiliary stream. Batch i's path kernel depends on no
+    // other batch (it writes its own light buffer, i % 2), so it starts on the CUs
+    // that batch i-1's drain frees; only its resolve waits for batch i-1's resolve
+    // (the accumulation order). Everything else stays on the primary stream.
+    const int si = (frame_par && ctx->batch_overlap) ? (int)(ctx->batches & 1u) : 0;
+    hipStream_t S = si ? ctx->aux_stream : ctx->stream;
+    if (!frame_par) RT_HIP(ctx, join_aux(ctx));  // a plain launch follows every earlier batch
+    if (si && ctx->primary_dirty) {  // primary-stream work (uploads, resets) the batch must follow
+        RT_HIP(ctx, hipEventRecord(ctx->ev_primary, ctx->stream));
+        RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_primary, 0));
+        ctx->primary_dirty = false;
+    }
+    ka.queue = ctx->d_queue + (size_t)(2 * si + ctx->queue_parity[si]) * kQueueStripesMax * kQueueStride;
+    ka.queue_next = ctx->d_queue + (size_t)(2 * si + (ctx->queue_parity[si] ^ 1u)) * kQueueStripesMax * kQueueStride;
+    if (frame_par) ka.frame_light = ctx->d_frame_light[ctx->batches & 1u];
     if (sched) {
         const size_t n = ctx->owned_tiles;
-        if (!ctx->d_tile_sched) {
-            int rc = dev_alloc(ctx, &ctx->d_tile_sched, 4 * n + 2);
+        uint32_t*& state = ctx->d_tile_sched[si];
+        if (!state) {
+            int rc = dev_alloc(ctx, &state, 4 * n + 2);
             if (rc) return rc;
-            RT_HIP(ctx, hipMemsetAsync(ctx->d_tile_sched, 0, (4 * n + 2) * 4, ctx->stream));
-            ctx->sched_launches = 0;
+            RT_HIP(ctx, hipMemsetAsync(state, 0, (4 * n + 2) * 4, ctx->stream));
+            ctx->primary_dirty = true;
+            if (si) {
+                RT_HIP(ctx, hipEventRecord(ctx->ev_primary, ctx->stream));
+                RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_primary, 0));
+            }
+            ctx->sched_launches[si] = 0;
         }
-        ka.sched = ctx->d_tile_sched;
-        // orders[parity] was written by the previous launch
-        ka.sched_bits = (uint32_t)(ctx->sched_launches & 1u);
+        ka.sched = state;
+        // orders[parity] was written by this stream's previous launch
+        ka.sched_bits = (uint32_t)(ctx->sched_launches[si] & 1u);
         ka.tile_cost = ka.sched + ka.sched_bits * (size_t)n;
-        ka.tile_order = ctx->sched_launches ? ka.sched + (2u + ka.sched_bits) * (size_t)n : nullptr;
+        ka.tile_order = ctx->sched_launches[si] ? ka.sched + (2u + ka.sched_bits) * (size_t)n : nullptr;
     }
 
     EventPair ev;
@@ -1090,25 +1151,33 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             RT_HIP(ctx, hipEventCreate(&ev.start));
             RT_HIP(ctx, hipEventCreate(&ev.stop));
         }
-        RT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
+        RT_HIP(ctx, hipEventRecord(ev.start, S));
     }
-    hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, ctx->stream);
+    hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, S);
     ctx->last_blocks = blocks;
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
     if (frame_par) {
-        e = rt_launch_resolve(ctx->d_accum, ctx->d_out, ctx->d_frame_light, ctx->width, ctx->height, ctx->tiles_x,
+        // the accumulation is summed in frame order: after the previous batch's resolve
+        if (ctx->batches > 0) RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_resolved[(ctx->batches - 1) & 1u], 0));
+        e = rt_launch_resolve(ctx->d_accum, ctx->d_out, ka.frame_light, ctx->width, ctx->height, ctx->tiles_x,
                               ctx->owned_tiles, ctx->rank, ctx->world, p.accumulation_index, p.compute_per_frame,
-                              frames, ctx->stream);
+                              frames, S);
         if (e != hipSuccess) return hip_fail(ctx, "rt_resolve_frames_kernel launch", e);
+        RT_HIP(ctx, hipEventRecord(ctx->ev_resolved[ctx->batches & 1u], S));
+        ctx->batches += 1;
     }
     // every tile is claimed once and every wave makes one final failing claim
-    ctx->queue_parity ^= 1u;  // this launch zeroes the other half for the next one
+    ctx->queue_parity[si] ^= 1u;  // this launch zeroes the other half for the stream's next one
     if (ctx->timing) {
-        RT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
+        RT_HIP(ctx, hipEventRecord(ev.stop, S));
         ctx->pending.push_back(ev);
     }
-    if (sched) ++ctx->sched_launches;
+    if (si) {
+        RT_HIP(ctx, hipEventRecord(ctx->ev_aux_done, S));
+        ctx->aux_outstanding = true;
+    }
+    if (sched) ++ctx->sched_launches[si];
     return RT_OK;
 }
 
@@ -1329,25 +1398,29 @@ int rt_set_tile_schedule(rt_ctx* ctx, uint32_t schedule) {
     RT_ENTER(ctx);
     if (schedule > 1) return fail(ctx, RT_E_INVALID, "tile schedule must be 0 (index order) or 1 (cost-ordered)");
     ctx->tile_schedule = schedule;
-    if (ctx->d_tile_sched)
-        RT_HIP(ctx, hipMemsetAsync(ctx->d_tile_sched, 0, (4 * (size_t)ctx->owned_tiles + 2) * 4, ctx->stream));
-    ctx->sched_launches = 0;
+    for (int si = 0; si < 2; si++) {
+        if (ctx->d_tile_sched[si])
+            RT_HIP(ctx, hipMemsetAsync(ctx->d_tile_sched[si], 0, (4 * (size_t)ctx->owned_tiles + 2) * 4, ctx->stream));
+        ctx->sched_launches[si] = 0;
+    }
     return RT_OK;
 }
 
 int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
     RT_ENTER(ctx);
+    // the primary stream's schedule: the one every single-frame launch and every
+    // other overlapped batch follows
     const size_t n = ctx->owned_tiles;
-    const bool on = ctx->tile_schedule && ctx->d_tile_sched;
-    const uint32_t par = (uint32_t)(ctx->sched_launches & 1u);  // the next launch's parity
+    const uint32_t* st = ctx->d_tile_sched[0];
+    const uint64_t launches = ctx->sched_launches[0];
+    const bool on = ctx->tile_schedule && st;
+    const uint32_t par = (uint32_t)(launches & 1u);  // the next launch's parity
     for (size_t i = 0; i < n && order; i++) order[i] = (uint32_t)i;
-    if (order && on && ctx->sched_launches)
-        RT_HIP(ctx, hipMemcpyAsync(order, ctx->d_tile_sched + 2 * n + par * n, n * 4, hipMemcpyDeviceToHost,
-                                   ctx->stream));
+    if (order && on && launches)
+        RT_HIP(ctx, hipMemcpyAsync(order, st + 2 * n + par * n, n * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (costs) {
-        if (on && ctx->sched_launches)  // what the last launch recorded
-            RT_HIP(ctx, hipMemcpyAsync(costs, ctx->d_tile_sched + (par ^ 1u) * n, n * 4, hipMemcpyDeviceToHost,
-                                       ctx->stream));
+        if (on && launches)  // what the last launch recorded
+            RT_HIP(ctx, hipMemcpyAsync(costs, st + (par ^ 1u) * n, n * 4, hipMemcpyDeviceToHost, ctx->stream));
         else
             std::memset(costs, 0, n * 4);
     }
@@ -1473,7 +1546,13 @@ int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uin
     return RT_OK;
 }
 
-void* rt_stream(rt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+void* rt_stream(rt_ctx* ctx) {
+    if (!ctx) return nullptr;
+    // work the caller orders on this stream follows every frame submitted so far
+    if (flush_frames(ctx) != RT_OK || join_aux(ctx) != hipSuccess) return nullptr;
+    ctx->primary_dirty = true;
+    return (void*)ctx->stream;
+}
 
 }  // extern "C"
 

@@ -623,3 +623,44 @@ def test_gpu_device_edit_models_invalidated_by_range_change(gpu):
         t = np.ascontiguousarray(np.stack([builder.transform_of(o) for o in scene.objects]))
         with pytest.raises(RtError):
             r._call("rt_update_objects", N.ptr(t), t.shape[0])
+
+
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_gpu_overlapped_batches_with_updates(gpu, oracle_lib, monkeypatch, overlap):
+    """Consecutive frame-parallel batches alternate between two HIP streams (the path
+    kernel of batch i overlaps batch i-1's drain; only its resolve waits for batch
+    i-1's): results must equal the one-frame-at-a-time sequence, including when
+    scene updates, a reset and readbacks are interleaved with queued batches."""
+    monkeypatch.setenv("RT_BATCH_OVERLAP", overlap)
+    scene, bounces = build_config("c2_rtiow", width=128, height=72)
+    rays = scene.camera.recalculate_ray_directions()
+
+    def run(batch):
+        with Renderer(scene, camera_rays=rays, frame_batch=batch) as r:
+            for _ in range(7):
+                r.compute_frame(bounces)
+            a1 = r.read_accumulation()
+            scene.materials["emission_power"][1] = np.float32(3.0)
+            r._call("rt_update_materials", N.ptr(scene.materials), scene.materials.shape[0])
+            for _ in range(5):
+                r.compute_frame(bounces)
+            r.reset_accumulation()
+            for _ in range(6):
+                r.compute_frame(bounces)
+            out = r.read_accumulation(), r.read_output(), r.ray_count()
+        scene.materials["emission_power"][1] = base_e
+        return a1, out
+
+    base_e = scene.materials["emission_power"][1].copy()
+    a1_ref, ref = run(1)
+    a1, got = run(2)
+    assert np.array_equal(a1.view(np.uint32), a1_ref.view(np.uint32))
+    assert got[2] == ref[2] and np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[0].view(np.uint32), ref[0].view(np.uint32))
+    # and the last six frames against the oracle (after the reset: k = 1..6, new material)
+    scene.materials["emission_power"][1] = np.float32(3.0)
+    try:
+        acc_o, out_o, _ = oracle_frames(oracle_lib, scene, bounces, 6, rays)
+    finally:
+        scene.materials["emission_power"][1] = base_e
+    assert np.array_equal(got[1], out_o) and np.array_equal(got[0].view(np.uint32), acc_o.view(np.uint32))

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--device-rays", action="store_true", help="generate primary rays on the device")
+    ap.add_argument("--frame-batch", type=int, default=8, help="rt_set_frame_batch (frames is rounded to a multiple)")
     args = ap.parse_args()
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     rays_dirs = scene.camera.recalculate_ray_directions()
@@ -51,13 +52,15 @@ def main():
             os.environ[k] = v
         lib = N.load_library(Path(p).resolve())
         if args.device_rays:
-            rs.append(Renderer(scene, lib=lib, device_rays=True))
+            rs.append(Renderer(scene, lib=lib, device_rays=True, frame_batch=args.frame_batch))
         else:
-            rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib))
+            rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib, frame_batch=args.frame_batch))
         os.environ.clear()
         os.environ.update(saved)
+    args.frames = max(1, args.frames // args.frame_batch) * args.frame_batch
     for r in rs:  # warmup
-        r.compute_frame(bounces)
+        for _ in range(args.frame_batch):
+            r.compute_frame(bounces)
         r.synchronize()
     times = {p: [] for p in args.libs}
     walls = {p: [] for p in args.libs}
@@ -75,7 +78,7 @@ def main():
             walls[p].append((time.perf_counter() - t0) * 1e3 / args.frames)
             r.set_timing(False)
             ms, n = r.dispatch_time_total()
-            times[p].append(ms / n)
+            times[p].append(ms / args.frames)  # kernel time per frame (a launch renders a batch)
             rays[p] = r.ray_count() / args.frames
     ref = rs[0].read_accumulation().view(np.uint32)
     same = [bool(np.array_equal(r.read_accumulation().view(np.uint32), ref)) for r in rs]

@@ -1,6 +1,6 @@
 """Time split of the frame loop from an RT_DIAG build (in-kernel s_memtime stamps).
 
-usage: RT_LIB=build/ab/lib_diag.so python tools/diag_split.py [config ...]
+usage: RT_LIB=build/variants/lib_diag.so python tools/diag_split.py [--frame-batch F] [config ...]
 Reports, summed over waves, the share of wave-cycles spent in the traversal
 loop (step 4 of the kernel loop); the rest is shading, RNG, refill and
 framebuffer I/O. Also: traversal steps per ray and mean lanes per step.
@@ -18,19 +18,24 @@ from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 SIZES = {"c1_four_spheres": (800, 600), "c2_rtiow": (1920, 1080), "c3_chess": (1920, 1080),
          "c4_mixed": (1920, 1080), "c5_heightfield": (1920, 1080)}
 
-for name in sys.argv[1:] or list(SIZES):
+argv = sys.argv[1:]
+fb = 1
+if argv[:1] == ["--frame-batch"]:
+    fb, argv = int(argv[1]), argv[2:]
+for name in argv or list(SIZES):
     w, h = SIZES[name]
     scene, bounces = build_config(name, width=w, height=h)
-    with Renderer(scene) as r:
-        r.compute_frame(bounces)
+    with Renderer(scene, frame_batch=fb) as r:
+        for _ in range(fb):
+            r.compute_frame(bounces)
         r.synchronize()
         r.reset_ray_count()
-        for _ in range(3):
+        for _ in range(3 * fb):
             r.compute_frame(bounces)
         c = r.debug_counters()
         rays = r.ray_count()
     total, trav, steps, it, step_lanes, shade, refill, setup = c[:8]
-    print(json.dumps({"config": name, "trav_share": trav / total, "shade_share": shade / total,
+    print(json.dumps({"config": name, "frame_batch": fb, "trav_share": trav / total, "shade_share": shade / total,
                       "refill_share": refill / total, "setup_share": setup / total,
                       "rest_share": 1 - (trav + shade + refill + setup) / total,
                       "cycles_per_ray": total / rays, "steps_per_ray": steps / rays,

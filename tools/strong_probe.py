@@ -56,13 +56,14 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--ns", type=int, nargs="*", default=[1, 2, 4, 8])
+    ap.add_argument("--frame-batch", type=int, default=0, help="override bench.default_frame_batch(N)")
     ap.add_argument("--link-gbs", type=float, default=50.0,
                     help="xGMI bandwidth one peer achieves into rank 0 (GB/s, per link; 7 links)")
     args = ap.parse_args()
     scene, bounces = build_config(args.config)
     base = None
     for n in args.ns:
-        fb = bench.default_frame_batch(n)
+        fb = args.frame_batch or bench.default_frame_batch(n)
         per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb) for r in range(n)]
         t_max = max(p[0] for p in per)
         rays = sum(p[1] for p in per)
