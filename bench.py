@@ -21,7 +21,10 @@ gather_ms). A secondary "weak" object measures the same view at N x the pixels
 of tiles per GPU). `value` = all ranks' rays / the slowest rank's time.
 
 roofline: algorithmic bytes per launch (bench.algorithmic_bytes) /
-the average launch time from HIP events on the renderer's stream. traffic and
+the average launch span on the device clock (rt_set_timing: first workgroup start
+to last workgroup end, what rocprofv3's kernel trace reports); consecutive batches
+overlap on two streams, so `achieved_effective` also divides by the wall time per
+launch. traffic and
 valu: the committed rocprofv3 PMC entry (profiles/pmc_traffic.json, FETCH_SIZE x2
 per the gfx950 note + WRITE_SIZE; SQ counters) of this workload, frame batch and
 kernel build hash; null (with the reason, and a warning) when stale.
@@ -279,6 +282,7 @@ def main() -> int:
         rays_per_launch = m["rays"] / max(n_timed, 1)
         b_launch = algorithmic_bytes(m["owned_px"], rays_per_launch, scene_bytes(scene), frames_per_launch)
         achieved = b_launch / avg_kernel_s / 1e9
+        eff_launch_s = m["t_render"] / max(n_timed, 1)  # wall time per launch: overlapped launches pipeline
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
         build_hash = native_build.source_hash()
         pmc, pmc_why = pmc_entry(f"{workload} | frame_batch {fb}", build_hash) if world == 1 else (None, "N>1")
@@ -319,6 +323,9 @@ def main() -> int:
                 "traffic_source": pmc["source"] if pmc else pmc_why,
                 "kernel": "rt_pathtrace_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
+                "kernel_timing": "device-clock span per launch (first workgroup start to last end), rt_set_timing",
+                "effective_ms_per_launch": eff_launch_s * 1e3,
+                "achieved_effective": b_launch / eff_launch_s / 1e9,
                 "frames_per_launch": frames_per_launch,
                 "launch": m["launch"],
                 "bytes_per_launch": b_launch,

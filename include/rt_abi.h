@@ -304,14 +304,16 @@ RT_API int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs)
 /* Current accumulation counter k (the value the next rt_compute_frame uses). */
 RT_API int rt_accumulation_index(const rt_ctx* ctx, uint32_t* out);
 
-/* Timing of the last rt_dispatch/rt_compute_frame launch, measured with HIP
- * events recorded on the context's stream around the kernel (milliseconds);
- * requires rt_set_timing(ctx, 1) before the launch. Synchronous. */
+/* Timing of path-tracing launches, enabled by rt_set_timing(ctx, 1) before them:
+ * each timed launch's span on the device clock, from the start of its first
+ * workgroup to the end of its last (s_memrealtime, the same interval rocprofv3's
+ * kernel trace reports; overlapped batches' spans overlap). rt_last_dispatch_ms:
+ * the last one (milliseconds). Synchronous. */
 RT_API int rt_set_timing(rt_ctx* ctx, int enable);
 RT_API int rt_last_dispatch_ms(rt_ctx* ctx, float* out_ms);
-/* Sum of the timed dispatch durations since the last rt_reset_timing, and
- * how many dispatches were timed (each one's events are read back at the next
- * launch or on this call, so timing a long run adds no host sync per frame). */
+/* Sum of the timed launch spans since the last rt_reset_timing, and how many
+ * launches were timed (read back in bulk on this call, so timing a long run adds
+ * no host sync per frame). */
 RT_API int rt_dispatch_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed);
 RT_API int rt_reset_timing(rt_ctx* ctx);
 

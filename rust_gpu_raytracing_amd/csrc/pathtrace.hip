@@ -700,12 +700,23 @@ __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka, TileQueue& 
 }
 
 // Queue position -> local tile (identity unless cost-ordered) and, in a
-// frame-parallel batch, the frame (positions are frame-major, so a launch ends
-// on the last frame's cheapest tiles). 0xffffffff (empty queue) stays so.
+// frame-parallel batch, the frame: frame-major positions (a cost-ordered launch
+// then ends on the last frame's cheapest tiles) or tile-major (a tile's frames
+// are claimed one after another: the same camera rays, near-identical primary
+// walks). 0xffffffff (empty queue) stays so.
 __device__ __forceinline__ uint32_t unit_tile(const KernelArgs& ka, uint32_t pos, uint32_t& frame) {
     if (pos == 0xffffffffu) return pos;
-    frame = ka.frame_light ? pos / ka.owned_tiles : 0u;
-    const uint32_t q = pos - frame * ka.owned_tiles;
+    uint32_t q;
+    if (!ka.frame_light) {
+        frame = 0u;
+        q = pos;
+    } else if (ka.unit_tile_major) {
+        q = pos / ka.frames;
+        frame = pos - q * ka.frames;
+    } else {
+        frame = pos / ka.owned_tiles;
+        q = pos - frame * ka.owned_tiles;
+    }
     return ka.tile_order ? ka.tile_order[q] : q;
 }
 
@@ -858,6 +869,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     __shared__ uint32_t block_rays;
 
     const uint32_t tid = threadIdx.x;
+    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, ka.objects,
                  l_srgb,          ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f};
@@ -1207,6 +1219,10 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         if (sorter == 0)
             sort_tiles_by_cost<kThreads>(ka.sched + (par ^ 1u) * n, sched_orders(ka) + (par ^ 1u) * n, n,
                                          reinterpret_cast<uint32_t*>(lds + ka.lds_srgb_offset));
+    }
+    if (ka.launch_clock) {  // the workgroup's end, once all its waves are done
+        __syncthreads();
+        if (tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
     }
 }
 

@@ -111,9 +111,7 @@ void rt_set_global_error(const std::string& msg) { g_create_error = msg; }
 
 namespace {
 
-struct EventPair {
-    hipEvent_t start = nullptr, stop = nullptr;
-};
+constexpr uint32_t kClockSlots = 4096;
 
 }  // namespace
 
@@ -144,6 +142,10 @@ struct rt_ctx {
     bool primary_dirty = true;        // primary-stream work since then that an aux batch must follow
     uint64_t batches = 0;             // frame-parallel batches launched
     bool batch_overlap = true;        // RT_BATCH_OVERLAP=0: every batch on the primary stream (A/B switch)
+    bool batch_schedule = false;      // RT_BATCH_SCHEDULE=1: cost-ordered claims in batches too (A/B switch)
+    // a tile's frames claimed one after another (C3 -12%, C4 -8%, C5 -4%, C2 -1.8% per frame
+    // against frame-major, profiles/r02_knobs2); RT_UNIT_TILE_MAJOR=0: frame-major (A/B switch)
+    bool unit_tile_major = true;
 
     uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
     // extents the kernel clamps against (>= 1 so clamps never underflow)
@@ -240,8 +242,14 @@ struct rt_ctx {
     bool timing = false;
     bool gen_rays = false;  // rt_update_camera_matrices: primary rays computed on the device
     float inv_proj[16] = {}, inv_view[16] = {};
-    std::vector<EventPair> pending;
-    std::vector<EventPair> pool;
+    // launch timing (rt_set_timing): each timed launch's kernel span on the device
+    // clock -- the first workgroup's start to the last one's end (s_memrealtime) --
+    // in a ring of slots read back in bulk; HIP events would time each launch from
+    // the moment its stream reached it, which overlapped batches make meaningless
+    unsigned long long* d_clock = nullptr;  // kClockSlots x {~min start, max end}
+    std::vector<uint32_t> clock_pending;    // slots of timed launches not yet read back
+    uint32_t clock_next = 0;
+    double wall_khz = 100000.0;             // device wall clock rate (hipDeviceAttributeWallClockRate)
     double total_ms = 0.0;
     uint64_t n_timed = 0;
     float last_ms = 0.0f;
@@ -494,36 +502,20 @@ int dev_alloc(rt_ctx* ctx, T** p, size_t count) {
 }
 
 int collect_timing(rt_ctx* ctx) {
-    for (EventPair& ev : ctx->pending) {
-        RT_HIP(ctx, hipEventSynchronize(ev.stop));
-        float ms = 0.f;
-        RT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
+    if (ctx->clock_pending.empty()) return RT_OK;
+    RT_HIP(ctx, join_aux(ctx));
+    std::vector<unsigned long long> c(2 * (size_t)kClockSlots);
+    RT_HIP(ctx, hipMemcpyAsync(c.data(), ctx->d_clock, c.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t slot : ctx->clock_pending) {
+        const unsigned long long t0 = ~c[2 * (size_t)slot], t1 = c[2 * (size_t)slot + 1];
+        if (c[2 * (size_t)slot] == 0 || t1 < t0) continue;  // no workgroup ran
+        const float ms = (float)((double)(t1 - t0) / ctx->wall_khz);
         ctx->total_ms += ms;
         ctx->n_timed += 1;
         ctx->last_ms = ms;
-        ctx->pool.push_back(ev);
     }
-    ctx->pending.clear();
-    return RT_OK;
-}
-
-int reap_finished_timing(rt_ctx* ctx) {
-    // non-blocking: harvest only pairs whose stop event has completed
-    size_t keep = 0;
-    for (size_t i = 0; i < ctx->pending.size(); i++) {
-        EventPair ev = ctx->pending[i];
-        if (hipEventQuery(ev.stop) == hipSuccess) {
-            float ms = 0.f;
-            RT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
-            ctx->total_ms += ms;
-            ctx->n_timed += 1;
-            ctx->last_ms = ms;
-            ctx->pool.push_back(ev);
-        } else {
-            ctx->pending[keep++] = ev;
-        }
-    }
-    ctx->pending.resize(keep);
+    ctx->clock_pending.clear();
     return RT_OK;
 }
 
@@ -635,9 +627,18 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->frame_batch = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxFrameBatch, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_BATCH_OVERLAP");
         if (env) ctx->batch_overlap = env[0] != '0';
+        env = std::getenv("RT_BATCH_SCHEDULE");
+        if (env) ctx->batch_schedule = env[0] == '1';
+        env = std::getenv("RT_UNIT_TILE_MAJOR");
+        if (env) ctx->unit_tile_major = env[0] != '0';
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) == hipSuccess && khz > 0)
+            ctx->wall_khz = (double)khz;
+    }
     e = hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate (aux)", e));
     for (hipEvent_t* ev : {&ctx->staging_done, &ctx->ev_resolved[0], &ctx->ev_resolved[1], &ctx->ev_aux_done,
@@ -697,18 +698,11 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
-                    ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1]};
+                    ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
+                    ctx->d_clock};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-    for (EventPair& ev : ctx->pending) {
-        (void)hipEventDestroy(ev.start);
-        (void)hipEventDestroy(ev.stop);
-    }
-    for (EventPair& ev : ctx->pool) {
-        (void)hipEventDestroy(ev.start);
-        (void)hipEventDestroy(ev.stop);
-    }
     for (hipEvent_t ev : {ctx->staging_done, ctx->ev_resolved[0], ctx->ev_resolved[1], ctx->ev_aux_done,
                           ctx->ev_primary})
         if (ev) (void)hipEventDestroy(ev);
@@ -1022,6 +1016,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ctx->frame_light_cap = want;
         }
         ka.queue_units = ctx->owned_tiles * frames;
+        ka.unit_tile_major = ctx->unit_tile_major ? 1u : 0u;
     }
 
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
@@ -1101,7 +1096,11 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // Cost-ordered schedule, when each wave takes several tiles per launch (with
     // about one tile per wave the claim order cannot shorten the drain, and the
     // sort would sit on a short launch's critical path).
-    const bool sched = ctx->tile_schedule &&
+    // Frame-parallel batches claim in index order: with the drain paid once per batch
+    // (and overlapped) the cost order's recording and sort cost more than they save,
+    // and index order keeps neighbouring tiles together (C2 -5.2%, C3 -2.7% per frame
+    // measured, profiles/r02_knobs); RT_BATCH_SCHEDULE=1 sorts them too (A/B switch).
+    const bool sched = ctx->tile_schedule && (!frame_par || ctx->batch_schedule) &&
                        (uint64_t)ka.queue_units >= kSchedMinTilesPerWave * blocks * waves_per_block;
     // Overlapped batches: frame-parallel batches alternate between
     // the primary and the auxiliary stream. Batch i's path kernel depends on no
@@ -1140,18 +1139,25 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.tile_order = ctx->sched_launches[si] ? ka.sched + (2u + ka.sched_bits) * (size_t)n : nullptr;
     }
 
-    EventPair ev;
+    ka.launch_clock = nullptr;
     if (ctx->timing) {
-        int rc = reap_finished_timing(ctx);
-        if (rc) return rc;
-        if (!ctx->pool.empty()) {
-            ev = ctx->pool.back();
-            ctx->pool.pop_back();
-        } else {
-            RT_HIP(ctx, hipEventCreate(&ev.start));
-            RT_HIP(ctx, hipEventCreate(&ev.stop));
+        if (ctx->clock_pending.size() >= kClockSlots) {
+            const int rc = collect_timing(ctx);
+            if (rc) return rc;
         }
-        RT_HIP(ctx, hipEventRecord(ev.start, S));
+        if (!ctx->d_clock) {
+            const int rc = dev_alloc(ctx, &ctx->d_clock, 2 * (size_t)kClockSlots);
+            if (rc) return rc;
+            if (si) {  // the zeroed slots must be in place before an aux launch
+                RT_HIP(ctx, hipEventRecord(ctx->ev_primary, ctx->stream));
+                RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_primary, 0));
+            }
+        }
+        const uint32_t slot = ctx->clock_next;
+        ctx->clock_next = (ctx->clock_next + 1) % kClockSlots;
+        ka.launch_clock = ctx->d_clock + 2 * (size_t)slot;
+        RT_HIP(ctx, hipMemsetAsync(ka.launch_clock, 0, 16, S));
+        ctx->clock_pending.push_back(slot);
     }
     hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, S);
     ctx->last_blocks = blocks;
@@ -1169,10 +1175,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     // every tile is claimed once and every wave makes one final failing claim
     ctx->queue_parity[si] ^= 1u;  // this launch zeroes the other half for the stream's next one
-    if (ctx->timing) {
-        RT_HIP(ctx, hipEventRecord(ev.stop, S));
-        ctx->pending.push_back(ev);
-    }
     if (si) {
         RT_HIP(ctx, hipEventRecord(ctx->ev_aux_done, S));
         ctx->aux_outstanding = true;

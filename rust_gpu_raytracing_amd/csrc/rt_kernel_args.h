@@ -155,6 +155,10 @@ struct KernelArgs {
     // accumulation in the reference's order. Null / owned_tiles otherwise.
     float4* __restrict__ frame_light;
     uint32_t queue_units;
+    uint32_t unit_tile_major;  // frame-parallel units: 1 = a tile's frames consecutive, 0 = frame-major
+    // launch timing (rt_set_timing), null otherwise: {~earliest workgroup start, latest
+    // workgroup end} on the device wall clock
+    unsigned long long* __restrict__ launch_clock;
     uint32_t texture_width;
     uint32_t texture_height;
     uint32_t env_map_width;

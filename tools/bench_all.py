@@ -1,7 +1,8 @@
 """Measure every BASELINE.json configuration on one GPU (+ the CPU oracle on a sample).
 
 usage: python tools/bench_all.py [--frames 10] [--configs c1_four_spheres c2_rtiow ...] [--cpu-seconds 8]
-Prints one JSON object per config: GPU Mray/s (HIP-event kernel time and wall),
+Prints one JSON object per config: GPU Mray/s (wall time of the timed frames; the
+device-clock span of each launch is reported too),
 rays per frame, algorithmic HBM bytes per launch and fraction of 8 TB/s, and the
 CPU oracle's Mray/s on a tile sample of the same frame.
 C4 is the 8-GPU configuration; here it runs whole on one GPU (the per-GPU share is
@@ -63,15 +64,18 @@ def main():
             ms, n = r.dispatch_time_total()
             rays = r.ray_count()
             launch = r.launch_config()
-        kern_s = ms / args.frames / 1e3  # kernel time per frame (a launch may render several)
+        # per frame: wall time of the timed frames (batches overlap on two streams, so the
+        # sum of the launches' device spans exceeds it); spans reported per launch
+        kern_s = wall / args.frames
+        span_ms = ms / max(n, 1)
         rpf = rays / args.frames
-        fpl = args.frames / n  # frames per launch
+        fpl = args.frames / max(n, 1)  # frames per launch
         b = bench.algorithmic_bytes(w * h, rpf * fpl, bench.scene_bytes(scene), fpl) / fpl  # per frame
         res = {
             "config": name, "width": w, "height": h, "bounces": bounces,
             "spheres": int(scene.spheres.shape[0]), "triangles": int(scene.flatten()[2].shape[0]),
             "gpu_mray_s": rpf / kern_s / 1e6, "gpu_mray_s_wall": rays / wall / 1e6,
-            "kernel_ms": kern_s * 1e3, "launches": n, "frame_batch": args.frame_batch, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
+            "ms_per_frame": kern_s * 1e3, "kernel_span_ms_per_launch": span_ms, "launches": n, "frame_batch": args.frame_batch, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
             "hbm_bytes_per_frame": b, "hbm_frac": b / kern_s / 8e12, "launch": launch,
             "scene_build_s": round(t_build, 2),
         }
