@@ -83,36 +83,90 @@ def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0
     return [b[: owned_tiles(n_tiles, r, world_size).shape[0] * 64].to(device) for r, b in enumerate(bufs)]
 
 
+class TileGather:
+    """Reusable readback gather for a tile-split Renderer: the pack buffer and (on
+    `dst`) the receive buffers are allocated once, so repeated gathers (one per
+    displayed frame in an interactive loop, once per run in bench.py) allocate
+    nothing. The first gather also makes RCCL set up its peer connections, which it
+    does lazily on a pair's first transfer; bench.py runs one during warmup.
+
+    Accumulating renders move the RGBA32F accumulation (16 B/px) and rebuild the
+    RGBA8 output from it with the last frame's divisor k*c (compute_shader.wgsl:166);
+    non-accumulating ones (which never write the accumulation, :171-178) move the
+    RGBA8 words as is."""
+
+    def __init__(self, renderer, dst: int = 0):
+        import torch
+        import torch.distributed as dist
+
+        self.r, self.dst = renderer, dst
+        self.rank, self.world = renderer.rank, renderer.world_size
+        tx_n, ty_n = tile_grid(renderer.width, renderer.height)
+        self.n_tiles = tx_n * ty_n
+        cap = max_owned_tiles(self.n_tiles, self.world) * 64
+        self.device = torch.device("cuda", renderer.device)  # the renderer's GPU, whatever torch's current device is
+        shape, dtype = ((cap, 4), torch.float32) if renderer.accumulate else ((cap,), torch.int32)
+        self.packed = torch.zeros(shape, dtype=dtype, device=self.device)
+        # gloo moves host tensors only
+        self.host = dist.get_backend() == "gloo"
+        send_dev = "cpu" if self.host else self.device
+        self.send = torch.zeros(shape, dtype=dtype, device=send_dev) if self.host else self.packed
+        self.recv = ([torch.empty(shape, dtype=dtype, device=send_dev) for _ in range(self.world)]
+                     if self.rank == dst else None)
+        self.recv_dev = ([torch.empty(shape, dtype=dtype, device=self.device) for _ in range(self.world)]
+                         if self.rank == dst and self.host else self.recv)
+
+    def __call__(self) -> None:
+        import torch
+        import torch.distributed as dist
+
+        r = self.r
+        if self.host:  # gloo: through host memory, synchronously
+            self._pack()
+            r.synchronize()
+            self.send.copy_(self.packed)
+            dist.gather(self.send, gather_list=self.recv, dst=self.dst)
+            if self.rank == self.dst:
+                for a, b in zip(self.recv_dev, self.recv):
+                    a.copy_(b)
+                torch.cuda.synchronize(self.device)
+                self._unpack()
+            r.synchronize()
+            return
+        # RCCL: everything stream-ordered on the renderer's own HIP stream (no host
+        # waits): the pack kernel, the gather (ProcessGroupNCCL orders its stream
+        # after the current stream, and the current stream after the collective),
+        # then the unpack kernels on the destination.
+        stream = torch.cuda.ExternalStream(r.stream_handle(), device=self.device)
+        with torch.cuda.device(self.device), torch.cuda.stream(stream):
+            self._pack()
+            dist.gather(self.send, gather_list=self.recv, dst=self.dst)
+            if self.rank == self.dst:
+                self._unpack()
+
+    def _pack(self) -> None:
+        if self.r.accumulate:
+            self.r.pack_owned_accumulation(self.packed.data_ptr())
+        else:
+            self.r.pack_owned_output(self.packed.data_ptr())
+
+    def _unpack(self) -> None:
+        r = self.r
+        divisor = max(r.accumulation_index - 1, 1) * r.compute_per_frame  # the last frame's k*c
+        for src, part in enumerate(self.recv_dev):
+            if src != self.rank and owned_tiles(self.n_tiles, src, self.world).shape[0]:
+                if r.accumulate:
+                    r.unpack_accumulation(part.data_ptr(), src, self.world, divisor)
+                else:
+                    r.unpack_output(part.data_ptr(), src, self.world)
+
+
 def gather_accumulation(renderer, dst: int = 0):
     """Assemble the whole frame of a tile-split render on rank `dst`'s Renderer:
-    device pack -> RCCL gather -> device unpack. Accumulating renders move the
-    RGBA32F accumulation (16 B/px) and rebuild the RGBA8 output from it with the
-    last frame's divisor k*c (compute_shader.wgsl:166); non-accumulating ones
-    (which never write the accumulation, :171-178) move the RGBA8 words as is."""
-    import torch
-
-    rank, world = renderer.rank, renderer.world_size
-    tx_n, ty_n = tile_grid(renderer.width, renderer.height)
-    n_tiles = tx_n * ty_n
-    cap = max_owned_tiles(n_tiles, world) * 64
-    device = torch.device("cuda", renderer.device)  # the renderer's GPU, whatever torch's current device is
-    if renderer.accumulate:
-        packed = torch.zeros((cap, 4), dtype=torch.float32, device=device)
-        renderer.pack_owned_accumulation(packed.data_ptr())
-    else:
-        packed = torch.zeros((cap,), dtype=torch.int32, device=device)
-        renderer.pack_owned_output(packed.data_ptr())
-    renderer.synchronize()
-    parts = gather_packed(packed, n_tiles, rank, world, dst)
-    if parts is None:
-        return
-    torch.cuda.synchronize(device)
-    k = renderer.accumulation_index - 1  # the last frame's accumulation_index
-    divisor = max(k, 1) * renderer.compute_per_frame
-    for src, part in enumerate(parts):
-        if src != rank and part.shape[0]:
-            if renderer.accumulate:
-                renderer.unpack_accumulation(part.data_ptr(), src, world, divisor)
-            else:
-                renderer.unpack_output(part.data_ptr(), src, world)
+    device pack -> RCCL gather -> device unpack (a TileGather cached on the
+    renderer, so a second call allocates nothing)."""
+    g = getattr(renderer, "_tile_gather", None)
+    if g is None or g.dst != dst:
+        g = renderer._tile_gather = TileGather(renderer, dst)
+    g()
     renderer.synchronize()

@@ -36,6 +36,7 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb):
         t0 = time.perf_counter()
         for _ in range(steps):
             r.compute_frame(bounces)
+        t_submit = time.perf_counter() - t0
         r.synchronize()
         t = time.perf_counter() - t0
         rays = r.ray_count()
@@ -47,7 +48,7 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb):
         r.pack_owned_accumulation(buf.data_ptr())
         r.synchronize()
         t_pack = time.perf_counter() - p0
-    return t, rays, t_pack, n * 16
+    return t, rays, t_pack, n * 16, t_submit
 
 
 def main():
@@ -78,6 +79,7 @@ def main():
             "ms_per_frame_per_rank": [round(p[0] / args.steps * 1e3, 4) for p in per],
             "pred_mray_s": v, "pred_eff": v / (n * base),
             "gather_est_ms": t_gather * 1e3, "pred_mray_s_with_gather": vg, "pred_eff_with_gather": vg / (n * base),
+            "host_submit_ms_max": max(p[4] for p in per) * 1e3,
             "steps": args.steps,
         }), flush=True)
 
