@@ -32,11 +32,12 @@ for name in argv or list(SIZES):
         r.reset_ray_count()
         for _ in range(3 * fb):
             r.compute_frame(bounces)
-        c = r.debug_counters()
+        c = r.debug_counters(10)
         rays = r.ray_count()
-    total, trav, steps, it, step_lanes, shade, refill, setup = c[:8]
+    total, trav, steps, it, step_lanes, shade, refill, setup, leaf_cyc, leaf_steps = c[:10]
     print(json.dumps({"config": name, "frame_batch": fb, "trav_share": trav / total, "shade_share": shade / total,
                       "refill_share": refill / total, "setup_share": setup / total,
                       "rest_share": 1 - (trav + shade + refill + setup) / total,
                       "cycles_per_ray": total / rays, "steps_per_ray": steps / rays,
-                      "lanes_per_step": step_lanes / max(steps, 1), "outer_iters_per_ray": it / rays}))
+                      "lanes_per_step": step_lanes / max(steps, 1), "outer_iters_per_ray": it / rays,
+                      "leaf_share": leaf_cyc / total, "leaf_steps_per_ray": leaf_steps / rays}))
