@@ -301,11 +301,17 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
 // and triangle tests for one (object, sub-object) pair (compute_shader.wgsl:431-500).
-__device__ __forceinline__ void tri_leaf_tris(const KernelArgs& ka, f3 o, f3 d, TraceState& ts, uint32_t first,
-                                              uint32_t count, uint32_t seq_base, uint32_t obj) {
-    for (uint32_t j = 0; j < count; ++j) {
-        const uint32_t ti = min(first + j, ka.triangle_count - 1u);
-        const uint32_t seq = seq_base + j;
+__device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
+                                         uint32_t prim) {
+    const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base
+    const RtObject& ob = sv.obj[pr.x];
+    const RtSubObject sub = ka.sub_objects[pr.y];
+    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) ||
+        !ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds))
+        return;
+    for (uint32_t j = 0; j < sub.triangle_count; ++j) {
+        const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
+        const uint32_t seq = pr.z + j;
         const TriGeom g = load_tri(ka.triangles, ti);
         const float det = -dot(d, g.cn);
         const float inv_det = 1.0f / det;
@@ -325,137 +331,7 @@ __device__ __forceinline__ void tri_leaf_tris(const KernelArgs& ka, f3 o, f3 d, 
             ts.nan_hit = true;
             continue;
         }
-        ts.tri = TriHit{dist, seq, ti, obj, det > 0.0f};
-    }
-}
-
-__device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
-                                         uint32_t prim) {
-    const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base
-    const RtObject& ob = sv.obj[pr.x];
-    const RtSubObject sub = ka.sub_objects[pr.y];
-    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) ||
-        !ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds))
-        return;
-    tri_leaf_tris(ka, o, d, ts, sub.first_triangle_index, sub.triangle_count, pr.z, pr.x);
-}
-
-// Wave-cooperative triangle leaves (the leaf batch of the traversal loop; the
-// whole wave calls it, `mine` = this lane holds a deferred triangle leaf).
-//
-// Per lane, a leaf is 7 triangles of 48 B each: three 16-B loads per triangle,
-// each of the wave's 64 lanes on its own cache line, so a leaf batch costs
-// 21 x 64 line lookups in the texture addresser (TA) -- the unit that bounded
-// C5 (TA busy 64% of cycles) and half of C3's traversal. Here each lane first
-// runs its leaf's object and sub-object tests (the reference's, :431-446),
-// then the work is transposed: in rounds of 8 leaves, lane t tests triangle
-// t % 8 of leaf t / 8, reading it from the leaf-major copy (ka.leaf_tris:
-// per sub-object, piece k of triangle j at [k * 8 + j]), so the 8 lanes of a
-// leaf read one 128-B line per load and an instruction touches 8 lines
-// instead of 64. The ray comes from the owner lane (ds_bpermute), the test is
-// the reference's (:447-500) verbatim, and each leaf's candidates are reduced
-// to the lexicographic minimum of (distance, sweep position) -- the sweep's
-// first-wins result, so the order of the tests is free -- which its owner
-// merges into its best hit. Distances are keyed with -0.0 folded onto +0.0
-// (equal under the `<` of :457) and the winner's sign kept in a flag bit. A
-// NaN distance that passes the barycentric tests is flagged to the owner
-// (ts.nan_hit: the sweep decides, as in tri_leaf_tris). Sub-objects of more
-// than 8 triangles (none built by create_sub_objects) take tri_leaf_tris.
-__device__ __forceinline__ uint64_t tri_key(float dist, uint32_t seq, bool front) {
-    const uint32_t bits = dist == 0.0f ? 0u : __float_as_uint(dist);
-    const uint32_t negz = (dist == 0.0f && (__float_as_uint(dist) >> 31)) ? 2u : 0u;
-    return ((uint64_t)bits << 32) | (uint64_t)((seq << 2) | negz | (front ? 1u : 0u));
-}
-
-__device__ __forceinline__ void tri_leaves_coop(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d,
-                                                TraceState& ts, bool mine) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t count = 0, first = 0, seq_base = 0, sub_i = 0, obj_i = 0;
-    if (mine) {
-        const uint4 pr = sv.tri_prims[ts.pending];  // object, sub, seq_base
-        const RtObject& ob = sv.obj[pr.x];
-        const RtSubObject sub = ka.sub_objects[pr.y];
-        ts.pending = kNoLeaf;
-        if (ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) &&
-            ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) {
-            first = sub.first_triangle_index;
-            seq_base = pr.z;
-            sub_i = pr.y;
-            obj_i = pr.x;
-            if (sub.triangle_count <= 8u)
-                count = sub.triangle_count;
-            else
-                tri_leaf_tris(ka, o, d, ts, first, sub.triangle_count, seq_base, obj_i);
-        }
-    }
-    uint64_t rem = __ballot(count != 0u);
-    const uint32_t group = lane >> 3, j = lane & 7u;
-    while (rem) {
-        // this round's leaves: the 8 lowest owner lanes left; lane t tests for group t / 8
-        uint64_t round = 0;
-        uint32_t src = lane;
-        bool has = false;  // this lane's group has a leaf this round
-        for (uint32_t g = 0; g < 8u && rem; ++g) {
-            const uint32_t owner = (uint32_t)__builtin_ctzll(rem);
-            rem &= rem - 1u;
-            round |= 1ull << owner;
-            if (group == g) {
-                src = owner;
-                has = true;
-            }
-        }
-        const uint32_t n = (uint32_t)__shfl((int)count, (int)src);
-        const uint32_t sb = (uint32_t)__shfl((int)sub_i, (int)src);
-        const uint32_t sq = (uint32_t)__shfl((int)seq_base, (int)src) + j;
-        const f3 ro = mk(__shfl(o.x, (int)src), __shfl(o.y, (int)src), __shfl(o.z, (int)src));
-        const f3 rd = mk(__shfl(d.x, (int)src), __shfl(d.y, (int)src), __shfl(d.z, (int)src));
-        uint64_t key = ~0ull;
-        bool nan_flag = false;
-        if (has) {
-            if (j < n) {
-                const float4* lt = ka.leaf_tris + (size_t)sb * 24u + j;
-                const float4 p0 = lt[0], p1 = lt[8], p2 = lt[16];
-                const f3 a = mk(p0.x, p0.y, p0.z), ab = mk(p0.w, p1.x, p1.y), ac = mk(p1.z, p1.w, p2.x),
-                         cn = mk(p2.y, p2.z, p2.w);
-                const float det = -dot(rd, cn);
-                const float inv_det = 1.0f / det;
-                const f3 ao = ro - a;
-                const float dist = dot(ao, cn) * inv_det;
-                if (!(dist < 0.0f)) {
-                    const f3 dao = cross(ao, rd);
-                    const float v = -dot(ab, dao) * inv_det;
-                    const float u = dot(ac, dao) * inv_det;
-                    const float w = 1.0f - u - v;
-                    if (!(v < 0.0f) && !(u < 0.0f) && !(w < 0.0f)) {
-                        if (dist != dist)
-                            nan_flag = true;
-                        else
-                            key = tri_key(dist, sq, det > 0.0f);
-                    }
-                }
-            }
-        }
-        // lexicographic minimum over each group of 8 lanes
-#pragma unroll
-        for (int off = 1; off < 8; off <<= 1) {
-            const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), off) << 32) |
-                                   (uint32_t)__shfl_xor((int)(uint32_t)key, off);
-            key = other < key ? other : key;
-        }
-        const uint64_t nan_mask = __ballot(nan_flag);
-        // each owner of the round takes its group's result from the group's first lane
-        const uint32_t my_group = (uint32_t)__popcll(round & ((1ull << lane) - 1ull));
-        const uint64_t k = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), (int)(8u * my_group)) << 32) |
-                           (uint32_t)__shfl((int)(uint32_t)key, (int)(8u * my_group));
-        if ((round >> lane) & 1ull) {
-            if ((nan_mask >> (8u * my_group)) & 0xffull) ts.nan_hit = true;
-            const float kd = __uint_as_float((uint32_t)(k >> 32));
-            const uint32_t kseq = ((uint32_t)k) >> 2;
-            if (k != ~0ull && (kd < ts.tri.t || (kd == ts.tri.t && kseq < ts.tri.seq))) {
-                ts.tri = TriHit{((uint32_t)k & 2u) ? -0.0f : kd, kseq,
-                                min(first + (kseq - seq_base), ka.triangle_count - 1u), obj_i, ((uint32_t)k & 1u) != 0u};
-            }
-        }
+        ts.tri = TriHit{dist, seq, ti, pr.x, det > 0.0f};
     }
 }
 
@@ -1275,19 +1151,11 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #ifdef RT_DIAG
             const unsigned long long tl0 = stamp();
 #endif
-            bool coop_done = false;  // this lane's triangle leaf was tested by the wave
-            if constexpr (kTris) {
-                if (leaves && ka.leaf_tris) {
-                    coop_done = mode == kTrav && ts.pending != kNoLeaf && ts.phase == 0;
-                    tri_leaves_coop(sv, ka, p.o, p.d, ts, coop_done);
-                }
-            }
-            if (mode == kTrav && (!leaves || ts.pending != kNoLeaf || coop_done)) {
-                if (kDeferLeaves<kTris> && leaves) {
-                    if (ts.pending != kNoLeaf) leaf_step<kTris>(sv, ka, p.o, p.d, ts);
-                } else {
+            if (mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
+                if (kDeferLeaves<kTris> && leaves)
+                    leaf_step<kTris>(sv, ka, p.o, p.d, ts);
+                else
                     node_step<kTris>(sv, ka, p.o, p.d, ts);
-                }
                 phase_end<kTris>(sv, ka, p.o, p.d, ts);
                 if (ts.phase == 2) mode = kDone;
                 if (!(kDeferLeaves<kTris> && leaves)) {
@@ -1549,34 +1417,6 @@ hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t wi
     const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
     hipLaunchKernelGGL(rt_pack_output_kernel, dim3(blocks), dim3(256), 0, stream, output, packed, width, height,
                        tiles_x, owned_tiles, rank, world, unpack ? 1u : 0u);
-    return hipGetLastError();
-}
-
-// The leaf-major triangle copy of KernelArgs::leaf_tris (tri_leaves_coop): one
-// thread per (sub-object, piece k, triangle j < 8). Triangle indices are
-// clamped exactly as the kernel clamps them (min(first + j, triangle_count -
-// 1), :447); slots past the sub-object's count, and sub-objects of more than 8
-// triangles (tested per lane), stay unread.
-__global__ void rt_build_leaf_tris_kernel(const RtTriangleHot* __restrict__ tris, const RtSubObject* __restrict__ subs,
-                                          uint32_t n_sub, uint32_t n_tri, float4* __restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)n_sub * 24u) return;
-    const uint32_t s = (uint32_t)(i / 24u), k = (uint32_t)(i % 24u) >> 3, j = (uint32_t)i & 7u;
-    const RtSubObject sub = subs[s];
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (j < sub.triangle_count && sub.triangle_count <= 8u) {
-        const RtTriangleHot& t = tris[min(sub.first_triangle_index + j, n_tri - 1u)];
-        v = k == 0 ? t.p0 : (k == 1 ? t.p1 : t.p2);
-    }
-    out[i] = v;
-}
-
-hipError_t rt_launch_build_leaf_tris(const RtTriangleHot* tris, const RtSubObject* subs, uint32_t n_sub,
-                                     uint32_t n_tri, float4* out, hipStream_t stream) {
-    const uint64_t threads = (uint64_t)n_sub * 24u;
-    if (threads == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_build_leaf_tris_kernel, dim3((uint32_t)((threads + 255u) / 256u)), dim3(256), 0, stream,
-                       tris, subs, n_sub, n_tri, out);
     return hipGetLastError();
 }
 

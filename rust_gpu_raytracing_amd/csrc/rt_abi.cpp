@@ -43,8 +43,6 @@ hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t wi
                                  uint32_t owned_tiles, uint32_t rank, uint32_t world, bool unpack, hipStream_t stream);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
-hipError_t rt_launch_build_leaf_tris(const RtTriangleHot* tris, const RtSubObject* subs, uint32_t n_sub,
-                                     uint32_t n_tri, float4* out, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
                             uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, float divisor,
                             hipStream_t stream);
@@ -202,11 +200,6 @@ struct rt_ctx {
     bool tri_dirty = true;
     uint32_t tri_count_built = 0xffffffffu;
     bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
-    // leaf-major triangle copy for the wave-cooperative leaf test (KernelArgs::leaf_tris)
-    float4* d_leaf_tris = nullptr;
-    bool leaf_dirty = true;      // triangles or sub-objects changed since it was built
-    bool use_leaf_coop = true;   // RT_TRI_COOP=0 disables (A/B switch)
-    bool tri_seq_ok = false;     // every sweep position < 2^30 (the cooperative test's key)
     uint32_t tri_nodes = 0, tri_prim_count = 0;
     float* d_tri_extent = nullptr;   // margin extent, in device memory (refit updates it)
     uint32_t* d_tri_order = nullptr; // node indices by depth, deepest level first (refit)
@@ -422,10 +415,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         return rc;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
     ctx->tri_prim_count = (uint32_t)acc.prims.size();
-    uint64_t max_seq = 0;  // sweep positions key the cooperative leaf test's minimum (30 bits)
-    for (const SubObjectPrim& pr : acc.prims)
-        max_seq = std::max<uint64_t>(max_seq, (uint64_t)pr.seq_base + ctx->h_sub[pr.sub].triangle_count);
-    ctx->tri_seq_ok = max_seq < (1ull << 30);
     // depth levels for the device refit (preorder: a node precedes its children)
     std::vector<uint32_t> depth(acc.nodes.size(), 0);
     uint32_t max_depth = 0;
@@ -455,7 +444,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
 
 int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     if (n == 0) return RT_OK;
-    ctx->leaf_dirty = true;
     void* p;
     int rc = staging(ctx, (size_t)n * sizeof(RtTriangleHot), &p);
     if (rc) return rc;
@@ -615,8 +603,6 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->waves_cap = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_TRI_BVH");
         ctx->use_tri_bvh = !(env && env[0] == '0');
-        env = std::getenv("RT_TRI_COOP");
-        ctx->use_leaf_coop = !(env && env[0] == '0');
         env = std::getenv("RT_SPHERE_LEAF");
         ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
@@ -681,8 +667,6 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         (rc = dev_alloc(ctx, &ctx->d_srgb, 256)) || (rc = dev_alloc(ctx, &ctx->d_tex, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_env, 1)))
         return bail(rc);
-    if (info->object_count && ctx->use_leaf_coop && (rc = dev_alloc(ctx, &ctx->d_leaf_tris, 24 * (size_t)ctx->n_sub_dev)))
-        return bail(rc);
     ctx->tex_w = ctx->tex_h = ctx->tex_layers = 1;  // a black 1x1 placeholder until textures arrive
     ctx->env_w = ctx->env_h = 1;
 
@@ -715,7 +699,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
-                    ctx->d_clock, ctx->d_leaf_tris};
+                    ctx->d_clock};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -912,7 +896,6 @@ int rt_update_sub_object_info(rt_ctx* ctx, const rt_sub_object_info* sub_objects
             saved[i].triangle_count != sub_objects[i].triangle_count)
             ctx->models_valid = false;  // the device edit path's triangle maps are stale
     ctx->tri_dirty = true;
-    ctx->leaf_dirty = true;
     return upload_raw(ctx, ctx->d_sub, sub_objects, (size_t)count * 32);
 }
 
@@ -961,15 +944,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tri_extent = ctx->d_tri_extent;
     ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
     ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);
-    if (ka.tri_nodes && ctx->d_leaf_tris && ctx->tri_seq_ok) {
-        if (ctx->leaf_dirty) {  // stream-ordered after the uploads / edits that changed the triangles
-            RT_HIP(ctx, rt_launch_build_leaf_tris(ctx->d_tri, ctx->d_sub, ctx->n_sub_dev, ctx->n_tri_dev,
-                                                  ctx->d_leaf_tris, ctx->stream));
-            ctx->leaf_dirty = false;
-            ctx->primary_dirty = true;  // an overlapped batch on the auxiliary stream must follow it
-        }
-        ka.leaf_tris = ctx->d_leaf_tris;
-    }
     ka.materials = ctx->d_mat;
     ka.objects = ctx->d_obj;
     ka.sub_objects = ctx->d_sub;
@@ -1352,7 +1326,6 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
                                count, ctx->model_tris, (uint32_t)ctx->h_sub.size(), ctx->d_tri, ctx->d_tri_bounds,
                                ctx->d_sub, ctx->d_obj, ctx->stream));
     ctx->geom_on_device = true;
-    ctx->leaf_dirty = true;  // triangles and sub-object records were rewritten
     // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds
     if (ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty)
         RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,

@@ -120,11 +120,6 @@ struct KernelArgs {
     const RtTriangleHot* __restrict__ triangles;
     const float4* __restrict__ tri_bvh;           // BVH over (object, sub-object) pairs, float4 pairs per node
     const uint4* __restrict__ tri_prims;          // per leaf: object, sub-object, sweep position of its first triangle
-    // leaf-major triangle copy for the wave-cooperative leaf test (pathtrace.hip,
-    // tri_leaves_coop), null when off: per sub-object 24 float4, piece k (p0, p1,
-    // p2 of RtTriangleHot) of its triangle j < min(count, 8) at [k * 8 + j], the
-    // triangle index clamped as the kernel clamps it (rt_build_leaf_tris_kernel)
-    const float4* __restrict__ leaf_tris;
     // textures (bindings 9, 11), RGBA8 sRGB, + decode table
     const uint32_t* __restrict__ textures;
     const uint32_t* __restrict__ env;
