@@ -98,24 +98,29 @@ def pmc_issue(e):
 def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
     """The CPU oracle (scalar C restatement, OpenMP over the host cores) on a bounded
     sample of the same workload: the tiles t % sample_world == 0, frames k = 1, 2, ...
-    until min_seconds have elapsed."""
+    until min_seconds have elapsed. SURVEY §8d also asks for a 1-thread figure: the
+    same loop on one thread over 1/64 of the tiles, for a quarter of the time."""
     from oracle import oracle as O
 
     O.build()
     o = O.Oracle(scene)
+
+    def run(threads, world, seconds):
+        accum = np.zeros((o.height, o.width, 4), np.float32)
+        out = np.zeros((o.height, o.width), np.uint32)
+        rays = frames = 0
+        t0 = time.perf_counter()
+        while True:
+            frames += 1
+            p = scene.params(accumulation_index=frames)
+            rays += o.render_frame(p, bounces, accum, out, rank=0, world_size=world, threads=threads)
+            el = time.perf_counter() - t0
+            if el >= seconds or frames >= 512:
+                return rays, frames, el
+
     threads = O.lib().oracle_num_threads()
-    accum = np.zeros((o.height, o.width, 4), np.float32)
-    out = np.zeros((o.height, o.width), np.uint32)
-    rays = 0
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
-        frames += 1
-        p = scene.params(accumulation_index=frames)
-        rays += o.render_frame(p, bounces, accum, out, rank=0, world_size=sample_world, threads=threads)
-        el = time.perf_counter() - t0
-        if el >= min_seconds or frames >= 512:
-            break
+    rays, frames, el = run(threads, sample_world, min_seconds)
+    rays1, frames1, el1 = run(1, 64, min_seconds / 4)
     return {
         "value": rays / el / 1e6,
         "unit": "Mray/s",
@@ -124,6 +129,8 @@ def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
         "sample": (f"CPU oracle (oracle/pathtrace_oracle.c, -O2 scalar f32, OpenMP {threads} threads) on "
                    f"1/{sample_world} of the 8x8 tiles of the same {o.width}x{o.height} {bounces}-bounce frame, "
                    f"{frames} frame(s), {rays} rays in {el:.1f} s"),
+        "single_thread": {"value": rays1 / el1 / 1e6, "unit": "Mray/s", "cores": 1,
+                          "sample": f"1/64 of the tiles, {frames1} frame(s), {rays1} rays in {el1:.1f} s"},
     }
 
 
