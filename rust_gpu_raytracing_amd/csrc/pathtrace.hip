@@ -334,22 +334,10 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) ||
         !ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds))
         return;
-#ifdef RT_TRI_PAIR
-    // two triangles' loads in flight together (the tests stay in sweep order)
-    for (uint32_t j = 0; j < sub.triangle_count; j += 2u) {
-        const uint32_t ti0 = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
-        const uint32_t ti1 = min(sub.first_triangle_index + j + 1u, ka.triangle_count - 1u);
-        const TriGeom g0 = load_tri(ka.triangles, ti0);
-        const TriGeom g1 = load_tri(ka.triangles, ti1);
-        tri_test(g0, ti0, pr.z + j, pr.x, o, d, ts);
-        if (j + 1u < sub.triangle_count) tri_test(g1, ti1, pr.z + j + 1u, pr.x, o, d, ts);
-    }
-#else
     for (uint32_t j = 0; j < sub.triangle_count; ++j) {
         const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
         tri_test(load_tri(ka.triangles, ti), ti, pr.z + j, pr.x, o, d, ts);
     }
-#endif
 }
 
 // Ends the current BVH walk once its nodes are exhausted and no leaf is pending.
@@ -686,34 +674,46 @@ __device__ __forceinline__ uint32_t xcc_id() {
 }
 
 struct TileQueue {
-    uint32_t stripe;  // stripe being drained (wave-uniform)
-    uint32_t tried;   // stripes found empty so far
+    uint32_t stripe;  // stripe being drained (wave-uniform): the home stripe, then the last one stolen from
+    uint32_t empty;   // every stripe was found drained
 };
 
 // Returns the claimed queue position in [0, queue_units), or 0xffffffff when
-// the queue is empty (unit_tile maps a position to its tile and frame).
+// the queue is empty (unit_tile maps a position to its tile and frame). Stripe
+// s holds the positions k * n_str + s; its counter is the next k. One atomic
+// on the current stripe; once that is drained, the wave reads every stripe's
+// counter at once (lane i the i-th stripe after the current one, one load
+// instruction) and claims from the first that has work left, so finding the
+// queue empty costs one round trip instead of a walk over the stripes one
+// dependent load at a time (up to 31 of them, with the whole wave waiting, when
+// the stripes run dry together at the end of a launch).
 __device__ __forceinline__ uint32_t claim_tile(const KernelArgs& ka, TileQueue& q) {
     const uint32_t n_str = ka.queue_stripes;
-    const bool leader = (threadIdx.x & 63u) == 0;
-    while (q.tried < n_str) {
-        const uint32_t count = ka.queue_units > q.stripe ? (ka.queue_units - q.stripe + n_str - 1u) / n_str : 0u;
-        uint32_t* ctr = ka.queue + q.stripe * kQueueStride;
-        bool attempt = true;
-        if (q.tried > 0) {  // stealing: skip stripes that are already drained
-            uint32_t v = 0;
-            if (leader) v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            attempt = __builtin_amdgcn_readlane(v, 0) < count;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (q.empty) return 0xffffffffu;
+    uint32_t old = 0;
+    if (lane == 0) old = atomicAdd(ka.queue + q.stripe * kQueueStride, 1u);
+    uint64_t pos = (uint64_t)__builtin_amdgcn_readlane(old, 0) * n_str + q.stripe;
+    if (pos < ka.queue_units) return (uint32_t)pos;
+    while (true) {
+        bool open = false;
+        if (lane < n_str) {
+            uint32_t st = q.stripe + 1u + lane;
+            st = st >= n_str ? st - n_str : st;
+            const uint32_t v = __hip_atomic_load(ka.queue + st * kQueueStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            open = (uint64_t)v * n_str + st < ka.queue_units;
         }
-        if (attempt) {
-            uint32_t old = 0;
-            if (leader) old = atomicAdd(ctr, 1u);
-            old = __builtin_amdgcn_readlane(old, 0);
-            if (old < count) return old * n_str + q.stripe;
+        const uint64_t m = __ballot(open);
+        if (m == 0) {
+            q.empty = 1u;
+            return 0xffffffffu;
         }
-        q.stripe = q.stripe + 1u == n_str ? 0u : q.stripe + 1u;
-        q.tried += 1;
+        uint32_t st = q.stripe + 1u + (uint32_t)__builtin_ctzll(m);
+        q.stripe = st >= n_str ? st - n_str : st;
+        if (lane == 0) old = atomicAdd(ka.queue + q.stripe * kQueueStride, 1u);
+        pos = (uint64_t)__builtin_amdgcn_readlane(old, 0) * n_str + q.stripe;
+        if (pos < ka.queue_units) return (uint32_t)pos;
     }
-    return 0xffffffffu;
 }
 
 // Queue position -> local tile (identity unless cost-ordered) and, in a

@@ -33,12 +33,16 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb):
             r.compute_frame(bounces)
         r.synchronize()
         r.reset_ray_count()
+        r.reset_timing()
+        r.set_timing(True)
         t0 = time.perf_counter()
         for _ in range(steps):
             r.compute_frame(bounces)
         t_submit = time.perf_counter() - t0
         r.synchronize()
         t = time.perf_counter() - t0
+        r.set_timing(False)
+        span_ms, n_launch = r.dispatch_time_total()
         rays = r.ray_count()
         # the device half of the gather: pack this rank's accumulation
         n = r.owned_pixel_count()
@@ -48,7 +52,7 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb):
         r.pack_owned_accumulation(buf.data_ptr())
         r.synchronize()
         t_pack = time.perf_counter() - p0
-    return t, rays, t_pack, n * 16, t_submit
+    return t, rays, t_pack, n * 16, t_submit, span_ms, n_launch
 
 
 def main():
@@ -80,6 +84,8 @@ def main():
             "pred_mray_s": v, "pred_eff": v / (n * base),
             "gather_est_ms": t_gather * 1e3, "pred_mray_s_with_gather": vg, "pred_eff_with_gather": vg / (n * base),
             "host_submit_ms_max": max(p[4] for p in per) * 1e3,
+            "kernel_span_ms_per_rank": [round(p[5], 4) for p in per], "launches": per[0][6],
+            "wall_ms_per_rank": [round(p[0] * 1e3, 4) for p in per],
             "steps": args.steps,
         }), flush=True)
 

@@ -1,6 +1,6 @@
 """Ramp and tail of the persistent grid, from an RT_DIAG_TAIL build.
 
-usage: RT_LIB=build/variants/lib_tail.so python tools/tail_probe.py [--frame-batch F] [config ...]
+usage: RT_LIB=build/variants/lib_tail.so python tools/tail_probe.py [--frame-batch F] [--split R/N] [config ...]
 With --frame-batch F each probed launch renders a batch of F frames (rt_set_frame_batch).
 Per launch: first wave start -> mean/last wave start (ramp), mean/last wave end
 (tail), when waves first found the tile queue empty (dry) and how long they ran
@@ -19,11 +19,16 @@ from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
 argv = sys.argv[1:]
 fb = 1
-if argv[:1] == ["--frame-batch"]:
-    fb, argv = int(argv[1]), argv[2:]
+rank, world = 0, 1
+while argv[:1] in (["--frame-batch"], ["--split"]):
+    if argv[0] == "--frame-batch":
+        fb, argv = int(argv[1]), argv[2:]
+    else:  # --split R/N: rank R's share of an N-way tile split (the strong-scaling bench)
+        rank, world = map(int, argv[1].split("/"))
+        argv = argv[2:]
 for name in argv or ["c2_rtiow"]:
     scene, bounces = build_config(name)
-    with Renderer(scene, frame_batch=fb) as r:
+    with Renderer(scene, frame_batch=fb, rank=rank, world_size=world) as r:
         for _ in range(fb):
             r.compute_frame(bounces)
         r.synchronize()
@@ -50,4 +55,4 @@ for name in argv or ["c2_rtiow"]:
                         "dry_pct": [round(float(np.percentile(dry, q)), 1) for q in (0, 10, 50, 90, 100)],
                         "drain_pct": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 99, 100)],
                         "end_pct": [round(float(np.percentile(ends, q)), 1) for q in (10, 50, 90, 99, 100)]})
-        print(json.dumps({"config": name, "frame_batch": fb, "runs": res[1:]}))
+        print(json.dumps({"config": name, "frame_batch": fb, "split": f"{rank}/{world}", "runs": res[1:]}))
