@@ -301,31 +301,6 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
 // and triangle tests for one (object, sub-object) pair (compute_shader.wgsl:431-500).
-// One triangle of check_triangles (:447-500), first-wins on equal distance by
-// sweep position (the lexicographic minimum, see TriHit).
-__device__ __forceinline__ void tri_test(const TriGeom& g, uint32_t ti, uint32_t seq, uint32_t obj, f3 o, f3 d,
-                                         TraceState& ts) {
-    const float det = -dot(d, g.cn);
-    const float inv_det = 1.0f / det;
-    const f3 ao = o - g.a;
-    const float dist = dot(ao, g.cn) * inv_det;
-    const bool nan_dist = dist != dist;
-    if (dist < 0.0f) return;
-    if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) return;
-    const f3 dao = cross(ao, d);
-    const float v = -dot(g.ab, dao) * inv_det;
-    if (v < 0.0f) return;
-    const float u = dot(g.ac, dao) * inv_det;
-    if (u < 0.0f) return;
-    const float w = 1.0f - u - v;
-    if (w < 0.0f) return;
-    if (nan_dist) {
-        ts.nan_hit = true;
-        return;
-    }
-    ts.tri = TriHit{dist, seq, ti, obj, det > 0.0f};
-}
-
 __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
                                          uint32_t prim) {
     const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base
@@ -336,7 +311,27 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         return;
     for (uint32_t j = 0; j < sub.triangle_count; ++j) {
         const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
-        tri_test(load_tri(ka.triangles, ti), ti, pr.z + j, pr.x, o, d, ts);
+        const uint32_t seq = pr.z + j;
+        const TriGeom g = load_tri(ka.triangles, ti);
+        const float det = -dot(d, g.cn);
+        const float inv_det = 1.0f / det;
+        const f3 ao = o - g.a;
+        const float dist = dot(ao, g.cn) * inv_det;
+        const bool nan_dist = dist != dist;
+        if (dist < 0.0f) continue;
+        if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) continue;
+        const f3 dao = cross(ao, d);
+        const float v = -dot(g.ab, dao) * inv_det;
+        if (v < 0.0f) continue;
+        const float u = dot(g.ac, dao) * inv_det;
+        if (u < 0.0f) continue;
+        const float w = 1.0f - u - v;
+        if (w < 0.0f) continue;
+        if (nan_dist) {
+            ts.nan_hit = true;
+            continue;
+        }
+        ts.tri = TriHit{dist, seq, ti, pr.x, det > 0.0f};
     }
 }
 
