@@ -244,7 +244,7 @@ __device__ __forceinline__ float prune_limit(const TraceState& ts) {
 // box only: no slack, no distance limit.
 __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArgs& ka, f3 o, float a, uint32_t phase,
                                             TraceState& ts) {
-    const float r = sqrt_rn(dot(o, o));
+    const float r = sqrt_up(dot(o, o));  // |o| sizes the margins only: an upper bound will do
     float m;
     if (phase == 0) {
         m = kTriMarginScale * (r + sv.tri_extent) + 1.0e-30f;
@@ -265,7 +265,15 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
 // kTris: the scene has objects (triangles); false compiles the triangle side out.
 template <bool kTris>
 __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
-    ts.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if constexpr (kTris) {
+        ts.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // ray_in_bounds (:407-419) needs the IEEE quotient
+    } else {
+        // sphere-only scenes use 1/d only in the culling slab test, whose error
+        // budget (rt_bvh_slab.h: 16u X for rounding, orders under the margin)
+        // covers v_rcp_f32's 1 ulp; the sign (the layout octant) and +-inf for
+        // a zero component are exact
+        ts.inv = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    }
     const float a = dot(d, d);
     ts.a4 = 4.0f * a;
     ts.a2 = 2.0f * a;

@@ -35,6 +35,24 @@ struct SlabRay {
 
 RT_SLAB_FN float slab_cap_inv(float v) { return fabsf(v) > 1e30f ? copysignf(1e30f, v) : v; }
 
+// Upper bounds for quantities that only size the margins (bigger = more
+// conservative): 1/x and sqrt(x) from the hardware approximations (<= 1 ulp)
+// rounded up by 1.000001 (~8.4u), on the host from the IEEE results.
+RT_SLAB_FN float rcp_up(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x) * 1.000001f;
+#else
+    return (1.0f / x) * 1.000001f;
+#endif
+}
+RT_SLAB_FN float sqrt_up(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x) * 1.000001f;
+#else
+    return sqrtf(x) * 1.000001f;
+#endif
+}
+
 // inv: the ray's 1/d (exact, as the reference computes it); m: the margin.
 RT_SLAB_FN SlabRay slab_ray(float ox, float oy, float oz, float inv_x, float inv_y, float inv_z, float m) {
     SlabRay r;
@@ -74,7 +92,7 @@ RT_SLAB_FN void sphere_cull_bounds(float olen, float extent, float r_min, float 
                                    float& lateral, float& slack) {
     const float u = 5.9604645e-8f;  // 2^-24
     const float X = (olen + extent) * 1.0000005f;
-    const float quad = r_min > 0.0f ? (40.0f * u) * (X * X) / r_min : INFINITY;  // 4 x 10u X^2 / r
+    const float quad = r_min > 0.0f ? ((40.0f * u) * (X * X)) * rcp_up(r_min) : INFINITY;  // 4 x 10u X^2 / r
     const float lin = 4.4e-3f * X;                                               // ~4 x sqrt(20u) X
     lateral = fminf(quad, lin) + (16.0f * u) * X + (16.0f * u) * r_max + 1.0e-6f;
     slack = (4.4e-3f * (X + r_max) + (32.0f * u) * X) * (inv_dlen * 1.01f) + 1.0e-30f;

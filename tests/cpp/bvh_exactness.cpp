@@ -125,6 +125,16 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
         if (getenv("LAT_SCALE")) lateral *= (float)atof(getenv("LAT_SCALE"));
         if (getenv("SLACK_SCALE")) slack *= (float)atof(getenv("SLACK_SCALE"));
         V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        if (getenv("INV_ULP")) {
+            // sphere-only kernels take 1/d from v_rcp_f32 (<= 1 ulp): each component
+            // one ulp up or down, chosen per ray and axis
+            static uint32_t h = 0x9e3779b9u;
+            auto nudge = [&](float v) {
+                h = h * 747796405u + 2891336453u;
+                return std::isfinite(v) ? std::nextafter(v, (h >> 31) ? INFINITY : -INFINITY) : v;
+            };
+            inv = {nudge(inv.x), nudge(inv.y), nudge(inv.z)};
+        }
         const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);  // the kernel's slab test
         const bool oct = !getenv("SINGLE_LAYOUT");
         if (oct && g_oct.size() != 8 * (size_t)n) order_bvh_by_octant(sl.nodes, &g_oct);

@@ -35,6 +35,14 @@ def test_bvh_matches_brute_force(harness, seed):
     assert float(avg_tests) < 0.1 * int(n_spheres)  # the culling actually culls
 
 
+def test_bvh_with_one_ulp_reciprocals(harness):
+    """Sphere-only kernels take 1/d from v_rcp_f32 (<= 1 ulp); the culling stays exact
+    with every component of 1/d one ulp off in either direction."""
+    env = dict(os.environ, INV_ULP="1")
+    out = subprocess.run([str(harness), "400000", "4"], capture_output=True, text=True, env=env)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
+
+
 def test_margin_is_load_bearing(harness):
     env = dict(os.environ, LAT_SCALE="0.01")
     out = subprocess.run([str(harness), "1000000", "3"], capture_output=True, text=True, env=env)
