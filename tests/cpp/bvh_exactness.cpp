@@ -3,6 +3,7 @@
 // order, compiled with -ffp-contract=off) must return exactly the sphere and
 // t of the reference's brute-force scan (compute_shader.wgsl:355-404).
 // usage: bvh_exactness <n_rays> <seed>   -> prints "ok <rays> <hits> <avg_tests>" or the first mismatch
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -171,9 +172,12 @@ static int replay(const char* rays_path, const char* sph_path) {
     float q[6];
     long n = 0, bad = 0;
     g_tests = 0;
+    std::vector<uint32_t> visits;  // node visits per ray (distribution)
     while (fread(q, sizeof(q), 1, f) == 1) {
         V o{q[0], q[1], q[2]}, d{q[3], q[4], q[5]};
+        const long before = g_nodes;
         Res a = brute(s, o, d), b = getenv("ORDERED") ? ordered_like(sl, o, d) : kernel_like(sl, o, d);
+        visits.push_back((uint32_t)(g_nodes - before));
         uint32_t ta, tb;
         memcpy(&ta, &a.t, 4);
         memcpy(&tb, &b.t, 4);
@@ -185,6 +189,12 @@ static int replay(const char* rays_path, const char* sph_path) {
            " disc>=0 %.2f accepted %.2f\n",
            n, bad, s.size(), sl.n_always, sl.nodes.size(), (double)g_nodes / n, (double)g_tests / n,
            (double)g_disc_pos / n, (double)g_accept / n);
+    if (!visits.empty()) {
+        std::sort(visits.begin(), visits.end());
+        auto pct = [&](double q) { return visits[(size_t)(q * (visits.size() - 1))]; };
+        printf("node visits per ray: p10 %u p50 %u p90 %u p99 %u max %u\n", pct(0.1), pct(0.5), pct(0.9), pct(0.99),
+               visits.back());
+    }
     return bad ? 1 : 0;
 }
 
