@@ -5,15 +5,17 @@ Workload (BASELINE.json configs[1]): the RTIOW cover scene (484 spheres),
 1920x1080, 8 bounces, 1 sample per pixel per frame, accumulation on. One
 "step" = one Renderer.compute_frame (one frame: every pixel traced, its
 accumulation and RGBA8 output written). Frames are launched in batches of
---frame-batch (rt_set_frame_batch; default 8 at N=1: the persistent grid's fill
-and drain are paid once per 8 frames; every frame is traced in full and added to
-the accumulation in the reference's order). Inputs are resident in HBM before timing; the timed region
-holds exactly `--steps` frames bracketed by barrier + device synchronize.
+--frame-batch (rt_set_frame_batch; default: the steps split evenly into launches
+of at most 32N frames, default_frame_batch: the persistent grid's fill and drain
+are paid once per launch; every frame is traced in full and added to the
+accumulation in the reference's order). Inputs are resident in
+HBM before timing; the timed region holds exactly `--steps` frames bracketed by
+barrier + device synchronize.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 default "--scaling strong", the metric's config: the 1920x1080 frame is
-tile-split across ranks (8x8 tile t -> rank t % N), frame batch 8N
-(each GPU's launch holds the work of an N=1 launch), and the timed region also
+tile-split across ranks (8x8 tile t -> rank t % N), launches of up
+to 32N frames (a GPU's launch holds the units of an N=1 launch), and the timed region also
 assembles the image on rank 0 once (device pack -> RCCL gather of the RGBA32F
 accumulation -> unpack), so `value` includes the gather (also reported as
 gather_ms). A secondary "weak" object measures the same view at N x the pixels
@@ -134,12 +136,18 @@ def cpu_baseline(scene, bounces, min_seconds: float, sample_world: int):
     }
 
 
-def default_frame_batch(world: int) -> int:
-    """Frames per launch: 8 at N=1 (the persistent grid's fill and drain paid once per
-    8 frames, DESIGN.md §5.1: C2 0.454 -> 0.365 ms/frame, C3 0.830 -> 0.383), 8N at N
-    GPUs so that each GPU's launch holds the same work as at N=1 when the frame is
-    split N ways (capped at 64)."""
-    return min(64, 8 * world)
+def default_frame_batch(world: int, steps: int) -> int:
+    """Frames per launch: the timed steps split into launches of at most 32N frames
+    (64 at most), as evenly as they go -- 20 steps at N=1 are one 20-frame launch,
+    64 steps two of 32. A persistent launch pays one fill and one drain (about one
+    path at full iteration cost) whatever its size, and a tile split
+    over N GPUs needs N x the frames per launch for the same units per GPU. Measured
+    at 20 steps, per frame (profiles/r02_s3/r02_s3n, r02_s3o): C2 8 -> 20 frames
+    0.337 -> 0.329 ms, C3 0.333 -> 0.290, C5 17.5 -> 15.5; 64 steps, C2 batches of
+    8 -> 32: 0.318 -> 0.310."""
+    cap = min(64, 32 * world)
+    launches = -(-max(steps, 1) // cap)
+    return -(-max(steps, 1) // launches)
 
 
 def main() -> int:
@@ -158,7 +166,7 @@ def main() -> int:
                     help="N>1: leave the RCCL gather of the image to rank 0 out of the timed region")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the secondary weak-scaling measurement")
     ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
-                    help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N)")
+                    help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N, steps)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="N>1: strong = the 1920x1080 frame split N ways (the metric's config, `value`); "
                          "weak = N x the pixels (per-GPU work fixed)")
@@ -267,7 +275,7 @@ def main() -> int:
         res["t_total_max"], res["t_render_max"], res["t_gather_max"], res["rays_total"] = map(float, stats.tolist())
         return res
 
-    fb = args.frame_batch or default_frame_batch(world)
+    fb = args.frame_batch or default_frame_batch(world, args.steps)
     main_run = run(args.scaling, fb)
     r = main_run["r"]
     if main_run["gathered"] and os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
@@ -283,14 +291,14 @@ def main() -> int:
     r.close()
     weak = None
     if world > 1 and args.scaling == "strong" and not args.no_weak:
-        w_run = run("weak", args.frame_batch or default_frame_batch(1))
+        w_run = run("weak", args.frame_batch or default_frame_batch(1, args.steps))
         w_run["r"].close()
         weak = {
             "value": w_run["rays_total"] / w_run["t_total_max"] / 1e6,
             "ms_per_step": w_run["t_total_max"] / args.steps * 1e3,
             "render_ms_per_step": w_run["t_render_max"] / args.steps * 1e3,
             "gather_ms": w_run["t_gather_max"] * 1e3,
-            "width": w_run["width"], "height": w_run["height"], "frame_batch": args.frame_batch or default_frame_batch(1),
+            "width": w_run["width"], "height": w_run["height"], "frame_batch": args.frame_batch or default_frame_batch(1, args.steps),
             "note": "secondary: the same view at N x the pixels, every GPU owning one 1920x1080 frame's worth of tiles",
         }
 

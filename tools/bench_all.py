@@ -41,14 +41,16 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kw", default="{}", help="JSON builder kwargs applied to every config, e.g. '{\"env_size\": [1024, 512]}'")
     ap.add_argument("--size", default=None, help="WxH override")
-    ap.add_argument("--frame-batch", type=int, default=1, help="rt_set_frame_batch (frames per launch at most)")
+    ap.add_argument("--frame-batch", type=int, default=0,
+                    help="rt_set_frame_batch (frames per launch at most); 0 = bench.default_frame_batch(1, frames)")
     args = ap.parse_args()
     for name in args.configs:
         w, h = SIZES[name] if args.size is None else map(int, args.size.split("x"))
         t0 = time.perf_counter()
         scene, bounces = build_config(name, width=w, height=h, **json.loads(args.kw))
         t_build = time.perf_counter() - t0
-        with Renderer(scene, frame_batch=args.frame_batch) as r:
+        fb = args.frame_batch or default_frame_batch(1, args.frames)
+        with Renderer(scene, frame_batch=fb) as r:
             for _ in range(args.warmup):
                 r.compute_frame(bounces)
             r.synchronize()
@@ -75,7 +77,7 @@ def main():
             "config": name, "width": w, "height": h, "bounces": bounces,
             "spheres": int(scene.spheres.shape[0]), "triangles": int(scene.flatten()[2].shape[0]),
             "gpu_mray_s": rpf / kern_s / 1e6, "gpu_mray_s_wall": rays / wall / 1e6,
-            "ms_per_frame": kern_s * 1e3, "kernel_span_ms_per_launch": span_ms, "launches": n, "frame_batch": args.frame_batch, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
+            "ms_per_frame": kern_s * 1e3, "kernel_span_ms_per_launch": span_ms, "launches": n, "frame_batch": fb, "rays_per_frame": rpf, "nominal_rays_per_frame": w * h * bounces,
             "hbm_bytes_per_frame": b, "hbm_frac": b / kern_s / 8e12, "launch": launch,
             "scene_build_s": round(t_build, 2),
         }

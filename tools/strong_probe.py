@@ -4,7 +4,7 @@ On an N-GPU node every rank renders only its own 8x8 tiles (tile t -> rank t % N
 with no communication until the final gather, so a rank's timed loop on its own
 GPU is the same program whether or not the other ranks exist. This tool runs
 each rank's share of the bench workload alone on the one GPU of the box, in
-turn, with the bench's settings (bench.default_frame_batch(N), same steps), and reports per N:
+turn, with the bench's settings (bench.default_frame_batch(N, steps), same steps), and reports per N:
 the slowest rank's render time per frame, the predicted whole-job Mray/s (all
 ranks' rays / the slowest rank's time, as bench.py computes `value`), and the
 predicted parallel efficiency against N=1 without and with a measured estimate
@@ -68,7 +68,7 @@ def main():
     scene, bounces = build_config(args.config)
     base = None
     for n in args.ns:
-        fb = args.frame_batch or bench.default_frame_batch(n)
+        fb = args.frame_batch or bench.default_frame_batch(n, args.steps)
         per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb) for r in range(n)]
         t_max = max(p[0] for p in per)
         rays = sum(p[1] for p in per)
