@@ -49,7 +49,7 @@ def main():
         t0 = time.perf_counter()
         scene, bounces = build_config(name, width=w, height=h, **json.loads(args.kw))
         t_build = time.perf_counter() - t0
-        fb = args.frame_batch or default_frame_batch(1, args.frames)
+        fb = args.frame_batch or bench.default_frame_batch(1, args.frames)
         with Renderer(scene, frame_batch=fb) as r:
             for _ in range(args.warmup):
                 r.compute_frame(bounces)
