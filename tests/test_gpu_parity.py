@@ -266,6 +266,8 @@ def test_gpu_pack_unpack_gather(gpu, accumulate):
     ("c3_chess", 2, 1, 3, "0", dict(env_size=(512, 256))),
     ("c1_four_spheres", 1, 0, 4, "1", {}),
     ("c5_heightfield", 1, 1, 2, "1", dict(nx=80, nz=40)),
+    ("c2_rtiow", 1, 1, 20, "1", {}),  # the bench's launch at its default 20 steps
+    ("c3_chess", 1, 1, 64, "1", dict(env_size=(512, 256))),  # the largest batch
 ])
 def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, batch, parallel, kw):
     """rt_set_frame_batch: queued frames launched F at a time give, after every
