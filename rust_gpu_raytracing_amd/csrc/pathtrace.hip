@@ -50,6 +50,7 @@ struct SceneView {
     const uint32_t* sph_mat;  // per original index: material index
     const float4* nodes;      // sphere BVH, 2 float4 per node (sphere_bvh.h)
     const RtMaterial* mat;    // LDS
+    const float4* mat_aux;    // LDS (modes 1, 2): per material {1/ior, r0 front, r0 back, roughness/10}
     const RtObject* obj;      // LDS
     const float* srgb;        // LDS, 256 entries
     const float4* tri_nodes;  // triangle accelerator nodes (LDS in mode 2, else global)
@@ -572,6 +573,9 @@ __device__ __forceinline__ void start_sample(const KernelArgs& ka, uint32_t inde
 // The shading half of one iteration of the bounce loop, :228-311, given the
 // trace result. Returns true when the path is finished (escaped to the
 // environment, or the bounce limit is reached).
+// kAux: the material's glass constants come from the LDS table staged with the
+// materials (same f32 operations, computed once per workgroup instead of per hit).
+template <bool kAux>
 __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka, Path& p, const Hit& h) {
     if (h.t == kF32Max) {
         const f4 c = sample_env(ka, sv.srgb, p.d);
@@ -581,7 +585,8 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
         p.light.w = p.light.w + c.w * p.contrib.w;
         return true;
     }
-    const RtMaterial m = sv.mat[min(h.material_index, ka.material_count - 1u)];
+    const uint32_t mi = min(h.material_index, ka.material_count - 1u);
+    const RtMaterial m = sv.mat[mi];
     // the texel load is issued first so that its latency overlaps the draws
     const uint32_t texel = fetch_texture(ka, m.texture_index, h.u, h.v);
     const float gx = normal01(p.seed);
@@ -598,13 +603,22 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
     const bool is_glass = m.glass > random01(p.seed);
     bool tint;
     if (is_glass) {
-        float ior = m.refraction_index;
-        if (h.front_face) ior = 1.0f / ior;
+        float ior, r0, rough10;
+        if constexpr (kAux) {
+            const float4 ax = sv.mat_aux[mi];
+            ior = h.front_face ? ax.x : m.refraction_index;
+            r0 = h.front_face ? ax.y : ax.z;
+            rough10 = ax.w;
+        } else {
+            ior = m.refraction_index;
+            if (h.front_face) ior = 1.0f / ior;
+            r0 = (1.0f - ior) / (1.0f + ior);  // specular_percentage, :328-334
+            r0 = r0 * r0;
+            rough10 = div_const(m.roughness, 10.0f, kInv10);
+        }
         const float cos_t = fmin_nn(dot(-p.d, h.n), 1.0f);
         const float sin_t = sqrt_rn_nrm(1.0f - cos_t * cos_t);  // 0, >= 2^-24, or NaN
         const bool reflects = ior * sin_t > 1.0f;
-        float r0 = (1.0f - ior) / (1.0f + ior);  // specular_percentage, :328-334
-        r0 = r0 * r0;
         const float sp = r0 + (1.0f - r0) * pow5(1.0f - cos_t);
         const bool is_spec = (m.specular * sp) > random01(p.seed);
         if (reflects || is_spec) {
@@ -618,7 +632,7 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
             const float len_sq = len * len;
             // |1 - len_sq| is 0 or >= 2^-24 (exact difference near 1): sqrt_rn_nrm's domain
             const f3 refr = perp + h.n * (-sqrt_rn_nrm(__builtin_fabsf(1.0f - len_sq)));
-            p.d = lerp(refr, diffuse, div_const(m.roughness, 10.0f, kInv10));
+            p.d = lerp(refr, diffuse, rough10);
             p.o = h.p - h.n * 0.0001f;
             tint = true;
         }
@@ -891,8 +905,8 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     const uint32_t tid = threadIdx.x;
     if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
-    SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, ka.objects,
-                 l_srgb,          ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f};
+    SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
+                 ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f};
     if (tid == 0) block_rays = 0;
     if constexpr (kMode >= 1) {
         float4* l_sph = reinterpret_cast<float4*>(lds);
@@ -907,7 +921,19 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         }
         for (uint32_t i = tid; i < ka.sphere_count; i += kThreads) l_smat[i] = ka.sphere_material[i];
         for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
-        for (uint32_t i = tid; i < ka.material_count; i += kThreads) l_mat[i] = ka.materials[i];
+        float4* l_aux = reinterpret_cast<float4*>(lds + ka.lds_mat_aux_offset);
+        for (uint32_t i = tid; i < ka.material_count; i += kThreads) {
+            const RtMaterial m = ka.materials[i];
+            l_mat[i] = m;
+            // shade()'s glass constants, by the same f32 operations (:320, :328-334, :307)
+            const float ior_front = 1.0f / m.refraction_index;
+            float r0f = (1.0f - ior_front) / (1.0f + ior_front);
+            float r0b = (1.0f - m.refraction_index) / (1.0f + m.refraction_index);
+            r0f = r0f * r0f;
+            r0b = r0b * r0b;
+            l_aux[i] = make_float4(ior_front, r0f, r0b, div_const(m.roughness, 10.0f, kInv10));
+        }
+        sv.mat_aux = l_aux;
         if constexpr (kTris)
             for (uint32_t i = tid; i < ka.object_count; i += kThreads) l_obj[i] = ka.objects[i];
         sv.sph = l_sph;
@@ -1056,7 +1082,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         if (mode == kDone) {
             const Hit h = trace_end<kTris>(sv, ka, p.o, p.d, ts);
             ++rays;
-            if (shade(sv, ka, p, h)) {
+            if (shade<(kMode >= 1)>(sv, ka, p, h)) {
                 // rays of the sample: one per bounce, plus the escaping one unless the limit ended it
                 fin = true;
                 fin_rays = p.bounce + (p.bounce < ka.bounces ? 1u : 0u);

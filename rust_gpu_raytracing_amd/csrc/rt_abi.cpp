@@ -1028,6 +1028,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         size_t off = al16((size_t)ctx->n_slots * 16);
         ka.lds_mat_offset = (uint32_t)off;
         off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
+        ka.lds_mat_aux_offset = (uint32_t)off;
+        off = al16(off + (size_t)ctx->n_mat_dev * 16);
         ka.lds_obj_offset = (uint32_t)off;
         off = al16(off + (size_t)p.object_count * sizeof(RtObject));
         ka.lds_orig_offset = (uint32_t)off;

@@ -185,6 +185,7 @@ struct KernelArgs {
     uint32_t sched_bits;      // cost-ordered schedule: launch parity
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;
+    uint32_t lds_mat_aux_offset;  // per material float4 {1/ior, r0 front face, r0 back face, roughness/10} (modes 1, 2)
     uint32_t lds_obj_offset;
     uint32_t lds_orig_offset;
     uint32_t lds_smat_offset;
