@@ -666,3 +666,55 @@ def test_gpu_overlapped_batches_with_updates(gpu, oracle_lib, monkeypatch, overl
     finally:
         scene.materials["emission_power"][1] = base_e
     assert np.array_equal(got[1], out_o) and np.array_equal(got[0].view(np.uint32), acc_o.view(np.uint32))
+
+
+def _fuzz_scene(seed, w, h, with_tris):
+    """A random scene that leans on the culling: clustered and far spheres, tiny and huge
+    radii, duplicates and overlaps, every material kind, emitters; camera rays with exact
+    zero, denormal and axis-aligned components next to random ones."""
+    from rust_gpu_raytracing_amd.scene import RenderScene, _material, _sphere, solid_color_image
+    from rust_gpu_raytracing_amd.camera import Camera
+
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(5, 600))
+    pos = np.concatenate([rng.uniform(-8, 8, (n // 2, 3)),                          # a cluster
+                          rng.normal(0, 40, (n - n // 2, 3))]).astype(np.float32)   # far ones
+    rad = np.exp(rng.uniform(np.log(1e-3), np.log(3.0), n)).astype(np.float32)
+    pos[0], rad[0] = (0.0, 1000.5, 0.0), 1000.0                                      # a ground
+    if n > 8:
+        pos[1], rad[1] = pos[2], rad[2]                                               # a duplicate (tie)
+    n_mat = int(rng.integers(1, 12))
+    mats = np.stack([_material(int(rng.integers(0, 3)), float(rng.uniform(0, 1)),
+                               float(rng.choice([0.0, 0.0, 0.0, rng.uniform(0, 8)])),
+                               float(rng.uniform(0, 1)), float(rng.uniform(0, 1)),
+                               float(rng.choice([0.0, 1.0, rng.uniform(0, 1)])),
+                               float(rng.uniform(1.0, 2.4))) for _ in range(n_mat)])
+    spheres = np.stack([_sphere(pos[i], rad[i], int(rng.integers(0, n_mat))) for i in range(n)])
+    tex = np.stack([solid_color_image(rng.uniform(0, 1, 3), (1, 1)) for _ in range(3)])
+    env = np.ascontiguousarray((rng.uniform(0, 255, (16, 32, 4))).astype(np.uint8))
+    objects = []
+    if with_tris:
+        hf, _ = build_config("c5_heightfield", width=w, height=h, nx=24, nz=12, seed=int(seed))
+        objects = hf.objects
+    cam = Camera(w, h, position=np.array(rng.uniform(-15, 15, 3), np.float32))
+    scene = RenderScene(spheres.astype(B.SPHERE), mats.astype(B.MATERIAL), objects, tex, env, cam, name="fuzz")
+    d = rng.normal(0, 1, (w * h, 3)).astype(np.float32)
+    k = w * h // 8
+    d[:k, int(seed) % 3] = 0.0                    # exact zero components
+    d[k:2 * k, :2] = 0.0                          # axis-aligned
+    d[2 * k:3 * k, 1] = np.float32(1e-40)         # denormal component
+    rays = np.zeros(w * h, B.RAY)
+    rays["direction"] = d
+    return scene, rays
+
+
+@pytest.mark.parametrize("seed,with_tris", [(s, False) for s in range(1, 25)] + [(s, True) for s in range(25, 35)])
+def test_gpu_fuzz_scenes(gpu, oracle_lib, seed, with_tris):
+    """Random scenes (see _fuzz_scene) rendered for 2 accumulated frames of 6 bounces:
+    accumulation, output and ray count bit-identical to the oracle. Exercises the
+    culling margins and the sphere-only kernels' v_rcp_f32 1/d on inputs no config has."""
+    w, h = 48, 32
+    scene, rays = _fuzz_scene(seed, w, h, with_tris)
+    acc_o, out_o, rays_o = oracle_frames(oracle_lib, scene, 6, 2, rays)
+    acc, out, n = gpu_render(scene, 6, 2, rays=rays)
+    assert_same(acc, out, n, acc_o, out_o, rays_o)
