@@ -50,7 +50,7 @@ struct SceneView {
     const uint32_t* sph_mat;  // per original index: material index
     const float4* nodes;      // sphere BVH, 2 float4 per node (sphere_bvh.h)
     const RtMaterial* mat;    // LDS
-    const float4* mat_aux;    // LDS (modes 1, 2): per material {1/ior, r0 front, r0 back, roughness/10}
+    const float4* mat_aux;    // LDS (modes 1, 2): per material {1/ior, r0 front, r0 back, roughness/10}, 1x1 texel
     const RtObject* obj;      // LDS
     const float* srgb;        // LDS, 256 entries
     const float4* tri_nodes;  // triangle accelerator nodes (LDS in mode 2, else global)
@@ -587,14 +587,24 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
     }
     const uint32_t mi = min(h.material_index, ka.material_count - 1u);
     const RtMaterial m = sv.mat[mi];
-    // the texel load is issued first so that its latency overlaps the draws
-    const uint32_t texel = fetch_texture(ka, m.texture_index, h.u, h.v);
+    // 1x1 texture layers: every uv fetches texel (0, 0) of the material's layer,
+    // decoded once per workgroup into the material table (kAux); otherwise the
+    // texel load is issued first so that its latency overlaps the draws
+    const bool tex1 = kAux && ka.tex_w == 1u && ka.tex_h == 1u;
+    uint32_t texel = 0;
+    if (!tex1) texel = fetch_texture(ka, m.texture_index, h.u, h.v);
     const float gx = normal01(p.seed);
     const float gy = normal01(p.seed);
     const float gz = normal01(p.seed);
     const f3 diffuse = normalize(h.n + mk(gx, gy, gz));
     const f3 specular = p.d - h.n * (2.0f * dot(h.n, p.d));  // reflect(d, n)
-    const f4 color = decode_texel(texel, sv.srgb);
+    f4 color;
+    if (tex1) {
+        const float4 c = sv.mat_aux[2u * mi + 1u];
+        color = f4{c.x, c.y, c.z, c.w};
+    } else {
+        color = decode_texel(texel, sv.srgb);
+    }
     const float e = m.emission_power;
     p.light.x = p.light.x + (color.x * e) * p.contrib.x;
     p.light.y = p.light.y + (color.y * e) * p.contrib.y;
@@ -605,7 +615,7 @@ __device__ __forceinline__ bool shade(const SceneView& sv, const KernelArgs& ka,
     if (is_glass) {
         float ior, r0, rough10;
         if constexpr (kAux) {
-            const float4 ax = sv.mat_aux[mi];
+            const float4 ax = sv.mat_aux[2u * mi];
             ior = h.front_face ? ax.x : m.refraction_index;
             r0 = h.front_face ? ax.y : ax.z;
             rough10 = ax.w;
@@ -931,7 +941,10 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             float r0b = (1.0f - m.refraction_index) / (1.0f + m.refraction_index);
             r0f = r0f * r0f;
             r0b = r0b * r0b;
-            l_aux[i] = make_float4(ior_front, r0f, r0b, div_const(m.roughness, 10.0f, kInv10));
+            l_aux[2u * i] = make_float4(ior_front, r0f, r0b, div_const(m.roughness, 10.0f, kInv10));
+            // the decoded texel a 1x1 texture layer gives every hit (sample_texture, :26-32)
+            const f4 c = decode_texel(ka.textures[min(m.texture_index, ka.tex_layers - 1u)], ka.srgb);
+            l_aux[2u * i + 1u] = make_float4(c.x, c.y, c.z, c.w);
         }
         sv.mat_aux = l_aux;
         if constexpr (kTris)

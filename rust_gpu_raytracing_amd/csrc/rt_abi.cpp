@@ -1029,7 +1029,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.lds_mat_offset = (uint32_t)off;
         off = al16(off + (size_t)ctx->n_mat_dev * sizeof(RtMaterial));
         ka.lds_mat_aux_offset = (uint32_t)off;
-        off = al16(off + (size_t)ctx->n_mat_dev * 16);
+        off = al16(off + (size_t)ctx->n_mat_dev * 32);
         ka.lds_obj_offset = (uint32_t)off;
         off = al16(off + (size_t)p.object_count * sizeof(RtObject));
         ka.lds_orig_offset = (uint32_t)off;

@@ -185,7 +185,8 @@ struct KernelArgs {
     uint32_t sched_bits;      // cost-ordered schedule: launch parity
     // dynamic LDS carve-up (byte offsets)
     uint32_t lds_mat_offset;
-    uint32_t lds_mat_aux_offset;  // per material float4 {1/ior, r0 front face, r0 back face, roughness/10} (modes 1, 2)
+    uint32_t lds_mat_aux_offset;  // per material 2 float4: {1/ior, r0 front face, r0 back face, roughness/10},
+                                  // the decoded texel of a 1x1 texture layer (modes 1, 2)
     uint32_t lds_obj_offset;
     uint32_t lds_orig_offset;
     uint32_t lds_smat_offset;
