@@ -159,6 +159,8 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=None)
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="after the warmup steps, keep rendering untimed frames for this long (GPU clock ramp)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-sample-world", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -229,6 +231,26 @@ def main() -> int:
             from rust_gpu_raytracing_amd.distributed import gather_accumulation
         for _ in range(args.warmup):
             r.compute_frame(bounces)
+        # Clock settle: the GPU's power management raises its clocks only after tens of
+        # ms of sustained load (a 20-frame C2 launch: 6.2 ms right after a 5-frame
+        # warmup, 5.75 ms from the fourth launch on, 6.2 ms again after a 100 ms idle
+        # gap; DESIGN.md §6, profiles/r02_s4d). A display loop renders continuously, so
+        # the steady rate is the one to time: after the W warmup steps, more untimed
+        # frames until --settle-ms of wall time have passed (on every rank alike).
+        settle_frames = 0
+        r.synchronize()
+        t_settle = time.perf_counter()
+        while args.settle_ms > 0:
+            go = torch.tensor([1.0 if (time.perf_counter() - t_settle) * 1e3 < args.settle_ms else 0.0],
+                              device="cuda" if backend == "nccl" else "cpu")
+            if world > 1:
+                dist.all_reduce(go, op=dist.ReduceOp.MIN)
+            if go.item() == 0.0:
+                break
+            for _ in range(frame_batch):
+                r.compute_frame(bounces)
+            settle_frames += frame_batch
+            r.synchronize()
         if gathered:
             # one untimed readback: allocates the gather's buffers and lets RCCL set up its
             # peer connections (made lazily on a pair's first transfer), as any display
@@ -262,6 +284,7 @@ def main() -> int:
             t_gather = time.perf_counter() - t1
         t_render = t_total - t_gather
         res = dict(r=r, scene=scene, bounces=bounces, width=width, height=height, rays=r.ray_count(),
+                   settle_frames=settle_frames,
                    t_render=t_render, t_gather=t_gather, gathered=gathered, launch=r.launch_config(),
                    timing=r.dispatch_time_total(), owned_px=r.owned_pixel_count())
         stats = torch.tensor([t_total, t_render, t_gather, float(res["rays"])], dtype=torch.float64,
@@ -281,7 +304,7 @@ def main() -> int:
     if main_run["gathered"] and os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
         # the assembled tile-split image must equal a 1-GPU render of the same frames
         with Renderer(main_run["scene"], device=device) as ref:
-            for _ in range(args.warmup + args.steps):
+            for _ in range(args.warmup + main_run["settle_frames"] + args.steps):
                 ref.compute_frame(main_run["bounces"])
             same = np.array_equal(ref.read_accumulation().view(np.uint32), r.read_accumulation().view(np.uint32))
             same = same and np.array_equal(ref.read_output(), r.read_output())
@@ -322,6 +345,8 @@ def main() -> int:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"ms": args.settle_ms, "frames": m["settle_frames"],
+                       "note": "untimed frames after the warmup steps until the GPU clocks settle (DESIGN.md §6)"},
             "ms_per_step": m["t_total_max"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": args.scaling if world > 1 else "strong",

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    ap.add_argument("--settle-ms", type=float, default=150.0, help="as bench.py --settle-ms")
     ap.add_argument("--cpu-sample-world", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kw", default="{}", help="JSON builder kwargs applied to every config, e.g. '{\"env_size\": [1024, 512]}'")
@@ -54,6 +55,11 @@ def main():
             for _ in range(args.warmup):
                 r.compute_frame(bounces)
             r.synchronize()
+            t_settle = time.perf_counter()  # as bench.py: untimed frames until the clocks settle
+            while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+                for _ in range(fb):
+                    r.compute_frame(bounces)
+                r.synchronize()
             r.reset_ray_count()
             r.reset_timing()
             r.set_timing(True)

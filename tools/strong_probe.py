@@ -10,7 +10,7 @@ ranks' rays / the slowest rank's time, as bench.py computes `value`), and the
 predicted parallel efficiency against N=1 without and with a measured estimate
 of the gather (pack + the bytes rank 0 receives, priced at --link-gbs).
 
-usage: python tools/strong_probe.py [--steps 20] [--warmup 3] [--ns 1 2 4 8]
+usage: python tools/strong_probe.py [--steps 20] [--warmup 3] [--settle-ms 150] [--ns 1 2 4 8]
 """
 import argparse
 import json
@@ -25,13 +25,18 @@ from rust_gpu_raytracing_amd import Renderer  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
 
-def time_rank(scene, bounces, rank, world, steps, warmup, fb):
+def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms):
     import torch
 
     with Renderer(scene, rank=rank, world_size=world, frame_batch=fb) as r:
         for _ in range(warmup):
             r.compute_frame(bounces)
         r.synchronize()
+        t_settle = time.perf_counter()  # as bench.py: untimed frames until the clocks settle
+        while (time.perf_counter() - t_settle) * 1e3 < settle_ms:
+            for _ in range(fb):
+                r.compute_frame(bounces)
+            r.synchronize()
         r.reset_ray_count()
         r.reset_timing()
         r.set_timing(True)
@@ -61,6 +66,7 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--ns", type=int, nargs="*", default=[1, 2, 4, 8])
+    ap.add_argument("--settle-ms", type=float, default=150.0, help="as bench.py --settle-ms")
     ap.add_argument("--frame-batch", type=int, default=0, help="override bench.default_frame_batch(N)")
     ap.add_argument("--link-gbs", type=float, default=50.0,
                     help="xGMI bandwidth one peer achieves into rank 0 (GB/s, per link; 7 links)")
@@ -69,7 +75,7 @@ def main():
     base = None
     for n in args.ns:
         fb = args.frame_batch or bench.default_frame_batch(n, args.steps)
-        per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb) for r in range(n)]
+        per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms) for r in range(n)]
         t_max = max(p[0] for p in per)
         rays = sum(p[1] for p in per)
         # gather estimate: packs run in parallel (max), rank 0 receives N-1 blocks over N-1 links
