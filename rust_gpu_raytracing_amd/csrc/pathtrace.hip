@@ -28,7 +28,6 @@
 #include "rt_bvh_slab.h"
 #include "rt_device_math.h"
 #include "rt_kernel_args.h"
-#include "sphere_bvh.h"  // the pair layout's child codes
 
 #pragma clang fp contract(off)
 
@@ -219,8 +218,6 @@ __device__ __forceinline__ TriHit sweep_triangles(const SceneView& sv, const Ker
 // the triangle hit (a sphere wins only when strictly closer, :347).
 // Phase 2: done.
 constexpr uint32_t kNoLeaf = 0xffffffffu;
-constexpr int kSphereStackWords = (int)(kSphereStackDepth / 2);  // pair walk: 16-bit codes, two per register
-static_assert(kSphereStackDepth % 2 == 0, "stack words");
 
 struct TraceState {
     f3 inv;
@@ -234,7 +231,6 @@ struct TraceState {
     bool nan_hit;
     SphereHit sph;
     TriHit tri;
-    uint32_t stk[kSphereStackWords];  // pair walk: pending child codes, 16 bits each, top in stk[0]'s low half
 };
 
 // A sphere must be strictly closer than the best sphere so far and than the
@@ -260,9 +256,7 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
     }
     ts.slab = slab_ray(o.x, o.y, o.z, ts.inv.x, ts.inv.y, ts.inv.z, m);
     ts.limit = phase == 0 ? __builtin_inff() : prune_limit(ts);
-    if (phase == 1 && ka.sphere_pairs) {
-        ts.node = 0;  // pair 0: the root's children
-    } else if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
+    if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
                              ((__float_as_uint(ts.inv.z) >> 31) << 2);
         ts.node = oct * ka.sphere_octant_stride;
@@ -289,8 +283,6 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
     ts.nan_hit = false;
     ts.node = 0;
     ts.pending = kNoLeaf;
-#pragma unroll
-    for (int k = 0; k < kSphereStackWords; ++k) ts.stk[k] = 0xffffffffu;
     // brute-force sphere set: wave-uniform sweep over groups of 4, then the rest
     // one by one (a sphere's own test is exact, so the visiting order is free)
     // (the slots after the set up to the next group boundary are NaN padding:
@@ -365,8 +357,6 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
         ts.node = 0;
         ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
         phase_setup(sv, ka, o, ts.a2 * 0.5f, 1, ts);
-    } else if (!kTris && ka.sphere_pairs) {
-        if (ts.node == kNoLeaf && (ts.stk[0] & 0xffffu) == kPairNone) ts.phase = 2;
     } else if (ts.node >= ka.sphere_nodes) {
         ts.phase = 2;
     }
@@ -403,104 +393,8 @@ constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
 template <int kMode, bool kTris>
 constexpr bool kDrainDecouple = kTris && kMode < 2;
 
-// Sphere leaves of sphere-only scenes are tested one sphere per traversal step
-// (RT_SPHERE_STEP 1): a step is either a node test or one sphere test, and the
-// leaf's padding slots are never tested. Testing a group at once in the node
-// step made every step pay the whole group's disc and candidate code (some
-// lane of the wave sits on a leaf at almost every step) at a few active lanes.
-#ifndef RT_SPHERE_STEP
-#define RT_SPHERE_STEP 1
-#endif
-
-// One sphere of the leaf a lane is working through: ts.pending = slot | spheres
-// left after it << 24 (sphere_bvh.h: leaf = first_slot | count << 24).
-__device__ __forceinline__ void sphere_step(const SceneView& sv, f3 o, f3 d, TraceState& ts) {
-    const uint32_t slot = ts.pending & 0xffffffu;
-    float b;
-    const float disc = sphere_disc(sv.sph[slot], o, d, ts.a4, b);
-    if (disc >= 0.0f) {
-        const float t = (-b - sqrt_rn_any(disc)) / ts.a2;
-        if (t > 0.0f && t <= ts.sph.t) {
-            const uint32_t orig = sv.orig[slot];
-            if (t < ts.sph.t || orig < ts.sph.orig) {
-                ts.sph.t = t;
-                ts.sph.orig = orig;
-                ts.sph.slot = slot;
-                ts.limit = prune_limit(ts);
-            }
-        }
-    }
-    ts.pending = ts.pending >= (1u << 24) ? ts.pending + 1u - (1u << 24) : kNoLeaf;
-}
-
-// The child-pair walk (sphere-only scenes, sphere_bvh.h build_sphere_pairs).
-// One step is either one sphere of the current leaf (sphere_step) or one pair
-// node: both children's inflated boxes are tested (two independent slab tests),
-// the walk descends into the hit child with the nearer entry and pushes the
-// other; with no child hit it pops the stack. Culling and pruning are the
-// skip-link walk's (same margins, slack and limit): the visiting order differs,
-// the set of spheres that can win does not.
-__device__ __forceinline__ void stack_push(TraceState& ts, uint32_t code) {
-#pragma unroll
-    for (int k = kSphereStackWords - 1; k > 0; --k) ts.stk[k] = __builtin_amdgcn_alignbit(ts.stk[k], ts.stk[k - 1], 16);
-    ts.stk[0] = (ts.stk[0] << 16) | code;
-}
-__device__ __forceinline__ uint32_t stack_pop(TraceState& ts) {
-    const uint32_t code = ts.stk[0] & 0xffffu;
-#pragma unroll
-    for (int k = 0; k < kSphereStackWords - 1; ++k) ts.stk[k] = __builtin_amdgcn_alignbit(ts.stk[k + 1], ts.stk[k], 16);
-    ts.stk[kSphereStackWords - 1] = (ts.stk[kSphereStackWords - 1] >> 16) | 0xffff0000u;
-    return code;
-}
-// A child code reached by the walk: an internal child becomes the next node, a
-// leaf the sphere run of the next steps (slot | spheres left after it << 24).
-__device__ __forceinline__ void pair_enter(TraceState& ts, uint32_t code) {
-    if (code & kPairLeaf) {
-        ts.pending = (code & 0x7ffcu) | ((code & 3u) << 24);
-        ts.node = kNoLeaf;
-    } else {
-        ts.node = code;
-    }
-}
-__device__ __forceinline__ void pair_step(const SceneView& sv, f3 o, f3 d, TraceState& ts) {
-    if (ts.pending == kNoLeaf && ts.node == kNoLeaf) pair_enter(ts, stack_pop(ts));  // non-empty: phase_end
-    if (ts.pending != kNoLeaf) {
-        sphere_step(sv, o, d, ts);
-        return;
-    }
-    const float4* nd = sv.nodes + 4u * ts.node;
-    const float4 lo0 = nd[0], hi0 = nd[1], lo1 = nd[2], hi1 = nd[3];
-    float n0, f0, n1, f1;
-    slab_hit(ts.slab, lo0.x, lo0.y, lo0.z, hi0.x, hi0.y, hi0.z, n0, f0);
-    slab_hit(ts.slab, lo1.x, lo1.y, lo1.z, hi1.x, hi1.y, hi1.z, n1, f1);
-    const bool h0 = n0 <= f0 && f0 >= -ts.slack && n0 <= ts.limit;
-    const bool h1 = n1 <= f1 && f1 >= -ts.slack && n1 <= ts.limit;
-    const uint32_t c0 = __float_as_uint(lo0.w), c1 = __float_as_uint(lo1.w);
-    if (h0 && h1) {
-        const bool second_first = n1 < n0;
-        stack_push(ts, second_first ? c0 : c1);
-        pair_enter(ts, second_first ? c1 : c0);
-    } else if (h0 || h1) {
-        pair_enter(ts, h0 ? c0 : c1);
-    } else {
-        ts.node = kNoLeaf;
-    }
-}
-
 template <bool kTris>
 __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
-    if constexpr (!kTris && kSpherePairsKernel) {
-        if (ka.sphere_pairs) {
-            pair_step(sv, o, d, ts);
-            return;
-        }
-    }
-    if constexpr (!kDeferLeaves<kTris> && RT_SPHERE_STEP) {
-        if (ts.pending != kNoLeaf) {
-            sphere_step(sv, o, d, ts);
-            return;
-        }
-    }
     const bool tri = kTris && ts.phase == 0;
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
@@ -516,9 +410,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     const bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
     const uint32_t leaf = __float_as_uint(hi.w);
     const bool at_leaf = hit && leaf != 0xffffffffu;
-    if (at_leaf && !kDeferLeaves<kTris> && RT_SPHERE_STEP) {
-        ts.pending = leaf - (1u << 24);  // its spheres, one per step from the next step on
-    } else if (at_leaf && !kDeferLeaves<kTris>) {
+    if (at_leaf && !kDeferLeaves<kTris>) {
         test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
         ts.limit = prune_limit(ts);
     } else if (at_leaf) {
@@ -1038,8 +930,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             l_orig[i] = ka.sphere_orig[i];
         }
         for (uint32_t i = tid; i < ka.sphere_count; i += kThreads) l_smat[i] = ka.sphere_material[i];
-        const uint32_t node_f4 = (ka.sphere_pairs ? 4u : 2u) * ka.sphere_nodes;  // pair / skip-link nodes
-        for (uint32_t i = tid; i < node_f4; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
+        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
         float4* l_aux = reinterpret_cast<float4*>(lds + ka.lds_mat_aux_offset);
         for (uint32_t i = tid; i < ka.material_count; i += kThreads) {
             const RtMaterial m = ka.materials[i];

@@ -184,15 +184,11 @@ struct rt_ctx {
     uint32_t* d_slot_orig = nullptr;
     uint32_t* d_sph_mat = nullptr;       // by original index
     SphereBvhNode* d_bvh = nullptr;
-    SpherePairNode* d_pairs = nullptr;   // child-pair layout of the sphere BVH (sphere-only kernels)
     std::vector<rt_scene_sphere> h_sph;  // host copy: the BVH is rebuilt from it
     bool slots_dirty = true;
     uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
     bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
     bool sphere_octants = true;          // RT_SPHERE_OCTANTS=0: one BVH layout (A/B switch)
-    bool sphere_pairs = true;            // RT_SPHERE_PAIRS=0: sphere-only kernels walk the skip-link layouts (A/B switch)
-    bool pairs_ok = false;               // the pair layout was built (16-bit codes, depth <= kSphereStackDepth)
-    uint32_t n_pairs = 0;
     uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
     uint32_t n_always = 0, n_nodes = 0, n_slots = 0;
     float sphere_extent = 0.0f;
@@ -357,17 +353,12 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     for (uint32_t i = 0; i < count; i++) mat[i] = ctx->h_sph[i].material_index;
     std::vector<SphereBvhNode> oct;  // 8 direction-ordered copies; layout 0 alone is a complete walk too
     order_bvh_by_octant(sl.nodes, &oct);
-    std::vector<SpherePairNode> pairs;
-    uint32_t depth = 0;
-    ctx->pairs_ok = build_sphere_pairs(sl.nodes, kSphereStackDepth, &pairs, &depth) && !pairs.empty();
     int rc;
     if ((rc = upload_raw(ctx, ctx->d_slot_sph, sl.slot_sph.data(), sl.slot_sph.size() * 4)) ||
         (rc = upload_raw(ctx, ctx->d_slot_orig, sl.slot_orig.data(), sl.slot_orig.size() * 4)) ||
         (rc = upload_raw(ctx, ctx->d_sph_mat, mat.data(), mat.size() * 4)) ||
-        (rc = upload_raw(ctx, ctx->d_bvh, oct.data(), oct.size() * sizeof(SphereBvhNode))) ||
-        (rc = upload_raw(ctx, ctx->d_pairs, pairs.data(), pairs.size() * sizeof(SpherePairNode))))
+        (rc = upload_raw(ctx, ctx->d_bvh, oct.data(), oct.size() * sizeof(SphereBvhNode))))
         return rc;
-    ctx->n_pairs = (uint32_t)pairs.size();
     ctx->n_always = sl.n_always;
     ctx->n_slots = (uint32_t)sl.slot_orig.size();
     ctx->n_nodes = (uint32_t)sl.nodes.size();
@@ -618,8 +609,6 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->use_bvh = !(env && env[0] == '0');
         env = std::getenv("RT_SPHERE_OCTANTS");
         ctx->sphere_octants = !(env && env[0] == '0');
-        env = std::getenv("RT_SPHERE_PAIRS");
-        ctx->sphere_pairs = !(env && env[0] == '0');
         env = std::getenv("RT_QUEUE_STRIPES");
         if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TRAV_THRESHOLD");
@@ -671,7 +660,6 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
         (rc = dev_alloc(ctx, &ctx->d_sph_mat, info->sphere_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_bvh, 16 * (size_t)info->sphere_count + 8)) ||  // 8 ordered layouts
-        (rc = dev_alloc(ctx, &ctx->d_pairs, (size_t)info->sphere_count + 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
         (rc = dev_alloc(ctx, &ctx->d_tri_bounds, 2 * (size_t)ctx->n_tri_dev)) ||
@@ -706,7 +694,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
     void* bufs[] = {ctx->d_rays, ctx->d_accum, ctx->d_out, ctx->d_counter, ctx->d_queue, ctx->d_slot_sph,
-                    ctx->d_slot_orig, ctx->d_bvh, ctx->d_pairs, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
+                    ctx->d_slot_orig, ctx->d_bvh, ctx->d_sph_mat, ctx->d_tri_bvh, ctx->d_tri_prims,
                     ctx->d_mat,  ctx->d_obj,   ctx->d_sub, ctx->d_tri,     ctx->d_tex,     ctx->d_env,
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
@@ -1034,11 +1022,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
     const bool tris = p.object_count != 0;  // else the sphere-only kernels
-    // Sphere-only kernels walk the child-pair layout with a traversal stack
-    // (build_sphere_pairs) when it was built; otherwise the skip-link layouts.
-    const bool pairs = kSpherePairsKernel && !tris && ctx->sphere_pairs && ctx->pairs_ok && ctx->n_nodes != 0;
-    ka.sphere_pairs = pairs ? 1u : 0u;
-    if (pairs) ka.sphere_bvh = reinterpret_cast<const float4*>(ctx->d_pairs);
     size_t mode1_bytes = 0, mode2_bytes = 0;
     // lays out the LDS image for `layouts` sphere BVH layouts and returns the LDS mode it fits
     auto carve = [&](uint32_t layouts, size_t mode1_budget) -> int {
@@ -1054,8 +1037,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.lds_smat_offset = (uint32_t)off;
         off = al16(off + (size_t)p.sphere_count * 4);
         ka.lds_nodes_offset = (uint32_t)off;
-        off = al16(off + (pairs ? (size_t)ctx->n_pairs * sizeof(SpherePairNode)
-                                : (size_t)layouts * ctx->n_nodes * sizeof(SphereBvhNode)));
+        off = al16(off + (size_t)layouts * ctx->n_nodes * sizeof(SphereBvhNode));
         mode1_bytes = off + kLdsTailBytes;
         ka.lds_tri_nodes_offset = (uint32_t)off;
         off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
@@ -1072,13 +1054,13 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // larger workgroups); otherwise layout 0 alone.
     int mode = carve(1, kLdsSceneBudget);
     uint32_t layouts = 1;
-    if (ctx->sphere_octants && ctx->n_nodes != 0 && !pairs) {
+    if (ctx->sphere_octants && ctx->n_nodes != 0) {
         if (carve(8, kLdsAccelBudget) == mode)
             layouts = 8;
         else
             carve(1, kLdsSceneBudget);
     }
-    ka.sphere_nodes = pairs ? ctx->n_pairs : layouts * ctx->n_nodes;
+    ka.sphere_nodes = layouts * ctx->n_nodes;
     ka.sphere_octant_stride = layouts == 8 ? ctx->n_nodes : 0u;
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
     ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);

@@ -92,14 +92,6 @@ constexpr uint32_t kOrderBuckets = RT_ORDER_BUCKETS;
 constexpr size_t kLdsTailBytes = 1024 + 160;
 static_assert(kLdsTailBytes >= (kOrderBuckets * 16 + 1) * 4, "sort scratch fits the LDS tail");
 
-// Sphere-only kernels walk the child-pair BVH layout (sphere_bvh.h,
-// build_sphere_pairs) with a per-lane stack of kSphereStackDepth 16-bit child
-// codes (the host falls back to the skip-link walk for deeper trees).
-#ifndef RT_SPHERE_PAIRS
-#define RT_SPHERE_PAIRS 1
-#endif
-constexpr bool kSpherePairsKernel = RT_SPHERE_PAIRS != 0;
-
 struct KernelArgs {
     // framebuffer (bindings 1, 2, 6)
     const float4* __restrict__ camera_rays;
@@ -148,7 +140,6 @@ struct KernelArgs {
     uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     uint32_t sphere_octant_stride;  // nodes per direction-ordered layout (0: one layout, order_bvh_by_octant)
-    uint32_t sphere_pairs;    // 1: sphere_bvh holds SpherePairNode[sphere_nodes] (stack walk, sphere-only kernels)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
     float sphere_rmin, sphere_rmax;  // radius range over BVH spheres (culling bounds, rt_bvh_slab.h)
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)

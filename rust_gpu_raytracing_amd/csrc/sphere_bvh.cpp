@@ -214,70 +214,6 @@ void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<Spher
     }
 }
 
-bool build_sphere_pairs(const std::vector<SphereBvhNode>& nodes, uint32_t max_depth,
-                        std::vector<SpherePairNode>* out, uint32_t* depth_out) {
-    out->clear();
-    *depth_out = 0;
-    const uint32_t n = (uint32_t)nodes.size();
-    if (n == 0) return true;
-    // pair index of each internal node (pre-order rank among internal nodes)
-    std::vector<uint32_t> pair_of(n, kPairNone);
-    uint32_t n_pairs = 0;
-    for (uint32_t i = 0; i < n; i++)
-        if (nodes[i].leaf == kSphereBvhInternal) pair_of[i] = n_pairs++;
-    if (n_pairs >= kPairLeaf) return false;
-    bool ok = true;
-    auto ref_of = [&](uint32_t i) -> uint32_t {
-        if (nodes[i].leaf == kSphereBvhInternal) return pair_of[i];
-        const uint32_t slot = nodes[i].leaf & 0xffffffu, cnt = nodes[i].leaf >> 24;
-        if (slot % kSphereGroup != 0 || cnt == 0 || cnt > kSphereGroup || slot + kSphereGroup >= kPairLeaf - 4) {
-            ok = false;
-            return kPairNone;
-        }
-        return kPairLeaf | slot | (cnt - 1);
-    };
-    auto set_child = [&](SpherePairNode& p, int k, uint32_t i) {
-        float* lo = k ? p.lo1 : p.lo0;
-        float* hi = k ? p.hi1 : p.hi0;
-        for (int a = 0; a < 3; a++) {
-            lo[a] = nodes[i].bmin[a];
-            hi[a] = nodes[i].bmax[a];
-        }
-        (k ? p.ref1 : p.ref0) = ref_of(i);
-    };
-    if (n_pairs == 0) {  // the root is a leaf: one pair, second child empty
-        SpherePairNode p{};
-        set_child(p, 0, 0);
-        for (int a = 0; a < 3; a++) {
-            p.lo1[a] = INFINITY;
-            p.hi1[a] = -INFINITY;
-        }
-        p.ref1 = kPairNone;
-        out->push_back(p);
-        *depth_out = 1;
-        return ok;
-    }
-    out->resize(n_pairs);
-    std::vector<uint32_t> depth(n, 0);  // internal nodes on the path from the root, this one included
-    uint32_t max_d = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        if (nodes[i].leaf != kSphereBvhInternal) continue;
-        const uint32_t a = i + 1, b = nodes[i + 1].skip;  // left child, right child (pre-order)
-        depth[i] += 1;
-        max_d = std::max(max_d, depth[i]);
-        depth[a] = depth[b] = depth[i];
-        SpherePairNode& p = (*out)[pair_of[i]];
-        set_child(p, 0, a);
-        set_child(p, 1, b);
-    }
-    *depth_out = max_d;
-    if (!ok || max_d > max_depth) {
-        out->clear();
-        return false;
-    }
-    return true;
-}
-
 void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, const rt_sub_object_info* subs,
                           uint32_t sub_count, TriangleAccel* out) {
     out->prims.clear();
@@ -398,7 +334,7 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
         const uint32_t slot = (uint32_t)out->slot_orig.size();
         for (uint32_t k = 0; k < cnt; k++) push_slot(b.leaf_order[first + k]);
         pad_group();
-        nd.leaf = slot | (cnt << 24);  // the kernel's sphere steps test the cnt real slots
+        nd.leaf = slot | (kSphereGroup << 24);
     }
     out->extent = std::nextafter((float)extent, INFINITY);
     // radii are f32 already: r_min is exact, r_max too (kept as the float value)

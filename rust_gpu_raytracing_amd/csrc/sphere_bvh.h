@@ -61,39 +61,6 @@ void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use
 // (the lexicographic minimum, conservative pruning).
 void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out);
 
-// Child-pair layout of the same BVH for stack-based traversal: one 64-byte
-// record per internal node holding both children's boxes, so one step tests
-// both children (two independent slab tests) and descends into the nearer hit,
-// pushing the other. A walk then takes one step per internal node entered
-// instead of one per node tested. Child references are 16-bit codes (the
-// kernel's traversal stack packs two per register): an internal child is its
-// pair index (< 0x8000), a leaf is kPairLeaf | first_slot | (count - 1) (slots
-// are group-aligned, so the low two bits are free). Pair 0 is the root's
-// children; a one-leaf tree gets one pair whose second child is an empty box.
-struct SpherePairNode {
-    float lo0[3];
-    uint32_t ref0;
-    float hi0[3];
-    uint32_t _pad0;
-    float lo1[3];
-    uint32_t ref1;
-    float hi1[3];
-    uint32_t _pad1;
-};
-static_assert(sizeof(SpherePairNode) == 64, "pair node layout");
-constexpr uint32_t kPairLeaf = 0x8000u;
-constexpr uint32_t kPairNone = 0xffffu;  // an empty child (never hit) / empty stack entry
-// Entries of the kernel's pair-walk stack (two per register): the deepest
-// root-to-leaf path a pair layout may have, in internal nodes.
-constexpr uint32_t kSphereStackDepth = 12;
-
-// Builds the pair layout of a depth-first BVH (build_sphere_slots' nodes, leaf =
-// slot | count << 24). Returns false -- and leaves *out empty -- when the codes
-// do not fit 16 bits or the tree has more than `max_depth` internal nodes on a
-// root-to-leaf path (the kernel's stack holds max_depth entries).
-bool build_sphere_pairs(const std::vector<SphereBvhNode>& nodes, uint32_t max_depth,
-                        std::vector<SpherePairNode>* out, uint32_t* depth_out);
-
 // Generic builder: binned-SAH BVH over axis-aligned boxes (lo/hi, 3 floats each
 // per primitive), leaves of at most `leaf_max` primitives. Returns depth-first
 // nodes (same layout as SphereBvhNode; leaf = first | count << 24 indexing

@@ -160,87 +160,6 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
     return {bt, found ? (int)bo : -1};
 }
 
-// The kernel's child-pair walk (pathtrace.hip pair_step, sphere_bvh.h
-// build_sphere_pairs): both children tested per step, nearer hit entered, the
-// other pushed on a stack of kSphereStackDepth 16-bit codes; leaves' spheres
-// one at a time. g_nodes counts pair steps.
-static std::vector<SpherePairNode> g_pairs;
-static const SphereSlots* g_pairs_of = nullptr;
-
-static Res pair_like(const SphereSlots& sl, V o, V d) {
-    float bt = F32_MAX_;
-    uint32_t bo = 0;
-    bool found = false;
-    float a = dot(d, d), four_a = 4.0f * a, two_a = 2.0f * a;
-    for (uint32_t i = 0; i < sl.n_always; i++) cand(sl, i, o, d, four_a, two_a, bt, bo, found);
-    if (sl.nodes.empty()) return {bt, found ? (int)bo : -1};
-    if (g_pairs_of != &sl) {
-        uint32_t depth = 0;
-        if (!build_sphere_pairs(sl.nodes, kSphereStackDepth, &g_pairs, &depth)) {
-            printf("pair layout not built (depth %u)\n", depth);
-            exit(2);
-        }
-        g_pairs_of = &sl;
-    }
-    float lateral, slack;
-    sphere_cull_bounds(std::sqrt(dot(o, o)), sl.extent, sl.r_min, sl.r_max, 1.0f / std::sqrt(a), lateral, slack);
-    if (getenv("LAT_SCALE")) lateral *= (float)atof(getenv("LAT_SCALE"));
-    if (getenv("SLACK_SCALE")) slack *= (float)atof(getenv("SLACK_SCALE"));
-    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    if (getenv("INV_ULP")) {
-        static uint32_t h = 0x9e3779b9u;
-        auto nudge = [&](float v) {
-            h = h * 747796405u + 2891336453u;
-            return std::isfinite(v) ? std::nextafter(v, (h >> 31) ? INFINITY : -INFINITY) : v;
-        };
-        inv = {nudge(inv.x), nudge(inv.y), nudge(inv.z)};
-    }
-    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);
-    uint32_t stack[kSphereStackDepth];
-    uint32_t sp = 0, node = 0;
-    bool walking = true;
-    while (walking) {
-        g_nodes++;
-        const SpherePairNode& p = g_pairs[node];
-        const float lim = bt * 1.00001f + slack;
-        float n0, f0, n1, f1;
-        slab_hit(sr, p.lo0[0], p.lo0[1], p.lo0[2], p.hi0[0], p.hi0[1], p.hi0[2], n0, f0);
-        slab_hit(sr, p.lo1[0], p.lo1[1], p.lo1[2], p.hi1[0], p.hi1[1], p.hi1[2], n1, f1);
-        const bool h0 = n0 <= f0 && f0 >= -slack && n0 <= lim;
-        const bool h1 = n1 <= f1 && f1 >= -slack && n1 <= lim;
-        uint32_t next = kPairNone;
-        if (h0 && h1) {
-            const bool second_first = n1 < n0;
-            if (sp == kSphereStackDepth) { printf("stack overflow\n"); exit(2); }
-            stack[sp++] = second_first ? p.ref0 : p.ref1;
-            next = second_first ? p.ref1 : p.ref0;
-        } else if (h0 || h1) {
-            next = h0 ? p.ref0 : p.ref1;
-        }
-        for (;;) {  // leaves' spheres, then pops, until an internal node or the end
-            if (next == kPairNone) {
-                if (sp == 0) { walking = false; break; }
-                next = stack[--sp];
-            }
-            if (next & kPairLeaf) {
-                const uint32_t first = next & 0x7ffcu, cnt = (next & 3u) + 1;
-                for (uint32_t k = 0; k < cnt; k++) cand(sl, first + k, o, d, four_a, two_a, bt, bo, found);
-                next = kPairNone;
-                continue;
-            }
-            node = next;
-            break;
-        }
-    }
-    return {bt, found ? (int)bo : -1};
-}
-
-static Res walk(const SphereSlots& sl, V o, V d) {
-    if (getenv("ORDERED")) return ordered_like(sl, o, d);
-    if (getenv("SKIP_LINKS")) return kernel_like(sl, o, d);
-    return pair_like(sl, o, d);
-}
-
 static int replay(const char* rays_path, const char* sph_path) {
     FILE* f = fopen(sph_path, "rb");
     std::vector<rt_scene_sphere> s;
@@ -257,7 +176,7 @@ static int replay(const char* rays_path, const char* sph_path) {
     while (fread(q, sizeof(q), 1, f) == 1) {
         V o{q[0], q[1], q[2]}, d{q[3], q[4], q[5]};
         const long before = g_nodes;
-        Res a = brute(s, o, d), b = walk(sl, o, d);
+        Res a = brute(s, o, d), b = getenv("ORDERED") ? ordered_like(sl, o, d) : kernel_like(sl, o, d);
         visits.push_back((uint32_t)(g_nodes - before));
         uint32_t ta, tb;
         memcpy(&ta, &a.t, 4);
@@ -314,8 +233,7 @@ int main(int argc, char** argv) {
     // the kernel reads aligned groups of kSphereGroup slots: brute-force prefix and every leaf
     if (sl.slot_orig.size() % kSphereGroup) { printf("slot groups unaligned\n"); return 1; }
     for (const SphereBvhNode& nd : sl.nodes)
-        if (nd.leaf != kSphereBvhInternal &&
-            ((nd.leaf & 0xffffffu) % kSphereGroup || (nd.leaf >> 24) == 0 || (nd.leaf >> 24) > kSphereGroup)) {
+        if (nd.leaf != kSphereBvhInternal && ((nd.leaf & 0xffffffu) % kSphereGroup || (nd.leaf >> 24) != kSphereGroup)) {
             printf("leaf group unaligned\n");
             return 1;
         }
@@ -347,7 +265,7 @@ int main(int argc, char** argv) {
         }
         float scale = 0.5f + 2.0f * U(rng);  // non-unit directions (jitter breaks unit length, :219)
         d = {d.x * scale, d.y * scale, d.z * scale};
-        Res a = brute(s, o, d), b = walk(sl, o, d);
+        Res a = brute(s, o, d), b = getenv("ORDERED") ? ordered_like(sl, o, d) : kernel_like(sl, o, d);
         uint32_t ta, tb;
         memcpy(&ta, &a.t, 4);
         memcpy(&tb, &b.t, 4);
