@@ -83,9 +83,11 @@ uint32_t trav_threshold_for(int lds_mode, bool tris) {
 }
 // Triangle scenes test deferred leaves once this many eighths of the
 // traversing lanes hold one (pathtrace.hip, leaf_step): later for an LDS
-// accelerator (C3: 7 beats 6 and 8), earlier when the leaf's loads go to global
-// memory anyway (C5: 6 is 4% faster than 7).
-uint32_t leaf_batch_for(int lds_mode) { return lds_mode == 2 ? 7 : 6; }
+// accelerator, earlier when the leaf's loads go to global memory anyway.
+// Re-measured with 20-frame launches (profiles/r02_s4/r02_s4k, r02_s4l):
+// mode 2 at 6 (C4 -2.3% against 7, C3 within 0.3%), modes 0/1 at 5 (C5 -2.9%
+// against 6; 4 and 3 within 0.4% of 5).
+uint32_t leaf_batch_for(int lds_mode) { return lds_mode == 2 ? 6 : 5; }
 // Instances with the triangle accelerator in global memory: the same once the
 // tile queue is empty, when the wave goes back to shading only if some lane
 // has finished and after at least kDefaultDrainMinSteps traversal steps

@@ -49,6 +49,7 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms):
         r.set_timing(False)
         span_ms, n_launch = r.dispatch_time_total()
         rays = r.ray_count()
+        launch = r.launch_config()
         # the device half of the gather: pack this rank's accumulation
         n = r.owned_pixel_count()
         buf = torch.empty((n, 4), dtype=torch.float32, device="cuda")
@@ -57,7 +58,7 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms):
         r.pack_owned_accumulation(buf.data_ptr())
         r.synchronize()
         t_pack = time.perf_counter() - p0
-    return t, rays, t_pack, n * 16, t_submit, span_ms, n_launch
+    return t, rays, t_pack, n * 16, t_submit, span_ms, n_launch, launch
 
 
 def main():
@@ -92,7 +93,7 @@ def main():
             "host_submit_ms_max": max(p[4] for p in per) * 1e3,
             "kernel_span_ms_per_rank": [round(p[5], 4) for p in per], "launches": per[0][6],
             "wall_ms_per_rank": [round(p[0] * 1e3, 4) for p in per],
-            "steps": args.steps,
+            "steps": args.steps, "launch": per[0][7],
         }), flush=True)
 
 
