@@ -334,6 +334,15 @@ RT_API int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t 
  * (Params.accumulate == 0 never writes the accumulation, compute_shader.wgsl:171-178). */
 RT_API int rt_pack_owned_output(rt_ctx* ctx, void* dst_device);
 RT_API int rt_unpack_output(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size);
+/* One launch for a whole gather: `src_device` holds world_size consecutive
+ * blocks of `stride_px` pixels (>= rank 0's rt_owned_pixel_count, the largest),
+ * block r packed by rank r; every block except skip_rank's (the destination's
+ * own tiles, already in place; pass world_size or more to unpack all) is
+ * unpacked as rt_unpack_accumulation / rt_unpack_output would. */
+RT_API int rt_unpack_accumulation_ranks(rt_ctx* ctx, const void* src_device, uint64_t stride_px,
+                                        uint32_t world_size, uint32_t skip_rank, uint32_t divisor);
+RT_API int rt_unpack_output_ranks(rt_ctx* ctx, const void* src_device, uint64_t stride_px, uint32_t world_size,
+                                  uint32_t skip_rank);
 
 /* Launch geometry of the last rt_dispatch (diagnostics): workgroup size in
  * threads, workgroups launched, dynamic LDS bytes per workgroup, and the LDS

@@ -1383,15 +1383,24 @@ extern "C" __global__ void __launch_bounds__(256) rt_pack_tiles_kernel(const flo
     dst[gid] = v;
 }
 
-extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(const float4* __restrict__ src,
-                                                                        float4* __restrict__ accum,
-                                                                        uint32_t* __restrict__ output, uint32_t width,
-                                                                        uint32_t height, uint32_t tiles_x,
-                                                                        uint32_t owned_tiles, uint32_t rank,
-                                                                        uint32_t world, float divisor) {
+// Unpack: blockIdx.y selects the source rank first_rank + blockIdx.y, whose
+// packed block starts at src + blockIdx.y * stride_px; skip_rank's block (the
+// destination's own tiles, already in place) is left out. One launch unpacks
+// every rank's block of a gather.
+__device__ __forceinline__ uint32_t owned_tiles_of(uint32_t n_tiles, uint32_t rank, uint32_t world) {
+    return rank < n_tiles ? (n_tiles - rank + world - 1u) / world : 0u;
+}
+
+extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(
+    const float4* __restrict__ src, float4* __restrict__ accum, uint32_t* __restrict__ output, uint32_t width,
+    uint32_t height, uint32_t tiles_x, uint32_t n_tiles, uint32_t first_rank, uint32_t world, uint64_t stride_px,
+    uint32_t skip_rank, float divisor) {
+    const uint32_t rank = first_rank + blockIdx.y;
+    if (rank == skip_rank) return;
+    src += (uint64_t)blockIdx.y * stride_px;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t local_tile = gid >> 6;
-    if (local_tile >= owned_tiles) return;
+    if (local_tile >= owned_tiles_of(n_tiles, rank, world)) return;
     const uint32_t lane = (uint32_t)(gid & 63u);
     const uint32_t tile = (uint32_t)local_tile * world + rank;
     const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u);
@@ -1448,14 +1457,17 @@ hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* ligh
 }
 
 // The packed RGBA8 output, one u32 per pixel, both ways (non-accumulating renders).
-extern "C" __global__ void __launch_bounds__(256) rt_pack_output_kernel(const uint32_t* __restrict__ output,
-                                                                       uint32_t* __restrict__ dst, uint32_t width,
-                                                                       uint32_t height, uint32_t tiles_x,
-                                                                       uint32_t owned_tiles, uint32_t rank,
-                                                                       uint32_t world, uint32_t unpack) {
+// (Unpacking: blockIdx.y selects the source rank, as in rt_unpack_tiles_kernel.)
+extern "C" __global__ void __launch_bounds__(256) rt_pack_output_kernel(
+    const uint32_t* __restrict__ output, uint32_t* __restrict__ dst, uint32_t width, uint32_t height,
+    uint32_t tiles_x, uint32_t n_tiles, uint32_t first_rank, uint32_t world, uint64_t stride_px, uint32_t skip_rank,
+    uint32_t unpack) {
+    const uint32_t rank = first_rank + blockIdx.y;
+    if (rank == skip_rank) return;
+    dst += (uint64_t)blockIdx.y * stride_px;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t local_tile = gid >> 6;
-    if (local_tile >= owned_tiles) return;
+    if (local_tile >= owned_tiles_of(n_tiles, rank, world)) return;
     const uint32_t lane = (uint32_t)(gid & 63u);
     const uint32_t tile = (uint32_t)local_tile * world + rank;
     const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u);
@@ -1470,12 +1482,21 @@ extern "C" __global__ void __launch_bounds__(256) rt_pack_output_kernel(const ui
     }
 }
 
+static uint32_t owned_tiles_host(uint32_t n_tiles, uint32_t rank, uint32_t world) {
+    return rank < n_tiles ? (n_tiles - rank + world - 1u) / world : 0u;
+}
+
+// Packs rank `first_rank`'s output (ranks == 1, unpack false), or unpacks the
+// blocks of ranks [first_rank, first_rank + ranks) except skip_rank, block r at
+// packed + (r - first_rank) * stride_px.
 hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t width, uint32_t height, uint32_t tiles_x,
-                                 uint32_t owned_tiles, uint32_t rank, uint32_t world, bool unpack, hipStream_t stream) {
-    const uint64_t threads = (uint64_t)owned_tiles * 64u;
+                                 uint32_t n_tiles, uint32_t first_rank, uint32_t ranks, uint32_t world,
+                                 uint64_t stride_px, uint32_t skip_rank, bool unpack, hipStream_t stream) {
+    const uint64_t threads = (uint64_t)owned_tiles_host(n_tiles, first_rank, world) * 64u;  // the first rank has the most
     const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
-    hipLaunchKernelGGL(rt_pack_output_kernel, dim3(blocks), dim3(256), 0, stream, output, packed, width, height,
-                       tiles_x, owned_tiles, rank, world, unpack ? 1u : 0u);
+    if (blocks == 0 || ranks == 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_pack_output_kernel, dim3(blocks, ranks), dim3(256), 0, stream, output, packed, width, height,
+                       tiles_x, n_tiles, first_rank, world, stride_px, skip_rank, unpack ? 1u : 0u);
     return hipGetLastError();
 }
 
@@ -1489,12 +1510,13 @@ hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint
 }
 
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
-                            uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, float divisor,
-                            hipStream_t stream) {
-    const uint64_t threads = (uint64_t)owned_tiles * 64u;
+                            uint32_t tiles_x, uint32_t n_tiles, uint32_t first_rank, uint32_t ranks, uint32_t world,
+                            uint64_t stride_px, uint32_t skip_rank, float divisor, hipStream_t stream) {
+    const uint64_t threads = (uint64_t)owned_tiles_host(n_tiles, first_rank, world) * 64u;  // the first rank has the most
     const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
-    hipLaunchKernelGGL(rt_unpack_tiles_kernel, dim3(blocks), dim3(256), 0, stream, src, accum, output, width, height,
-                       tiles_x, owned_tiles, rank, world, divisor);
+    if (blocks == 0 || ranks == 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_unpack_tiles_kernel, dim3(blocks, ranks), dim3(256), 0, stream, src, accum, output, width,
+                       height, tiles_x, n_tiles, first_rank, world, stride_px, skip_rank, divisor);
     return hipGetLastError();
 }
 

@@ -40,12 +40,13 @@ hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* ligh
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
                              uint32_t samples, uint32_t frames, hipStream_t stream);
 hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t width, uint32_t height, uint32_t tiles_x,
-                                 uint32_t owned_tiles, uint32_t rank, uint32_t world, bool unpack, hipStream_t stream);
+                                 uint32_t n_tiles, uint32_t first_rank, uint32_t ranks, uint32_t world,
+                                 uint64_t stride_px, uint32_t skip_rank, bool unpack, hipStream_t stream);
 hipError_t rt_launch_pack(const float4* accum, float4* dst, uint32_t width, uint32_t height, uint32_t tiles_x,
                           uint32_t owned_tiles, uint32_t rank, uint32_t world, hipStream_t stream);
 hipError_t rt_launch_unpack(const float4* src, float4* accum, uint32_t* output, uint32_t width, uint32_t height,
-                            uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, float divisor,
-                            hipStream_t stream);
+                            uint32_t tiles_x, uint32_t n_tiles, uint32_t first_rank, uint32_t ranks, uint32_t world,
+                            uint64_t stride_px, uint32_t skip_rank, float divisor, hipStream_t stream);
 
 static_assert(sizeof(rt_params) == 48, "Params is 48 bytes (src/buffers.rs:9-22)");
 static_assert(sizeof(rt_ray_camera) == 16, "RayCamera is 16 bytes");
@@ -1187,10 +1188,12 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     return RT_OK;
 }
 
+// Queueing a frame is host bookkeeping only: the device is selected (a HIP call)
+// only when the call launches the batch.
 int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) {
     if (!ctx || ctx->frame_batch <= 1) return rt_compute_frames(ctx, bounces, 1);
-    RT_ENTER_NOFLUSH(ctx);
     if (ctx->pending_frames && bounces != ctx->pending_bounces) {
+        RT_ENTER_NOFLUSH(ctx);
         const int rc = flush_frames(ctx);
         if (rc) return rc;
     }
@@ -1200,7 +1203,9 @@ int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) {
     }
     if (ctx->params.accumulate) ctx->k += 1;
     ctx->pending_frames += 1;
-    return ctx->pending_frames >= ctx->frame_batch ? flush_frames(ctx) : RT_OK;
+    if (ctx->pending_frames < ctx->frame_batch) return RT_OK;
+    RT_ENTER_NOFLUSH(ctx);
+    return flush_frames(ctx);
 }
 
 int rt_set_frame_batch(rt_ctx* ctx, uint32_t max_frames) {
@@ -1502,11 +1507,22 @@ int rt_unpack_accumulation(rt_ctx* ctx, const void* src_device, uint32_t src_ran
     RT_ENTER(ctx);
     if (!src_device || world_size == 0 || src_rank >= world_size || divisor == 0)
         return fail(ctx, RT_E_INVALID, "unpack: bad arguments");
-    const uint32_t owned = owned_tile_count(ctx->tiles_x * ctx->tiles_y, src_rank, world_size);
-    if (owned == 0) return RT_OK;
     hipError_t e = rt_launch_unpack(static_cast<const float4*>(src_device), ctx->d_accum, ctx->d_out, ctx->width,
-                                    ctx->height, ctx->tiles_x, owned, src_rank, world_size, (float)divisor,
-                                    ctx->stream);
+                                    ctx->height, ctx->tiles_x, ctx->tiles_x * ctx->tiles_y, src_rank, 1, world_size,
+                                    0, 0xffffffffu, (float)divisor, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_unpack_tiles_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_unpack_accumulation_ranks(rt_ctx* ctx, const void* src_device, uint64_t stride_px, uint32_t world_size,
+                                 uint32_t skip_rank, uint32_t divisor) {
+    RT_ENTER(ctx);
+    const uint64_t cap = (uint64_t)owned_tile_count(ctx->tiles_x * ctx->tiles_y, 0, world_size ? world_size : 1) * 64u;
+    if (!src_device || world_size == 0 || divisor == 0 || stride_px < cap)
+        return fail(ctx, RT_E_INVALID, "unpack: bad arguments (stride below the largest rank's block?)");
+    hipError_t e = rt_launch_unpack(static_cast<const float4*>(src_device), ctx->d_accum, ctx->d_out, ctx->width,
+                                    ctx->height, ctx->tiles_x, ctx->tiles_x * ctx->tiles_y, 0, world_size, world_size,
+                                    stride_px, skip_rank, (float)divisor, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_unpack_tiles_kernel launch", e);
     return RT_OK;
 }
@@ -1516,7 +1532,8 @@ int rt_pack_owned_output(rt_ctx* ctx, void* dst_device) {
     if (!dst_device) return fail(ctx, RT_E_INVALID, "dst is NULL");
     if (ctx->owned_tiles == 0) return RT_OK;
     hipError_t e = rt_launch_pack_output(ctx->d_out, static_cast<uint32_t*>(dst_device), ctx->width, ctx->height,
-                                         ctx->tiles_x, ctx->owned_tiles, ctx->rank, ctx->world, false, ctx->stream);
+                                         ctx->tiles_x, ctx->tiles_x * ctx->tiles_y, ctx->rank, 1, ctx->world, 0,
+                                         0xffffffffu, false, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_pack_output_kernel launch", e);
     return RT_OK;
 }
@@ -1524,11 +1541,22 @@ int rt_pack_owned_output(rt_ctx* ctx, void* dst_device) {
 int rt_unpack_output(rt_ctx* ctx, const void* src_device, uint32_t src_rank, uint32_t world_size) {
     RT_ENTER(ctx);
     if (!src_device || world_size == 0 || src_rank >= world_size) return fail(ctx, RT_E_INVALID, "unpack: bad arguments");
-    const uint32_t owned = owned_tile_count(ctx->tiles_x * ctx->tiles_y, src_rank, world_size);
-    if (owned == 0) return RT_OK;
     hipError_t e = rt_launch_pack_output(ctx->d_out, const_cast<uint32_t*>(static_cast<const uint32_t*>(src_device)),
-                                         ctx->width, ctx->height, ctx->tiles_x, owned, src_rank, world_size, true,
-                                         ctx->stream);
+                                         ctx->width, ctx->height, ctx->tiles_x, ctx->tiles_x * ctx->tiles_y, src_rank, 1,
+                                         world_size, 0, 0xffffffffu, true, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "rt_pack_output_kernel launch", e);
+    return RT_OK;
+}
+
+int rt_unpack_output_ranks(rt_ctx* ctx, const void* src_device, uint64_t stride_px, uint32_t world_size,
+                           uint32_t skip_rank) {
+    RT_ENTER(ctx);
+    const uint64_t cap = (uint64_t)owned_tile_count(ctx->tiles_x * ctx->tiles_y, 0, world_size ? world_size : 1) * 64u;
+    if (!src_device || world_size == 0 || stride_px < cap)
+        return fail(ctx, RT_E_INVALID, "unpack: bad arguments (stride below the largest rank's block?)");
+    hipError_t e = rt_launch_pack_output(ctx->d_out, const_cast<uint32_t*>(static_cast<const uint32_t*>(src_device)),
+                                         ctx->width, ctx->height, ctx->tiles_x, ctx->tiles_x * ctx->tiles_y, 0,
+                                         world_size, world_size, stride_px, skip_rank, true, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "rt_pack_output_kernel launch", e);
     return RT_OK;
 }

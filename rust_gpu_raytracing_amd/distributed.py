@@ -106,15 +106,18 @@ class TileGather:
         cap = max_owned_tiles(self.n_tiles, self.world) * 64
         self.device = torch.device("cuda", renderer.device)  # the renderer's GPU, whatever torch's current device is
         shape, dtype = ((cap, 4), torch.float32) if renderer.accumulate else ((cap,), torch.int32)
+        self.cap = cap
         self.packed = torch.zeros(shape, dtype=dtype, device=self.device)
         # gloo moves host tensors only
         self.host = dist.get_backend() == "gloo"
         send_dev = "cpu" if self.host else self.device
         self.send = torch.zeros(shape, dtype=dtype, device=send_dev) if self.host else self.packed
-        self.recv = ([torch.empty(shape, dtype=dtype, device=send_dev) for _ in range(self.world)]
-                     if self.rank == dst else None)
-        self.recv_dev = ([torch.empty(shape, dtype=dtype, device=self.device) for _ in range(self.world)]
-                         if self.rank == dst and self.host else self.recv)
+        # the destination receives into one contiguous (world, cap, ...) buffer, so a
+        # single unpack launch covers every rank's block
+        self.recv_all = torch.empty((self.world, *shape), dtype=dtype, device=send_dev) if self.rank == dst else None
+        self.recv = list(self.recv_all.unbind(0)) if self.rank == dst else None
+        self.recv_dev_all = (torch.empty((self.world, *shape), dtype=dtype, device=self.device)
+                             if self.rank == dst and self.host else self.recv_all)
 
     def __call__(self) -> None:
         import torch
@@ -127,8 +130,7 @@ class TileGather:
             self.send.copy_(self.packed)
             dist.gather(self.send, gather_list=self.recv, dst=self.dst)
             if self.rank == self.dst:
-                for a, b in zip(self.recv_dev, self.recv):
-                    a.copy_(b)
+                self.recv_dev_all.copy_(self.recv_all)
                 torch.cuda.synchronize(self.device)
                 self._unpack()
             r.synchronize()
@@ -151,14 +153,13 @@ class TileGather:
             self.r.pack_owned_output(self.packed.data_ptr())
 
     def _unpack(self) -> None:
+        """Every other rank's block in one launch (the own block is already in place)."""
         r = self.r
-        divisor = max(r.accumulation_index - 1, 1) * r.compute_per_frame  # the last frame's k*c
-        for src, part in enumerate(self.recv_dev):
-            if src != self.rank and owned_tiles(self.n_tiles, src, self.world).shape[0]:
-                if r.accumulate:
-                    r.unpack_accumulation(part.data_ptr(), src, self.world, divisor)
-                else:
-                    r.unpack_output(part.data_ptr(), src, self.world)
+        if r.accumulate:
+            divisor = max(r.accumulation_index - 1, 1) * r.compute_per_frame  # the last frame's k*c
+            r.unpack_accumulation_ranks(self.recv_dev_all.data_ptr(), self.cap, self.world, self.rank, divisor)
+        else:
+            r.unpack_output_ranks(self.recv_dev_all.data_ptr(), self.cap, self.world, self.rank)
 
 
 def gather_accumulation(renderer, dst: int = 0):

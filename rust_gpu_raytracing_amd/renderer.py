@@ -216,8 +216,13 @@ class Renderer:
         self._call("rt_update_ray_directions", N.ptr(self.camera_rays), self.camera_rays.shape[0])
 
     def compute_frame(self, bounces: int = REFERENCE_BOUNCES) -> None:
-        """src/renderer.rs:201-252 (asynchronous)."""
-        self._call("rt_compute_frame", bounces)
+        """src/renderer.rs:201-252 (asynchronous). Called once per frame: one ctypes
+        call, the error path only on failure."""
+        rc = self._lib.rt_compute_frame(self._ctx, bounces)
+        if rc != N.RT_OK:
+            if self._ctx is None:
+                raise N.RtError(N.RT_E_INVALID, "renderer is closed")
+            N.check(self._ctx, rc, self._lib)
 
     def compute_frames(self, bounces: int = REFERENCE_BOUNCES, frames: int = 1) -> None:
         """``frames`` compute_frame calls fused into one launch (same results;
@@ -312,6 +317,15 @@ class Renderer:
 
     def unpack_output(self, src_device_ptr: int, src_rank: int, world_size: int) -> None:
         self._call("rt_unpack_output", ctypes.c_void_p(src_device_ptr), src_rank, world_size)
+
+    def unpack_accumulation_ranks(self, src_device_ptr: int, stride_px: int, world_size: int, skip_rank: int,
+                                  divisor: int) -> None:
+        """Every rank's block of a gather (block r at r * stride_px pixels) but skip_rank's, one launch."""
+        self._call("rt_unpack_accumulation_ranks", ctypes.c_void_p(src_device_ptr), stride_px, world_size, skip_rank,
+                   divisor)
+
+    def unpack_output_ranks(self, src_device_ptr: int, stride_px: int, world_size: int, skip_rank: int) -> None:
+        self._call("rt_unpack_output_ranks", ctypes.c_void_p(src_device_ptr), stride_px, world_size, skip_rank)
 
     def debug_counters(self, n: int = 8) -> list:
         """Diagnostic builds only: the 8 counters, then per-wave stamps (include/rt_abi.h)."""

@@ -259,6 +259,40 @@ def test_gpu_pack_unpack_gather(gpu, accumulate):
             r.close()
 
 
+@pytest.mark.parametrize("accumulate,world,dst", [(1, 3, 0), (1, 5, 2), (0, 4, 3)])
+def test_gpu_unpack_all_ranks_one_launch(gpu, accumulate, world, dst):
+    """rt_unpack_{accumulation,output}_ranks: the gather's blocks laid out in one
+    (world, cap) buffer, every rank's but the destination's unpacked by one launch;
+    the destination's frame equals a 1-GPU render. 200x104 is 25x13 = 325 tiles, so
+    the ranks own unequal tile counts and the padded blocks carry unused rows."""
+    import torch
+
+    scene, bounces = build_config("c2_rtiow", width=200, height=104)
+    acc1, out1, _ = gpu_render(scene, bounces, 3, accumulate=accumulate)
+    rs = [Renderer(scene, rank=r, world_size=world, accumulate=bool(accumulate)) for r in range(world)]
+    try:
+        cap = rs[0].owned_pixel_count()  # rank 0 owns the most tiles
+        shape = (world, cap, 4) if accumulate else (world, cap)
+        dtype = torch.float32 if accumulate else torch.int32
+        allb = torch.full(shape, -1, dtype=dtype, device=gpu)  # garbage in the padding rows
+        for r in rs:
+            for _ in range(3):
+                r.compute_frame(bounces)
+            (r.pack_owned_accumulation if accumulate else r.pack_owned_output)(allb[r.rank].data_ptr())
+            r.synchronize()
+        root = rs[dst]
+        if accumulate:
+            root.unpack_accumulation_ranks(allb.data_ptr(), cap, world, dst, root.accumulation_index - 1)
+        else:
+            root.unpack_output_ranks(allb.data_ptr(), cap, world, dst)
+        root.synchronize()
+        assert np.array_equal(root.read_accumulation().view(np.uint32), acc1.view(np.uint32))
+        assert np.array_equal(root.read_output(), out1)
+    finally:
+        for r in rs:
+            r.close()
+
+
 @pytest.mark.parametrize("config,spp,accumulate,batch,parallel,kw", [
     ("c2_rtiow", 1, 1, 4, "1", {}),
     ("c2_rtiow", 1, 1, 4, "0", {}),
