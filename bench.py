@@ -180,6 +180,9 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # RT_BENCH_DIST=1: take the N > 1 code path (process group, gather in the timed
+    # region, weak run) even with one rank -- the one-GPU test box's check of the RCCL path
+    dist_run = world > 1 or os.environ.get("RT_BENCH_DIST") == "1"
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     assert torch.cuda.is_available(), "bench.py needs a HIP device"
@@ -189,7 +192,7 @@ def main() -> int:
     device = 0 if os.environ.get("RT_BENCH_ONE_DEVICE") == "1" else local_rank
     backend = os.environ.get("RT_DIST_BACKEND", "nccl")
     torch.cuda.set_device(device)
-    if world > 1:
+    if dist_run:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
@@ -202,7 +205,7 @@ def main() -> int:
 
     if rank == 0:
         native_build.build(verbose=False)
-    if world > 1:
+    if dist_run:
         dist.barrier()
 
     def size_for(scaling):
@@ -223,10 +226,10 @@ def main() -> int:
         def barrier_sync():
             r.synchronize()
             torch.cuda.synchronize()
-            if world > 1:
+            if dist_run:
                 dist.barrier()
 
-        gathered = world > 1 and not args.no_gather
+        gathered = dist_run and not args.no_gather
         if gathered:
             from rust_gpu_raytracing_amd.distributed import gather_accumulation
         for _ in range(args.warmup):
@@ -243,7 +246,7 @@ def main() -> int:
         while args.settle_ms > 0:
             go = torch.tensor([1.0 if (time.perf_counter() - t_settle) * 1e3 < args.settle_ms else 0.0],
                               device="cuda" if backend == "nccl" else "cpu")
-            if world > 1:
+            if dist_run:
                 dist.all_reduce(go, op=dist.ReduceOp.MIN)
             if go.item() == 0.0:
                 break
@@ -289,7 +292,7 @@ def main() -> int:
                    timing=r.dispatch_time_total(), owned_px=r.owned_pixel_count())
         stats = torch.tensor([t_total, t_render, t_gather, float(res["rays"])], dtype=torch.float64,
                              device="cuda" if backend == "nccl" else "cpu")
-        if world > 1:
+        if dist_run:
             mx = stats[0:3].clone()
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             tot = stats[3:4].clone()
@@ -313,7 +316,7 @@ def main() -> int:
             return 3
     r.close()
     weak = None
-    if world > 1 and args.scaling == "strong" and not args.no_weak:
+    if dist_run and args.scaling == "strong" and not args.no_weak:
         w_run = run("weak", args.frame_batch or default_frame_batch(1, args.steps))
         w_run["r"].close()
         weak = {
@@ -388,7 +391,7 @@ def main() -> int:
                 "build_hash": build_hash,
             },
         }
-        if world > 1:
+        if dist_run:
             result["render_ms_per_step"] = m["t_render_max"] / args.steps * 1e3
             result["gather_ms"] = m["t_gather_max"] * 1e3
             result["gather_in_value"] = m["gathered"]
@@ -398,7 +401,7 @@ def main() -> int:
             log("cpu baseline ...")
             result["cpu_baseline"] = cpu_baseline(scene, bounces, args.cpu_seconds, args.cpu_sample_world)
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_run:
         dist.destroy_process_group()
     return 0
 

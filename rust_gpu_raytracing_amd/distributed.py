@@ -139,7 +139,7 @@ class TileGather:
         # waits): the pack kernel, the gather (ProcessGroupNCCL orders its stream
         # after the current stream, and the current stream after the collective),
         # then the unpack kernels on the destination.
-        stream = torch.cuda.ExternalStream(r.stream_handle(), device=self.device)
+        stream = torch.cuda.ExternalStream(r.stream_handle, device=self.device)
         with torch.cuda.device(self.device), torch.cuda.stream(stream):
             self._pack()
             dist.gather(self.send, gather_list=self.recv, dst=self.dst)
