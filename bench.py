@@ -16,9 +16,13 @@ Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
 default "--scaling strong", the metric's config: the 1920x1080 frame is
 tile-split across ranks (8x8 tile t -> rank t % N), launches of up
 to 32N frames (a GPU's launch holds the units of an N=1 launch), and the timed region also
-assembles the image on rank 0 once (device pack -> RCCL gather of the RGBA32F
-accumulation -> unpack), so `value` includes the gather (also reported as
-gather_ms). A secondary "weak" object measures the same view at N x the pixels
+assembles the frame on rank 0 once (device pack -> RCCL gather -> unpack), so `value`
+includes the gather (also reported as gather_ms). --gather image (default) moves the
+displayed RGBA8 frame (4 B/px; accumulations stay sharded on their owners, which keep
+accumulating their tiles), --gather accumulation the RGBA32F accumulation (16 B/px, the
+whole renderer state on rank 0). Both gathers are also timed alone after the timed
+region (gather_image_ms, gather_accum_ms), and value_with_accum_gather prices the
+accumulation gather instead. A secondary "weak" object measures the same view at N x the pixels
 ((1920*sqrt(N)) x (1080*sqrt(N)) in whole tiles, one 1920x1080 frame's worth
 of tiles per GPU). `value` = all ranks' rays / the slowest rank's time.
 
@@ -167,6 +171,9 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: leave the RCCL gather of the image to rank 0 out of the timed region")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the secondary weak-scaling measurement")
+    ap.add_argument("--gather", choices=["image", "accumulation"], default="image",
+                    help="N>1: the payload of the gather in the timed region: the displayed RGBA8 frame "
+                         "(4 B/px) or the RGBA32F accumulation (16 B/px)")
     ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
                     help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N, steps)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
@@ -231,7 +238,7 @@ def main() -> int:
 
         gathered = dist_run and not args.no_gather
         if gathered:
-            from rust_gpu_raytracing_amd.distributed import gather_accumulation
+            from rust_gpu_raytracing_amd.distributed import gather_frame
         for _ in range(args.warmup):
             r.compute_frame(bounces)
         # Clock settle: the GPU's power management raises its clocks only after tens of
@@ -255,10 +262,11 @@ def main() -> int:
             settle_frames += frame_batch
             r.synchronize()
         if gathered:
-            # one untimed readback: allocates the gather's buffers and lets RCCL set up its
+            # untimed readbacks: allocate the gathers' buffers and let RCCL set up its
             # peer connections (made lazily on a pair's first transfer), as any display
             # loop has done by its second frame
-            gather_accumulation(r, dst=0)
+            gather_frame(r, 0, "accumulation")
+            gather_frame(r, 0, "image")
         barrier_sync()
         r.reset_ray_count()
         r.reset_timing()
@@ -270,35 +278,43 @@ def main() -> int:
             if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
                 log(f"step {i + 1}/{args.steps}")
         if gathered:
-            # the image assembled on rank 0 (pack -> RCCL gather -> unpack), stream-ordered
+            # the frame assembled on rank 0 (pack -> RCCL gather -> unpack), stream-ordered
             # after the last frame; the closing barrier + sync waits for it
-            gather_accumulation(r, dst=0)
+            gather_frame(r, 0, args.gather, sync=False)
         barrier_sync()
         t_total = time.perf_counter() - t0
         r.set_timing(False)  # (reads the launch events back: outside the timed region)
-        t_gather = 0.0
+        t_gather = t_gather_accum = t_gather_image = 0.0
         if gathered:
-            # the gather's own cost, reported beside `value` (which already includes it):
-            # one more readback of the same frame, timed alone
-            barrier_sync()
-            t1 = time.perf_counter()
-            gather_accumulation(r, dst=0)
-            barrier_sync()
-            t_gather = time.perf_counter() - t1
+            # the gathers' own cost, reported beside `value` (which already includes the
+            # --gather one): one more readback of the same frame per payload, timed alone
+            # (the accumulation first, so that rank 0's output ends as the image gather
+            # left it and the gather verify checks both payloads)
+            def timed_gather(what):
+                barrier_sync()
+                t1 = time.perf_counter()
+                gather_frame(r, 0, what, sync=False)
+                barrier_sync()
+                return time.perf_counter() - t1
+
+            t_gather_accum = timed_gather("accumulation")
+            t_gather_image = timed_gather("image")
+            t_gather = t_gather_image if args.gather == "image" else t_gather_accum
         t_render = t_total - t_gather
         res = dict(r=r, scene=scene, bounces=bounces, width=width, height=height, rays=r.ray_count(),
                    settle_frames=settle_frames,
                    t_render=t_render, t_gather=t_gather, gathered=gathered, launch=r.launch_config(),
                    timing=r.dispatch_time_total(), owned_px=r.owned_pixel_count())
-        stats = torch.tensor([t_total, t_render, t_gather, float(res["rays"])], dtype=torch.float64,
-                             device="cuda" if backend == "nccl" else "cpu")
+        stats = torch.tensor([t_total, t_render, t_gather, t_gather_accum, t_gather_image, float(res["rays"])],
+                             dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         if dist_run:
-            mx = stats[0:3].clone()
+            mx = stats[0:5].clone()
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            tot = stats[3:4].clone()
+            tot = stats[5:6].clone()
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
             stats = torch.cat([mx, tot])
-        res["t_total_max"], res["t_render_max"], res["t_gather_max"], res["rays_total"] = map(float, stats.tolist())
+        (res["t_total_max"], res["t_render_max"], res["t_gather_max"], res["t_gather_accum_max"],
+         res["t_gather_image_max"], res["rays_total"]) = map(float, stats.tolist())
         return res
 
     fb = args.frame_batch or default_frame_batch(world, args.steps)
@@ -324,6 +340,7 @@ def main() -> int:
             "ms_per_step": w_run["t_total_max"] / args.steps * 1e3,
             "render_ms_per_step": w_run["t_render_max"] / args.steps * 1e3,
             "gather_ms": w_run["t_gather_max"] * 1e3,
+            "gather_accum_ms": w_run["t_gather_accum_max"] * 1e3,
             "width": w_run["width"], "height": w_run["height"], "frame_batch": args.frame_batch or default_frame_batch(1, args.steps),
             "note": "secondary: the same view at N x the pixels, every GPU owning one 1920x1080 frame's worth of tiles",
         }
@@ -395,6 +412,13 @@ def main() -> int:
             result["render_ms_per_step"] = m["t_render_max"] / args.steps * 1e3
             result["gather_ms"] = m["t_gather_max"] * 1e3
             result["gather_in_value"] = m["gathered"]
+            if m["gathered"]:
+                result["gather_payload"] = args.gather
+                result["gather_image_ms"] = m["t_gather_image_max"] * 1e3
+                result["gather_accum_ms"] = m["t_gather_accum_max"] * 1e3
+                # the same run priced with the accumulation gather (16 B/px) in place of
+                # the --gather one: rays / (render time + the accumulation gather's time)
+                result["value_with_accum_gather"] = m["rays_total"] / (m["t_render_max"] + m["t_gather_accum_max"]) / 1e6
             if weak is not None:
                 result["weak"] = weak
         if world == 1 and not args.no_cpu_baseline:

@@ -5,10 +5,18 @@ drives one GPU; the frame is cut into 8x8-pixel tiles and tile t belongs to rank
 t % world_size. Each rank's kernel launch renders only its tiles, using global
 pixel indices for the RNG seeds (compute_shader.wgsl:217), so the assembled image
 is bitwise identical to a 1-GPU render. Rendering needs no communication; at
-readback every rank packs its tiles' RGBA32F accumulation into one contiguous
-buffer (tile order, 64 pixels per tile) and one RCCL gather (torch.distributed,
-backend "nccl") moves them to the destination rank, which unpacks them into its
-framebuffer and re-packs the RGBA8 output.
+readback every rank packs its tiles into one contiguous buffer (tile order, 64
+pixels per tile) and one RCCL gather (torch.distributed, backend "nccl") moves them
+to the destination rank, which unpacks them into its framebuffer. Two payloads:
+
+* "image": the packed RGBA8 output words (4 B/px) -- the frame as the reference
+  displays it (the output buffer its render pass blits, src/renderer.rs:237-249,
+  src/render_shader.wgsl). The accumulation stays sharded on its owner ranks, which
+  keep accumulating their own tiles frame after frame; this is the per-frame
+  readback of an interactive multi-GPU loop.
+* "accumulation": the RGBA32F accumulation (16 B/px), from which the destination
+  also rebuilds the RGBA8 output: the whole renderer state on one rank (a
+  checkpoint, or a switch back to one GPU).
 """
 from __future__ import annotations
 
@@ -43,20 +51,22 @@ def owned_pixel_indices(width: int, height: int, rank: int, world_size: int) -> 
 
 
 def pack_owned_host(accum: np.ndarray, rank: int, world_size: int) -> np.ndarray:
-    """Host mirror of rt_pack_tiles_kernel: (H, W, 4) f32 -> (owned_tiles*64, 4)."""
-    h, w, _ = accum.shape
+    """Host mirror of rt_pack_tiles_kernel: (H, W, 4) f32 -> (owned_tiles*64, 4), or of
+    rt_pack_owned_output: (H, W) RGBA8 words -> (owned_tiles*64,). Padding slots are 0."""
+    h, w = accum.shape[:2]
     idx = owned_pixel_indices(w, h, rank, world_size)
-    out = np.zeros((idx.shape[0], 4), np.float32)
+    flat = accum.reshape(h * w, *accum.shape[2:])
+    out = np.zeros((idx.shape[0], *accum.shape[2:]), accum.dtype)
     ok = idx >= 0
-    out[ok] = accum.reshape(-1, 4)[idx[ok]]
+    out[ok] = flat[idx[ok]]
     return out
 
 
 def unpack_host(accum: np.ndarray, packed: np.ndarray, src_rank: int, world_size: int) -> None:
-    h, w, _ = accum.shape
+    h, w = accum.shape[:2]
     idx = owned_pixel_indices(w, h, src_rank, world_size)
     ok = idx >= 0
-    accum.reshape(-1, 4)[idx[ok]] = packed[: idx.shape[0]][ok]
+    accum.reshape(h * w, *accum.shape[2:])[idx[ok]] = packed[: idx.shape[0]][ok]
 
 
 def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0):
@@ -83,6 +93,9 @@ def gather_packed(packed, n_tiles: int, rank: int, world_size: int, dst: int = 0
     return [b[: owned_tiles(n_tiles, r, world_size).shape[0] * 64].to(device) for r, b in enumerate(bufs)]
 
 
+GATHER_PAYLOADS = ("image", "accumulation")
+
+
 class TileGather:
     """Reusable readback gather for a tile-split Renderer: the pack buffer and (on
     `dst`) the receive buffers are allocated once, so repeated gathers (one per
@@ -90,22 +103,33 @@ class TileGather:
     nothing. The first gather also makes RCCL set up its peer connections, which it
     does lazily on a pair's first transfer; bench.py runs one during warmup.
 
-    Accumulating renders move the RGBA32F accumulation (16 B/px) and rebuild the
-    RGBA8 output from it with the last frame's divisor k*c (compute_shader.wgsl:166);
-    non-accumulating ones (which never write the accumulation, :171-178) move the
-    RGBA8 words as is."""
+    what="image" moves the RGBA8 output words (4 B/px) as is: the destination's
+    output buffer then holds the whole frame, bit-identical to a 1-GPU render's,
+    while its accumulation keeps only its own tiles. what="accumulation" (only for
+    accumulating renders) moves the RGBA32F accumulation (16 B/px) and rebuilds the
+    RGBA8 output from it with the last frame's divisor k*c (compute_shader.wgsl:166),
+    so both buffers equal a 1-GPU render's. Default: the accumulation when the
+    renderer accumulates (non-accumulating renders never write it, :171-178)."""
 
-    def __init__(self, renderer, dst: int = 0):
+    def __init__(self, renderer, dst: int = 0, what: str | None = None):
         import torch
         import torch.distributed as dist
 
+        if what is None:
+            what = "accumulation" if renderer.accumulate else "image"
+        if what not in GATHER_PAYLOADS:
+            raise ValueError(f"TileGather: what must be one of {GATHER_PAYLOADS}, got {what!r}")
+        if what == "accumulation" and not renderer.accumulate:
+            raise ValueError("TileGather: a non-accumulating render never writes its accumulation; gather the image")
+        self.what = what
+        self.accum = what == "accumulation"
         self.r, self.dst = renderer, dst
         self.rank, self.world = renderer.rank, renderer.world_size
         tx_n, ty_n = tile_grid(renderer.width, renderer.height)
         self.n_tiles = tx_n * ty_n
         cap = max_owned_tiles(self.n_tiles, self.world) * 64
         self.device = torch.device("cuda", renderer.device)  # the renderer's GPU, whatever torch's current device is
-        shape, dtype = ((cap, 4), torch.float32) if renderer.accumulate else ((cap,), torch.int32)
+        shape, dtype = ((cap, 4), torch.float32) if self.accum else ((cap,), torch.int32)
         self.cap = cap
         self.packed = torch.zeros(shape, dtype=dtype, device=self.device)
         # gloo moves host tensors only
@@ -147,7 +171,7 @@ class TileGather:
                 self._unpack()
 
     def _pack(self) -> None:
-        if self.r.accumulate:
+        if self.accum:
             self.r.pack_owned_accumulation(self.packed.data_ptr())
         else:
             self.r.pack_owned_output(self.packed.data_ptr())
@@ -155,19 +179,34 @@ class TileGather:
     def _unpack(self) -> None:
         """Every other rank's block in one launch (the own block is already in place)."""
         r = self.r
-        if r.accumulate:
+        if self.accum:
             divisor = max(r.accumulation_index - 1, 1) * r.compute_per_frame  # the last frame's k*c
             r.unpack_accumulation_ranks(self.recv_dev_all.data_ptr(), self.cap, self.world, self.rank, divisor)
         else:
             r.unpack_output_ranks(self.recv_dev_all.data_ptr(), self.cap, self.world, self.rank)
 
 
-def gather_accumulation(renderer, dst: int = 0):
-    """Assemble the whole frame of a tile-split render on rank `dst`'s Renderer:
-    device pack -> RCCL gather -> device unpack (a TileGather cached on the
-    renderer, so a second call allocates nothing)."""
-    g = getattr(renderer, "_tile_gather", None)
-    if g is None or g.dst != dst:
-        g = renderer._tile_gather = TileGather(renderer, dst)
+def gather_frame(renderer, dst: int = 0, what: str | None = None, sync: bool = True):
+    """Assemble the frame of a tile-split render on rank `dst`'s Renderer: device
+    pack -> RCCL gather -> device unpack, of the payload `what` (TileGather). The
+    TileGather is cached on the renderer per (dst, payload), so a second call
+    allocates nothing. sync=False leaves the RCCL path stream-ordered (no host wait)."""
+    cache = renderer.__dict__.setdefault("_tile_gathers", {})
+    what = what or ("accumulation" if renderer.accumulate else "image")
+    g = cache.get((dst, what))
+    if g is None:
+        g = cache[(dst, what)] = TileGather(renderer, dst, what)
     g()
-    renderer.synchronize()
+    if sync:
+        renderer.synchronize()
+
+
+def gather_accumulation(renderer, dst: int = 0):
+    """The whole renderer state on `dst`: the accumulation when the render
+    accumulates (plus the output rebuilt from it), else the RGBA8 image."""
+    gather_frame(renderer, dst)
+
+
+def gather_image(renderer, dst: int = 0):
+    """The displayed frame (RGBA8 words) on `dst`; accumulations stay on their owners."""
+    gather_frame(renderer, dst, "image")

@@ -40,13 +40,22 @@ def main() -> int:
         r.synchronize()
         after = r.read_accumulation(), r.read_output()
         recv = g.recv_all[rank].cpu().numpy()
+        gi = TileGather(r, dst=0, what="image")  # bench.py's default payload at N > 1
+        gi()
+        r.synchronize()
+        after_image = r.read_accumulation(), r.read_output()
+        recv_words = gi.recv_all[rank].cpu().numpy().view(np.uint32)
     dist.destroy_process_group()
     same = np.array_equal(before[0].view(np.uint32), after[0].view(np.uint32)) and np.array_equal(before[1], after[1])
     # the block RCCL delivered is this rank's packed accumulation, bit for bit
     want = pack_owned_host(before[0], rank, 1)
     packed_ok = np.array_equal(recv[: want.shape[0]].view(np.uint32), want.view(np.uint32))
-    ok = same and packed_ok and before[0].any()
-    print("ok" if ok else f"MISMATCH same={same} packed={packed_ok}", flush=True)
+    same_image = (np.array_equal(before[0].view(np.uint32), after_image[0].view(np.uint32))
+                  and np.array_equal(before[1], after_image[1]))
+    want_words = pack_owned_host(before[1], rank, 1)
+    words_ok = np.array_equal(recv_words[: want_words.shape[0]], want_words)
+    ok = same and packed_ok and same_image and words_ok and before[0].any() and before[1].any()
+    print("ok" if ok else f"MISMATCH same={same} packed={packed_ok} image={same_image} words={words_ok}", flush=True)
     return 0 if ok else 1
 
 

@@ -39,13 +39,19 @@ def _worker(rank, world, port, config, w, h, frames, q):
         packed = torch.from_numpy(D.pack_owned_host(acc, rank, world))
         tx, ty = D.tile_grid(w, h)
         parts = D.gather_packed(packed, tx * ty, rank, world, dst=0)
+        # the "image" payload: the RGBA8 output words (as int32: gloo has no uint32)
+        words = torch.from_numpy(D.pack_owned_host(out.view(np.int32), rank, world))
+        word_parts = D.gather_packed(words, tx * ty, rank, world, dst=0)
         tot = torch.tensor([rays], dtype=torch.int64)
         dist.all_reduce(tot)
         if rank == 0:
             full = np.zeros_like(acc)
             for src, part in enumerate(parts):
                 D.unpack_host(full, part.numpy(), src, world)
-            q.put((full, int(tot.item())))
+            image = np.zeros(out.shape, np.int32)
+            for src, part in enumerate(word_parts):
+                D.unpack_host(image, part.numpy(), src, world)
+            q.put((full, image.view(np.uint32), int(tot.item())))
     finally:
         dist.destroy_process_group()
 
@@ -61,14 +67,15 @@ def test_gloo_tile_gather_matches_single_render(oracle_lib, world, config, w, h)
     procs = [ctx.Process(target=_worker, args=(r, world, port, config, w, h, frames, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full, rays = q.get(timeout=300)
+    full, image, rays = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     scene, bounces = build_config(config, width=w, height=h)
-    acc1, _, rays1 = oracle_lib.render_frames(scene, bounces, frames)
+    acc1, out1, rays1 = oracle_lib.render_frames(scene, bounces, frames)
     assert rays == rays1
     assert np.array_equal(full.view(np.uint32), acc1.view(np.uint32))
+    assert out1.any() and np.array_equal(image, out1)
 
 
 def test_owned_pixels_partition_the_image():
@@ -88,3 +95,20 @@ def test_pack_unpack_roundtrip_host():
     for r in range(3):
         D.unpack_host(out, D.pack_owned_host(acc, r, 3), r, 3)
     assert np.array_equal(out, acc)
+    words = rng.integers(0, 2**32, (20, 33), dtype=np.uint64).astype(np.uint32)
+    img = np.zeros_like(words)
+    for r in range(3):
+        packed = D.pack_owned_host(words, r, 3)
+        assert packed.dtype == np.uint32 and packed.shape == (D.owned_pixel_indices(33, 20, r, 3).shape[0],)
+        D.unpack_host(img, packed, r, 3)
+    assert np.array_equal(img, words)
+
+
+def test_tile_gather_payload_checks():
+    """TileGather refuses an accumulation gather of a render that never writes one."""
+    class FakeRenderer:
+        accumulate = False
+    with pytest.raises(ValueError):
+        D.TileGather(FakeRenderer(), 0, "accumulation")
+    with pytest.raises(ValueError):
+        D.TileGather(FakeRenderer(), 0, "pixels")

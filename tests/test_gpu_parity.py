@@ -215,13 +215,17 @@ def test_gpu_cost_ordered_schedule_inactive_on_small_frames(gpu):
         assert np.array_equal(order, np.arange(order.size)) and not costs.any()
 
 
-@pytest.mark.parametrize("accumulate", [1, 0])
-def test_gpu_pack_unpack_gather(gpu, accumulate):
+@pytest.mark.parametrize("accumulate,payload", [(1, "accumulation"), (0, "image"), (1, "image")])
+def test_gpu_pack_unpack_gather(gpu, accumulate, payload):
     """The multi-GPU readback path on one device: ranks pack their tiles into device
-    buffers, rank 0 unpacks them; the assembled frame equals a 1-GPU render. A
-    non-accumulating render (which never writes the accumulation, :171-178) moves
-    its RGBA8 words instead."""
+    buffers, rank 0 unpacks them; the assembled frame equals a 1-GPU render. The
+    "image" payload (bench.py's default at N > 1, and the only one of a
+    non-accumulating render, which never writes the accumulation, :171-178) moves the
+    RGBA8 words: rank 0's output is the whole frame, its accumulation keeps its own
+    tiles only."""
     import torch
+
+    from rust_gpu_raytracing_amd.distributed import owned_pixel_indices
 
     scene, bounces = build_config("c2_rtiow", width=200, height=104)
     acc1, out1, _ = gpu_render(scene, bounces, 3, accumulate=accumulate)
@@ -232,6 +236,25 @@ def test_gpu_pack_unpack_gather(gpu, accumulate):
             for _ in range(3):
                 r.compute_frame(bounces)
         bufs = []
+        if payload == "image" and accumulate:
+            for r in rs:
+                t = torch.empty((r.owned_pixel_count(),), dtype=torch.int32, device=gpu)
+                r.pack_owned_output(t.data_ptr())
+                r.synchronize()
+                bufs.append(t)
+            root = rs[0]
+            for src in range(1, world):
+                root.unpack_output(bufs[src].data_ptr(), src, world)
+            root.synchronize()
+            assert np.array_equal(root.read_output(), out1)
+            acc0 = root.read_accumulation().reshape(-1, 4)
+            own = owned_pixel_indices(200, 104, 0, world)
+            own = own[own >= 0]
+            mine = np.zeros(acc0.shape[0], bool)
+            mine[own] = True
+            assert np.array_equal(acc0[mine].view(np.uint32), acc1.reshape(-1, 4)[mine].view(np.uint32))
+            assert not acc0[~mine].any()  # the other ranks' accumulations stay on their owners
+            return
         for r in rs:
             n = r.owned_pixel_count()
             if accumulate:
