@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--device-rays", action="store_true", help="generate primary rays on the device")
     ap.add_argument("--frame-batch", type=int, default=8, help="rt_set_frame_batch (frames is rounded to a multiple)")
+    ap.add_argument("--world", type=int, default=1, help="time rank --rank's share of an N-way tile split")
+    ap.add_argument("--rank", type=int, default=0)
     args = ap.parse_args()
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     rays_dirs = scene.camera.recalculate_ray_directions()
@@ -52,9 +54,11 @@ def main():
             os.environ[k] = v
         lib = N.load_library(Path(p).resolve())
         if args.device_rays:
-            rs.append(Renderer(scene, lib=lib, device_rays=True, frame_batch=args.frame_batch))
+            rs.append(Renderer(scene, lib=lib, device_rays=True, frame_batch=args.frame_batch,
+                               rank=args.rank, world_size=args.world))
         else:
-            rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib, frame_batch=args.frame_batch))
+            rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib, frame_batch=args.frame_batch,
+                               rank=args.rank, world_size=args.world))
         os.environ.clear()
         os.environ.update(saved)
     args.frames = max(1, args.frames // args.frame_batch) * args.frame_batch
