@@ -243,6 +243,7 @@ __device__ __forceinline__ float prune_limit(const TraceState& ts) {
 
 // Slab constants and depth bounds of a BVH walk. The triangle walk culls by
 // box only: no slack, no distance limit.
+template <bool kTris>
 __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArgs& ka, f3 o, float a, uint32_t phase,
                                             TraceState& ts) {
     const float r = sqrt_up(dot(o, o));  // |o| sizes the margins only: an upper bound will do
@@ -260,6 +261,11 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
                              ((__float_as_uint(ts.inv.z) >> 31) << 2);
         ts.node = oct * ka.sphere_octant_stride;
+        // layouts storing (near, far) corners (sphere-only scenes, set by the host):
+        // the plane constants paired the same way, so node_step can skip slab_hit's
+        // min/max (rt_bvh_slab.h)
+        if constexpr (!kTris)
+            if (ka.sphere_boxes_ordered) slab_pair_by_octant(ts.slab);
     }
 }
 
@@ -305,7 +311,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
         ts.phase = ka.tri_nodes != 0 ? 0u : 1u;
     }
     if (ts.phase == 1 && ka.sphere_nodes == 0) ts.phase = 2;
-    phase_setup(sv, ka, o, a, ts.phase, ts);
+    phase_setup<kTris>(sv, ka, o, a, ts.phase, ts);
 }
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
@@ -356,7 +362,7 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
         if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
         ts.node = 0;
         ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
-        phase_setup(sv, ka, o, ts.a2 * 0.5f, 1, ts);
+        phase_setup<kTris>(sv, ka, o, ts.a2 * 0.5f, 1, ts);
     } else if (ts.node >= ka.sphere_nodes) {
         ts.phase = 2;
     }
@@ -402,7 +408,10 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     const float4 lo = nodes[2u * ts.node];
     const float4 hi = nodes[2u * ts.node + 1u];
     float near_t, far_t;
-    slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+    if (!kTris && ka.sphere_boxes_ordered)  // (near, far) corners: no min/max per axis (6 VALU per node step)
+        slab_hit_ordered(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+    else
+        slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
     // enters the inflated box and is not wholly behind the origin; on the sphere
     // side also not beyond the best sphere or the triangle hit (a sphere wins
     // only when strictly closer, :347); ts.slack / ts.limit are 0 / inf on the

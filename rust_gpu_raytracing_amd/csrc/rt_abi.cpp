@@ -192,6 +192,9 @@ struct rt_ctx {
     uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
     bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
     bool sphere_octants = true;          // RT_SPHERE_OCTANTS=0: one BVH layout (A/B switch)
+    bool sphere_box_order = true;        // RT_SPHERE_BOX_ORDER=0: octant layouts keep bmin/bmax (A/B switch)
+    bool sphere_boxes_ordered = false;   // the uploaded layouts store (near, far) corners
+    bool slots_sphere_only = false;      // the uploaded slots were laid out for the sphere-only kernels
     uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
     uint32_t n_always = 0, n_nodes = 0, n_slots = 0;
     float sphere_extent = 0.0f;
@@ -348,14 +351,17 @@ int upload_spheres(rt_ctx* ctx, const rt_scene_sphere* s, uint32_t n) {
 
 // Rebuild the kernel's sphere slots (brute-force set + BVH) for the first
 // `count` spheres and upload them, stream-ordered before the next launch.
-int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
-    if (!ctx->slots_dirty && ctx->slots_count == count) return RT_OK;
+int refresh_sphere_slots(rt_ctx* ctx, uint32_t count, bool sphere_only) {
+    if (!ctx->slots_dirty && ctx->slots_count == count && ctx->slots_sphere_only == sphere_only) return RT_OK;
     SphereSlots sl;
     build_sphere_slots(ctx->h_sph.data(), count, ctx->use_bvh, &sl, ctx->sphere_leaf_max);
     std::vector<uint32_t> mat(count);
     for (uint32_t i = 0; i < count; i++) mat[i] = ctx->h_sph[i].material_index;
     std::vector<SphereBvhNode> oct;  // 8 direction-ordered copies; layout 0 alone is a complete walk too
-    order_bvh_by_octant(sl.nodes, &oct);
+    // boxes stored as (near, far) corners per octant when that is exact (rt_bvh_slab.h);
+    // only the sphere-only kernels read them that way, so only for scenes without objects
+    const bool box_order = ctx->sphere_box_order && sphere_only && box_layout_orderable(sl.nodes);
+    order_bvh_by_octant(sl.nodes, &oct, box_order);
     int rc;
     if ((rc = upload_raw(ctx, ctx->d_slot_sph, sl.slot_sph.data(), sl.slot_sph.size() * 4)) ||
         (rc = upload_raw(ctx, ctx->d_slot_orig, sl.slot_orig.data(), sl.slot_orig.size() * 4)) ||
@@ -365,11 +371,13 @@ int refresh_sphere_slots(rt_ctx* ctx, uint32_t count) {
     ctx->n_always = sl.n_always;
     ctx->n_slots = (uint32_t)sl.slot_orig.size();
     ctx->n_nodes = (uint32_t)sl.nodes.size();
+    ctx->sphere_boxes_ordered = box_order;
     ctx->sphere_extent = sl.extent;
     ctx->sphere_rmin = sl.r_min;
     ctx->sphere_rmax = sl.r_max;
     ctx->slots_dirty = false;
     ctx->slots_count = count;
+    ctx->slots_sphere_only = sphere_only;
     return RT_OK;
 }
 
@@ -612,6 +620,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->use_bvh = !(env && env[0] == '0');
         env = std::getenv("RT_SPHERE_OCTANTS");
         ctx->sphere_octants = !(env && env[0] == '0');
+        env = std::getenv("RT_SPHERE_BOX_ORDER");
+        ctx->sphere_box_order = !(env && env[0] == '0');
         env = std::getenv("RT_QUEUE_STRIPES");
         if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TRAV_THRESHOLD");
@@ -920,7 +930,7 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
 static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     const rt_params& p = ctx->params;
     {
-        int rc = refresh_sphere_slots(ctx, p.sphere_count);
+        int rc = refresh_sphere_slots(ctx, p.sphere_count, p.object_count == 0);
         if (rc) return rc;
         rc = refresh_tri_accel(ctx, p.object_count);
         if (rc) return rc;
@@ -1065,6 +1075,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     ka.sphere_nodes = layouts * ctx->n_nodes;
     ka.sphere_octant_stride = layouts == 8 ? ctx->n_nodes : 0u;
+    ka.sphere_boxes_ordered = (layouts == 8 && ctx->sphere_boxes_ordered && !tris) ? 1u : 0u;
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
     ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);
     size_t lds_bytes;

@@ -107,3 +107,35 @@ RT_SLAB_FN void slab_hit(const SlabRay& r, float lox, float loy, float loz, floa
     near_t = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
     far_t = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
 }
+
+// Box-ordered layouts (order_bvh_by_octant with swap_boxes): layout k stores
+// every box as (near corner, far corner) for rays of direction octant k, i.e.
+// bmin/bmax swapped on the axes where bit k is set (the ray travels towards
+// -axis). The ray's constants are paired the same way (slab_pair_by_octant: l*
+// with the near corner, h* with the far one), so each slab's nearer plane is
+// known and the test needs no min/max per axis. It is the same arithmetic as
+// slab_hit on the unswapped box: for lo <= hi and a finite slope, rounding is
+// monotone, so fma(lo, ix, lx) <= fma(hi, ix, hx) when ix >= 0 and >= when
+// ix < 0 -- exactly the operands slab_hit's min/max would pick. The NaN-free
+// premise (|plane * ix| <= 1e8 * 1e30 stays finite) is what box_layout_orderable
+// checks on the host; a NaN origin makes both planes of an axis NaN, which both
+// forms ignore alike.
+RT_SLAB_FN void slab_pair_by_octant(SlabRay& r) {
+    const bool nx = signbit(r.ix), ny = signbit(r.iy), nz = signbit(r.iz);
+    const float lx = nx ? r.hx : r.lx, hx = nx ? r.lx : r.hx;
+    const float ly = ny ? r.hy : r.ly, hy = ny ? r.ly : r.hy;
+    const float lz = nz ? r.hz : r.lz, hz = nz ? r.lz : r.hz;
+    r.lx = lx;
+    r.hx = hx;
+    r.ly = ly;
+    r.hy = hy;
+    r.lz = lz;
+    r.hz = hz;
+}
+
+// near/far parameters of a box stored as (near corner n, far corner f).
+RT_SLAB_FN void slab_hit_ordered(const SlabRay& r, float nx, float ny, float nz, float fx, float fy, float fz,
+                                 float& near_t, float& far_t) {
+    near_t = fmaxf(fmaxf(fmaf(nx, r.ix, r.lx), fmaf(ny, r.iy, r.ly)), fmaf(nz, r.iz, r.lz));
+    far_t = fminf(fminf(fmaf(fx, r.ix, r.hx), fmaf(fy, r.iy, r.hy)), fmaf(fz, r.iz, r.hz));
+}

@@ -140,6 +140,7 @@ struct KernelArgs {
     uint32_t sphere_always;   // slots [0, sphere_always) are swept brute force
     uint32_t sphere_nodes;    // BVH nodes over the remaining slots (0: none)
     uint32_t sphere_octant_stride;  // nodes per direction-ordered layout (0: one layout, order_bvh_by_octant)
+    uint32_t sphere_boxes_ordered;  // 1: the 8 layouts store boxes as (near, far) corners (slab_hit_ordered)
     float sphere_extent;      // max |centre| + radius over BVH spheres (margin scale)
     float sphere_rmin, sphere_rmax;  // radius range over BVH spheres (culling bounds, rt_bvh_slab.h)
     uint32_t tri_nodes;       // triangle BVH nodes (0 with tri_accel: nothing to hit)

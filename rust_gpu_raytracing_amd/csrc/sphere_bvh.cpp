@@ -177,7 +177,15 @@ void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, u
     *leaf_order = std::move(b.leaf_order);
 }
 
-void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out) {
+bool box_layout_orderable(const std::vector<SphereBvhNode>& nodes) {
+    for (const SphereBvhNode& nd : nodes)
+        for (int k = 0; k < 3; k++)
+            if (!(nd.bmin[k] <= nd.bmax[k]) || !(std::fabs(nd.bmin[k]) <= 1e8f) || !(std::fabs(nd.bmax[k]) <= 1e8f))
+                return false;
+    return true;
+}
+
+void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out, bool swap_boxes) {
     out->clear();
     const uint32_t n = (uint32_t)in.size();
     if (n == 0) return;
@@ -189,6 +197,9 @@ void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<Spher
         std::function<void(uint32_t)> emit = [&](uint32_t src) {
             const uint32_t at = (uint32_t)out->size();
             out->push_back(in[src]);
+            if (swap_boxes)  // (near corner, far corner) for this octant
+                for (int k = 0; k < 3; k++)
+                    if ((oct >> k) & 1u) std::swap(out->back().bmin[k], out->back().bmax[k]);
             if (in[src].leaf == kSphereBvhInternal) {
                 uint32_t a = src + 1, b = in[src + 1].skip;  // left child, right child
                 int axis = 0;

@@ -59,7 +59,17 @@ void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use
 // and skips absolute); a skip that leaves a layout is 8 * nodes.size(), so
 // "node >= total" ends every walk. Visiting order does not change the result
 // (the lexicographic minimum, conservative pruning).
-void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out);
+// With swap_boxes, layout k also stores every box as (near corner, far corner)
+// for its octant (bmin/bmax swapped on the axes of k's set bits), for the
+// min/max-free slab test (rt_bvh_slab.h: slab_hit_ordered); layout 0 is
+// unchanged either way. Only valid when box_layout_orderable(in).
+void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out,
+                         bool swap_boxes = false);
+
+// Every box is valid (bmin <= bmax) with finite coordinates of magnitude
+// <= 1e8, so that no plane * (1/d, capped at 1e30) overflows: the premise of
+// slab_hit_ordered's equivalence with slab_hit.
+bool box_layout_orderable(const std::vector<SphereBvhNode>& nodes);
 
 // Generic builder: binned-SAH BVH over axis-aligned boxes (lo/hi, 3 floats each
 // per primitive), leaves of at most `leaf_max` primitives. Returns depth-first

@@ -110,6 +110,8 @@ static Res ordered_like(const SphereSlots& sl, V o, V d) {
 // The kernel walks the direction-ordered layouts (order_bvh_by_octant) unless
 // SINGLE_LAYOUT is set: g_oct holds them for the scene under test.
 static std::vector<SphereBvhNode> g_oct;
+static bool g_oct_ordered = false;  // g_oct stores (near, far) corners per octant (box-ordered layouts)
+static long g_slab_diff = 0;        // slab_hit_ordered != slab_hit on the same inputs (must stay 0)
 
 static Res kernel_like(const SphereSlots& sl, V o, V d) {
     float bt = F32_MAX_;
@@ -136,9 +138,14 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
             };
             inv = {nudge(inv.x), nudge(inv.y), nudge(inv.z)};
         }
-        const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);  // the kernel's slab test
+        SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, lateral);  // the kernel's slab test
         const bool oct = !getenv("SINGLE_LAYOUT");
-        if (oct && g_oct.size() != 8 * (size_t)n) order_bvh_by_octant(sl.nodes, &g_oct);
+        if (oct && g_oct.size() != 8 * (size_t)n) {
+            // the sphere-only kernels' layouts: boxes as (near, far) corners when exact
+            g_oct_ordered = !getenv("UNORDERED_BOXES") && box_layout_orderable(sl.nodes);
+            order_bvh_by_octant(sl.nodes, &g_oct, g_oct_ordered);
+        }
+        if (oct && g_oct_ordered) slab_pair_by_octant(sr);
         const SphereBvhNode* nodes = oct ? g_oct.data() : sl.nodes.data();
         const uint32_t total = oct ? 8 * n : n;
         uint32_t node = oct ? n * ((std::signbit(inv.x) ? 1u : 0u) | (std::signbit(inv.y) ? 2u : 0u) |
@@ -149,6 +156,14 @@ static Res kernel_like(const SphereSlots& sl, V o, V d) {
             const SphereBvhNode& nd = nodes[node];
             float near_t, far_t;
             slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], near_t, far_t);
+            if (oct && g_oct_ordered) {  // what the sphere-only kernels compute: must be the same values
+                float n2, f2;
+                slab_hit_ordered(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], n2, f2);
+                if (!(n2 == near_t || (n2 != n2 && near_t != near_t)) || !(f2 == far_t || (f2 != f2 && far_t != far_t)))
+                    g_slab_diff++;
+                near_t = n2;
+                far_t = f2;
+            }
             bool hit = near_t <= far_t && far_t >= -slack && near_t <= bt * 1.00001f + slack;
             if (hit && nd.leaf != kSphereBvhInternal) {
                 uint32_t first = nd.leaf & 0xffffffu, cnt = nd.leaf >> 24;
@@ -195,7 +210,8 @@ static int replay(const char* rays_path, const char* sph_path) {
         printf("node visits per ray: p10 %u p50 %u p90 %u p99 %u max %u\n", pct(0.1), pct(0.5), pct(0.9), pct(0.99),
                visits.back());
     }
-    return bad ? 1 : 0;
+    if (g_slab_diff) printf("slab_hit_ordered differs from slab_hit on %ld box tests\n", g_slab_diff);
+    return (bad || g_slab_diff) ? 1 : 0;
 }
 
 int main(int argc, char** argv) {
@@ -276,6 +292,7 @@ int main(int argc, char** argv) {
         }
         hits += a.idx >= 0;
     }
-    printf("ok %ld %ld %.1f %zu\n", n_rays, hits, (double)g_tests / n_rays, s.size());
+    if (g_slab_diff) { printf("slab_hit_ordered differs from slab_hit on %ld box tests\n", g_slab_diff); return 1; }
+    printf("ok %ld %ld %.1f %zu ordered_boxes %d\n", n_rays, hits, (double)g_tests / n_rays, s.size(), (int)g_oct_ordered);
     return 0;
 }

@@ -31,8 +31,16 @@ def harness(tmp_path_factory):
 def test_bvh_matches_brute_force(harness, seed):
     out = subprocess.run([str(harness), "400000", str(seed)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
-    _, n, hits, avg_tests, n_spheres = out.stdout.split()
+    _, n, hits, avg_tests, n_spheres, _, ordered = out.stdout.split()
     assert float(avg_tests) < 0.1 * int(n_spheres)  # the culling actually culls
+    assert ordered == "1"  # the sphere-only kernels' box-ordered layouts (slab_hit_ordered) were walked
+
+
+def test_bvh_unordered_boxes(harness):
+    """The octant layouts with bmin/bmax kept (scenes with objects, RT_SPHERE_BOX_ORDER=0) and slab_hit."""
+    env = dict(os.environ, UNORDERED_BOXES="1")
+    out = subprocess.run([str(harness), "200000", "5"], capture_output=True, text=True, env=env)
+    assert out.returncode == 0 and out.stdout.startswith("ok") and out.stdout.split()[-1] == "0", out.stdout
 
 
 def test_bvh_with_one_ulp_reciprocals(harness):
