@@ -773,115 +773,6 @@ __device__ __forceinline__ uint32_t unit_tile(const KernelArgs& ka, uint32_t pos
     return ka.tile_order ? ka.tile_order[q] : q;
 }
 
-// Drain pool (frame-parallel batches; KernelArgs::pool_*). Once the tile queue
-// is empty a wave cannot refill, and its lanes go idle one by one while every
-// iteration still costs a whole wave. Between two rays (every live lane has
-// shaded, none traverses) a path's state is 20 words, the same wherever it
-// continues: a wave with at most pool_push live paths stores them in its XCD's
-// pool and goes idle, and a wave with idle lanes takes paths from it. A path
-// runs the same operations on the same values on any lane, so the image is
-// unchanged. Every pool has one {tail, head} pair: a push reserves entries at
-// tail, a take claims [head, head + n) with a compare-and-swap bounded by tail
-// and waits for each claimed entry's flag (its writer is running), clears it
-// once read. Termination: a wave leaves only after a take found the pool empty
-// (it then holds no path), and every pusher takes right after pushing, so the
-// pool is empty when the last wave of the XCD leaves. Pools are per XCD (the
-// wave's HW_REG_XCC_ID): producer and consumer share one L2, so the entry's
-// stores are visible once they are acknowledged (s_waitcnt) and the reads
-// bypass only the CU's L1 (device-scope loads). Capacity >= the launch's lanes
-// bounds the entries in a pool, so a slot is rewritten only after it was read.
-__device__ __forceinline__ void pool_wait(uint32_t* f, uint32_t want) {
-    uint32_t n = 0;  // bounded: a fault shows up as a wrong image, never as a hang
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want && ++n < (1u << 22))
-        __builtin_amdgcn_s_sleep(2);
-}
-
-__device__ __forceinline__ void pool_settle() {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);  // every outstanding memory operation of the wave has completed
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ void pool_exchange(const KernelArgs& ka, bool live, uint32_t& mode, Path& p,
-                                           uint32_t& index, uint32_t& sample, uint32_t& frame,
-                                           uint32_t& lane_tile, uint32_t& lane_slot) {
-    constexpr uint32_t kIdle = 0, kSetup = 1;  // the kernel's lane states
-    const uint32_t x = xcc_id() & 7u;
-    const size_t cap = (size_t)ka.pool_mask + 1u;
-    uint32_t* tail = ka.pool_ctl + x * kPoolCtlStride;
-    uint32_t* head = tail + 16;
-    float4* data = ka.pool_data + (size_t)x * 5u * cap;
-    uint32_t* flag = ka.pool_flag + (size_t)x * cap;
-    const uint32_t lane = threadIdx.x & 63u;
-
-    const uint64_t lm = __ballot(live);
-    const uint32_t n_live = (uint32_t)__popcll(lm);
-    if (n_live != 0u && n_live <= ka.pool_push) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(tail, n_live);
-        base = __builtin_amdgcn_readlane(base, 0);
-        if (live) {
-            const uint32_t slot = (base + lane_rank(lm)) & ka.pool_mask;
-            pool_wait(flag + slot, 0u);
-            float4* e = data + (size_t)slot * 5u;
-            e[0] = make_float4(p.o.x, p.o.y, p.o.z, p.d.x);
-            e[1] = make_float4(p.d.y, p.d.z, p.light.x, p.light.y);
-            e[2] = make_float4(p.light.z, p.light.w, p.contrib.x, p.contrib.y);
-            e[3] = make_float4(p.contrib.z, p.contrib.w, __uint_as_float(p.seed), __uint_as_float(p.bounce));
-            e[4] = make_float4(__uint_as_float(index), __uint_as_float(sample), __uint_as_float((frame << 6) | lane_slot),
-                               __uint_as_float(lane_tile));
-            pool_settle();
-            __hip_atomic_store(flag + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mode = kIdle;
-        }
-    }
-
-    const uint64_t im = __ballot(mode == kIdle);
-    const uint32_t n_idle = (uint32_t)__popcll(im);
-    if (n_idle == 0u) return;
-    uint32_t h = 0, take = 0;
-    if (lane == 0) {
-        for (uint32_t tries = 0; tries < (1u << 20); ++tries) {
-            h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            take = min(t - h, n_idle);
-            if (take == 0u || atomicCAS(head, h, h + take) == h) break;
-            take = 0u;
-        }
-    }
-    h = __builtin_amdgcn_readlane(h, 0);
-    take = __builtin_amdgcn_readlane(take, 0);
-    if (take == 0u || mode != kIdle) return;
-    const uint32_t r = lane_rank(im);
-    if (r >= take) return;
-    const uint32_t slot = (h + r) & ka.pool_mask;
-    pool_wait(flag + slot, 1u);
-    uint64_t* e = reinterpret_cast<uint64_t*>(data + (size_t)slot * 5u);
-    uint64_t w[10];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) w[i] = __hip_atomic_load(e + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pool_settle();
-    __hip_atomic_store(flag + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    auto lo = [&](int i) { return __uint_as_float((uint32_t)w[i]); };
-    auto hi = [&](int i) { return __uint_as_float((uint32_t)(w[i] >> 32)); };
-    p.o = mk(lo(0), hi(0), lo(1));
-    p.d = mk(hi(1), lo(2), hi(2));
-    p.light = f4{lo(3), hi(3), lo(4), hi(4)};
-    p.contrib = f4{lo(5), hi(5), lo(6), hi(6)};
-    p.seed = (uint32_t)w[7];
-    p.bounce = (uint32_t)(w[7] >> 32);
-    index = (uint32_t)w[8];
-    sample = (uint32_t)(w[8] >> 32);
-    frame = (uint32_t)w[9] >> 6;
-    lane_slot = (uint32_t)w[9] & 63u;
-    lane_tile = (uint32_t)(w[9] >> 32);
-    mode = kSetup;
-}
-
 // Cost-ordered schedule support: adds the rays of the pixels this wave just
 // finished to their tiles' counters. Finished lanes almost always share one or
 // two tiles, so this is one wave reduction and one atomic per distinct tile.
@@ -1223,11 +1114,6 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             }
         }
         if (ka.tile_cost) record_tile_cost(ka.tile_cost, fin, lane_tile, fin_rays);
-        // 1b. Drain pool: with the queue empty and every live lane between two
-        // rays, hand sparse waves' paths to the XCD's pool and fill idle lanes
-        // from it.
-        if (ka.pool_push != 0u && tile >= ka.owned_tiles && __ballot(mode == kTrav || mode == kDone) == 0)
-            pool_exchange(ka, mode == kSetup, mode, p, index, sample, frame, lane_tile, lane_slot);
 #ifdef RT_DIAG
         const unsigned long long ts1 = stamp();
         shade_cyc += ts1 - ts0;

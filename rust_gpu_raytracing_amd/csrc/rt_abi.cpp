@@ -94,7 +94,6 @@ uint32_t leaf_batch_for(int lds_mode) { return lds_mode == 2 ? 6 : 5; }
 // has finished and after at least kDefaultDrainMinSteps traversal steps
 // (threshold 0: traverse to the end, as the other instances do).
 constexpr uint32_t kDefaultDrainThreshold = 32;
-constexpr uint32_t kDefaultPoolPush = 0;  // drain pool off until measured (RT_POOL_PUSH)
 constexpr uint32_t kDefaultDrainMinSteps = 64;
 // Tile claim order: 0 = tile index order, 1 = cost-ordered (most rays first,
 // sorted on the device from the previous frame's per-tile ray counts).
@@ -176,11 +175,6 @@ struct rt_ctx {
     uint32_t drain_threshold = kDefaultDrainThreshold;  // RT_DRAIN_THRESHOLD (A/B switch)
     uint32_t drain_min_steps = kDefaultDrainMinSteps;   // RT_DRAIN_MIN_STEPS (A/B switch)
     uint32_t leaf_batch = 0;  // RT_LEAF_BATCH, in eighths (A/B switch); 0 = by scene (leaf_batch_for)
-    // drain pool (KernelArgs::pool_*), per stream: 8 XCD pools of pool_cap entries
-    uint32_t pool_push = kDefaultPoolPush;  // RT_POOL_PUSH (A/B switch); 0 = off
-    float4* d_pool_data[2] = {};
-    uint32_t* d_pool_flag[2] = {};   // pool_cap x 8 flags, then the 8 XCDs' {tail, head} counters
-    uint32_t pool_cap[2] = {};
     // cost-ordered tile schedule (rt_set_tile_schedule), double-buffered by
     // launch parity: launch L records costs[L&1], reads order[L&1], and its
     // first idle workgroup sorts costs[~L&1] (launch L-1's) into order[~L&1]
@@ -636,8 +630,6 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->drain_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
         env = std::getenv("RT_DRAIN_MIN_STEPS");
         if (env) ctx->drain_min_steps = (uint32_t)std::strtoul(env, nullptr, 10);
-        env = std::getenv("RT_POOL_PUSH");
-        if (env) ctx->pool_push = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
         env = std::getenv("RT_LEAF_BATCH");
         if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_TILE_SCHEDULE");
@@ -720,7 +712,6 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
-                    ctx->d_pool_data[0], ctx->d_pool_data[1], ctx->d_pool_flag[0], ctx->d_pool_flag[1],
                     ctx->d_clock};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1143,38 +1134,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.queue = ctx->d_queue + (size_t)(2 * si + ctx->queue_parity[si]) * kQueueStripesMax * kQueueStride;
     ka.queue_next = ctx->d_queue + (size_t)(2 * si + (ctx->queue_parity[si] ^ 1u)) * kQueueStripesMax * kQueueStride;
     if (frame_par) ka.frame_light = ctx->d_frame_light[ctx->batches & 1u];
-    ka.pool_data = nullptr;
-    ka.pool_flag = ka.pool_ctl = nullptr;
-    ka.pool_mask = ka.pool_push = 0;
-    if (frame_par && ctx->pool_push) {
-        // Drain pool: one per XCD and stream (a stream's launches run one after
-        // another and leave their pools empty); capacity a power of two >= every
-        // lane of the launch, so a slot is reused only after its entry was read.
-        uint32_t cap = 64;
-        while (cap < blocks * ctx->occ_threads) cap *= 2;
-        if (cap > ctx->pool_cap[si]) {
-            if (ctx->d_pool_data[si]) RT_HIP(ctx, hipFree(ctx->d_pool_data[si]));
-            if (ctx->d_pool_flag[si]) RT_HIP(ctx, hipFree(ctx->d_pool_flag[si]));
-            ctx->d_pool_data[si] = nullptr;
-            ctx->d_pool_flag[si] = nullptr;
-            ctx->pool_cap[si] = 0;
-            int rc = dev_alloc(ctx, &ctx->d_pool_data[si], (size_t)8 * 5 * cap);
-            if (!rc) rc = dev_alloc(ctx, &ctx->d_pool_flag[si], (size_t)8 * cap + 8 * kPoolCtlStride);
-            if (rc) return rc;
-            RT_HIP(ctx, hipMemsetAsync(ctx->d_pool_flag[si], 0, ((size_t)8 * cap + 8 * kPoolCtlStride) * 4, ctx->stream));
-            ctx->primary_dirty = true;
-            if (si) {
-                RT_HIP(ctx, hipEventRecord(ctx->ev_primary, ctx->stream));
-                RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_primary, 0));
-            }
-            ctx->pool_cap[si] = cap;
-        }
-        ka.pool_data = ctx->d_pool_data[si];
-        ka.pool_flag = ctx->d_pool_flag[si];
-        ka.pool_ctl = ctx->d_pool_flag[si] + (size_t)8 * ctx->pool_cap[si];
-        ka.pool_mask = ctx->pool_cap[si] - 1u;
-        ka.pool_push = ctx->pool_push;
-    }
     if (sched) {
         const size_t n = ctx->owned_tiles;
         uint32_t*& state = ctx->d_tile_sched[si];

@@ -92,9 +92,6 @@ constexpr uint32_t kOrderBuckets = RT_ORDER_BUCKETS;
 constexpr size_t kLdsTailBytes = 1024 + 160;
 static_assert(kLdsTailBytes >= (kOrderBuckets * 16 + 1) * 4, "sort scratch fits the LDS tail");
 
-// drain pool counters: XCD x's {tail, head} at pool_ctl[x * kPoolCtlStride + {0, 16}]
-constexpr uint32_t kPoolCtlStride = 32;
-
 struct KernelArgs {
     // framebuffer (bindings 1, 2, 6)
     const float4* __restrict__ camera_rays;
@@ -160,17 +157,6 @@ struct KernelArgs {
     float4* __restrict__ frame_light;
     uint32_t queue_units;
     uint32_t unit_tile_major;  // frame-parallel units: 1 = a tile's frames consecutive, 0 = frame-major
-    // Drain pool (frame-parallel batches, pathtrace.hip "drain pool"): once the
-    // tile queue is empty, waves with at most pool_push live paths hand them to
-    // their XCD's pool and waves with idle lanes take them, so the drain runs on
-    // fewer, fuller waves. Per XCD: pool_cap entries of 5 float4 (pool_data), a
-    // full/free flag each (pool_flag), {tail, head} counters 128 B apart
-    // (pool_ctl, monotone, never reset). Null / 0 = off.
-    float4* __restrict__ pool_data;
-    uint32_t* __restrict__ pool_flag;
-    uint32_t* __restrict__ pool_ctl;
-    uint32_t pool_mask;  // pool_cap - 1 (a power of two >= the launch's lanes)
-    uint32_t pool_push;
     // launch timing (rt_set_timing), null otherwise: {~earliest workgroup start, latest
     // workgroup end} on the device wall clock
     unsigned long long* __restrict__ launch_clock;
