@@ -17,7 +17,7 @@ for s in $STEPS; do
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     all)   timeout -k 10 600 python3 tools/bench_all.py --no-cpu --frames 20 > "$OUT/bench_all.jsonl" 2> "$OUT/bench_all.err" ;;
-    strong) timeout -k 10 300 python3 tools/strong_probe.py > "$OUT/strong_probe.jsonl" 2> "$OUT/strong_probe.err" ;;
+    strong) timeout -k 10 300 python3 tools/strong_probe.py --steps 20 > "$OUT/strong_probe.jsonl" 2> "$OUT/strong_probe.err" ;;
     prof)  bash tools/profile.sh "$TAG" ;;  # then locally: python tools/update_traffic.py gpurun_out/prof_<tag> profiles/<tag>
     multi) # N-rank rehearsal on the one GPU of the box (gloo; the real run is RCCL, one GPU per rank)
            for n in 2 4 8; do

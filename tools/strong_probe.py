@@ -8,7 +8,8 @@ turn, with the bench's settings (bench.default_frame_batch(N, steps), same steps
 the slowest rank's render time per frame, the predicted whole-job Mray/s (all
 ranks' rays / the slowest rank's time, as bench.py computes `value`), and the
 predicted parallel efficiency against N=1 without and with a measured estimate
-of the gather (pack + the bytes rank 0 receives, priced at --link-gbs).
+of the gather (pack + unpack + the bytes rank 0 receives, priced at --link-gbs,
++ 2 x 50 us of collective latency), for the payload bench.py gathers (--gather).
 
 usage: python tools/strong_probe.py [--steps 20] [--warmup 3] [--settle-ms 150] [--ns 1 2 4 8]
 """
@@ -25,7 +26,7 @@ from rust_gpu_raytracing_amd import Renderer  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
 
-def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms):
+def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms, what="image"):
     import torch
 
     with Renderer(scene, rank=rank, world_size=world, frame_batch=fb) as r:
@@ -50,15 +51,21 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms):
         span_ms, n_launch = r.dispatch_time_total()
         rays = r.ray_count()
         launch = r.launch_config()
-        # the device half of the gather: pack this rank's accumulation
+        # the device half of the gather: pack this rank's share (the bench's payload: the RGBA8
+        # image, 4 B/px, or the accumulation, 16 B/px), averaged over 20 back-to-back packs so the
+        # host round trip of one synchronize does not count as pack time
         n = r.owned_pixel_count()
-        buf = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+        words = 4 if what == "accumulation" else 1
+        buf = torch.empty((n, words), dtype=torch.float32 if words == 4 else torch.int32, device="cuda")
+        pack = r.pack_owned_accumulation if what == "accumulation" else r.pack_owned_output
+        pack(buf.data_ptr())
         r.synchronize()
         p0 = time.perf_counter()
-        r.pack_owned_accumulation(buf.data_ptr())
+        for _ in range(20):
+            pack(buf.data_ptr())
         r.synchronize()
-        t_pack = time.perf_counter() - p0
-    return t, rays, t_pack, n * 16, t_submit, span_ms, n_launch, launch
+        t_pack = (time.perf_counter() - p0) / 20
+    return t, rays, t_pack, n * 4 * words, t_submit, span_ms, n_launch, launch
 
 
 def main():
@@ -69,6 +76,8 @@ def main():
     ap.add_argument("--ns", type=int, nargs="*", default=[1, 2, 4, 8])
     ap.add_argument("--settle-ms", type=float, default=150.0, help="as bench.py --settle-ms")
     ap.add_argument("--frame-batch", type=int, default=0, help="override bench.default_frame_batch(N)")
+    ap.add_argument("--gather", choices=["image", "accumulation"], default="image",
+                    help="the gather payload priced (bench.py --gather; default image, 4 B/px)")
     ap.add_argument("--link-gbs", type=float, default=50.0,
                     help="xGMI bandwidth one peer achieves into rank 0 (GB/s, per link; 7 links)")
     args = ap.parse_args()
@@ -76,11 +85,12 @@ def main():
     base = None
     for n in args.ns:
         fb = args.frame_batch or bench.default_frame_batch(n, args.steps)
-        per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms) for r in range(n)]
+        per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms, args.gather) for r in range(n)]
         t_max = max(p[0] for p in per)
         rays = sum(p[1] for p in per)
         # gather estimate: packs run in parallel (max), rank 0 receives N-1 blocks over N-1 links
-        t_gather = (max(p[2] for p in per) + (max(p[3] for p in per) / (args.link_gbs * 1e9)) + 2 * 50e-6) if n > 1 else 0.0
+        # (pack on every rank, then rank 0's unpack of about as many bytes: priced as a second pack)
+        t_gather = (2 * max(p[2] for p in per) + (max(p[3] for p in per) / (args.link_gbs * 1e9)) + 2 * 50e-6) if n > 1 else 0.0
         v = rays / t_max / 1e6
         vg = rays / (t_max + t_gather) / 1e6
         if base is None:
@@ -93,7 +103,8 @@ def main():
             "host_submit_ms_max": max(p[4] for p in per) * 1e3,
             "kernel_span_ms_per_rank": [round(p[5], 4) for p in per], "launches": per[0][6],
             "wall_ms_per_rank": [round(p[0] * 1e3, 4) for p in per],
-            "steps": args.steps, "launch": per[0][7],
+            "steps": args.steps, "launch": per[0][7], "gather_payload": args.gather,
+            "pack_ms_max": max(p[2] for p in per) * 1e3,
         }), flush=True)
 
 
