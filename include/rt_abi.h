@@ -315,6 +315,11 @@ RT_API int rt_last_dispatch_ms(rt_ctx* ctx, float* out_ms);
  * launches were timed (read back in bulk on this call, so timing a long run adds
  * no host sync per frame). */
 RT_API int rt_dispatch_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed);
+/* The same for the resolve pass of timed frame-parallel batches
+ * (rt_resolve_frames_kernel: each pixel's lights added to its accumulation in
+ * frame order, the last frame's RGBA8 packed), which the path kernel's span above
+ * does not include. n_timed counts the batches that had one. */
+RT_API int rt_resolve_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed);
 RT_API int rt_reset_timing(rt_ctx* ctx);
 
 /* Multi-GPU gather support. The pixels owned by this context's

@@ -121,6 +121,7 @@ SIGNATURES = {
     "rt_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "rt_last_dispatch_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_dispatch_time_total": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_resolve_time_total": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
     "rt_reset_timing": (ctypes.c_int, [_P]),
     "rt_owned_pixel_count": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_pack_owned_accumulation": (ctypes.c_int, [_P, _P]),

@@ -1275,8 +1275,8 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         atomicMax(ka.diag + 7, wave_t1 - wave_t0);
         const uint32_t w = blockIdx.x * (kThreads / 64u) + (threadIdx.x >> 6);
         if (w < 65536u) {
-            ka.diag[8 + 2 * w] = wave_dry ? wave_dry : wave_t1;  // queue dry (tools/tail_probe.py)
-            ka.diag[8 + 2 * w + 1] = wave_t1;
+            ka.diag[kDiagHeaderWords + 2 * w] = wave_dry ? wave_dry : wave_t1;  // queue dry (tools/tail_probe.py)
+            ka.diag[kDiagHeaderWords + 2 * w + 1] = wave_t1;
         }
     }
 #endif
@@ -1428,10 +1428,10 @@ extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(
 // -- so the sum is bit-identical to the frames rendered one after another; then
 // the accumulation and the last frame's packed output (:166-178). One thread per
 // owned pixel slot, coalesced: HBM-bound (16 + 16 * frames * samples + 20 B/px).
-extern "C" __global__ void __launch_bounds__(256) rt_resolve_frames_kernel(
-    float4* __restrict__ accum, uint32_t* __restrict__ output, const float4* __restrict__ light, uint32_t width,
-    uint32_t height, uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
-    uint32_t samples, uint32_t frames) {
+__device__ __forceinline__ void resolve_pixel(float4* __restrict__ accum, uint32_t* __restrict__ output,
+                                              const float4* __restrict__ light, uint32_t width, uint32_t height,
+                                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world,
+                                              uint32_t k0, uint32_t samples, uint32_t frames) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t owned_px = (uint64_t)owned_tiles * 64u;
     if (gid >= owned_px) return;
@@ -1455,13 +1455,26 @@ extern "C" __global__ void __launch_bounds__(256) rt_resolve_frames_kernel(
     output[idx] = pack_rgba8(clamp01(pix.x / div), clamp01(pix.y / div), clamp01(pix.z / div), clamp01(pix.w / div));
 }
 
+extern "C" __global__ void __launch_bounds__(256) rt_resolve_frames_kernel(
+    float4* __restrict__ accum, uint32_t* __restrict__ output, const float4* __restrict__ light, uint32_t width,
+    uint32_t height, uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
+    uint32_t samples, uint32_t frames, unsigned long long* __restrict__ clock) {
+    // clock (rt_set_timing): {~earliest workgroup start, latest workgroup end}
+    if (clock && threadIdx.x == 0) atomicMax(clock, ~(unsigned long long)wall_clock64());
+    resolve_pixel(accum, output, light, width, height, tiles_x, owned_tiles, rank, world, k0, samples, frames);
+    if (clock) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(clock + 1, (unsigned long long)wall_clock64());
+    }
+}
+
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
-                             uint32_t samples, uint32_t frames, hipStream_t stream) {
+                             uint32_t samples, uint32_t frames, unsigned long long* clock, hipStream_t stream) {
     const uint64_t threads = (uint64_t)owned_tiles * 64u;
     const uint32_t blocks = (uint32_t)((threads + 255u) / 256u);
     hipLaunchKernelGGL(rt_resolve_frames_kernel, dim3(blocks), dim3(256), 0, stream, accum, output, light, width,
-                       height, tiles_x, owned_tiles, rank, world, k0, samples, frames);
+                       height, tiles_x, owned_tiles, rank, world, k0, samples, frames, clock);
     return hipGetLastError();
 }
 

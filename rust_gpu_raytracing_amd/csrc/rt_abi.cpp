@@ -38,7 +38,7 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            hipStream_t stream);
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
-                             uint32_t samples, uint32_t frames, hipStream_t stream);
+                             uint32_t samples, uint32_t frames, unsigned long long* clock, hipStream_t stream);
 hipError_t rt_launch_pack_output(uint32_t* output, uint32_t* packed, uint32_t width, uint32_t height, uint32_t tiles_x,
                                  uint32_t n_tiles, uint32_t first_rank, uint32_t ranks, uint32_t world,
                                  uint64_t stride_px, uint32_t skip_rank, bool unpack, hipStream_t stream);
@@ -64,9 +64,12 @@ namespace {
 
 constexpr size_t kLdsSceneBudget = 64 * 1024;    // mode 1: spheres/materials/objects/sphere BVH per workgroup
 constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerator (one 1024-thread workgroup per CU)
-// Diagnostic builds (-DRT_DIAG_TAIL) record (start, end) per wave after the 8
-// counters: room for 65,536 waves.
+// d_counter: [0] the ray counter, [1, 1 + kDiagCounters) the diagnostic
+// counters of RT_DIAG / RT_DIAG_TAIL builds (KernelArgs::diag), then the
+// per-wave (queue dry, end) records of RT_DIAG_TAIL builds: room for 65,536 waves.
+constexpr size_t kDiagCounters = kDiagHeaderWords;
 constexpr size_t kDiagWaveRecords = 2 * 65536;
+constexpr size_t kCounterWords = 1 + kDiagCounters + kDiagWaveRecords;
 // Tile queue: counters per stripe (pathtrace.hip, claim_tile), 256 B apart;
 // kQueueStripes = 4 per XCD by default (measured: C2 0.599 ms at 8, 0.595 at 32; C1
 // 0.076 -> 0.058 ms), up to kQueueStripesMax (RT_QUEUE_STRIPES).
@@ -115,6 +118,7 @@ void rt_set_global_error(const std::string& msg) { g_create_error = msg; }
 namespace {
 
 constexpr uint32_t kClockSlots = 4096;
+constexpr uint32_t kClockWords = 4;  // per timed launch: path kernel {~start, end}, resolve kernel {~start, end}
 
 }  // namespace
 
@@ -252,12 +256,14 @@ struct rt_ctx {
     // clock -- the first workgroup's start to the last one's end (s_memrealtime) --
     // in a ring of slots read back in bulk; HIP events would time each launch from
     // the moment its stream reached it, which overlapped batches make meaningless
-    unsigned long long* d_clock = nullptr;  // kClockSlots x {~min start, max end}
+    unsigned long long* d_clock = nullptr;  // kClockSlots x {path: ~min start, max end; resolve: the same}
     std::vector<uint32_t> clock_pending;    // slots of timed launches not yet read back
     uint32_t clock_next = 0;
     double wall_khz = 100000.0;             // device wall clock rate (hipDeviceAttributeWallClockRate)
     double total_ms = 0.0;
     uint64_t n_timed = 0;
+    double resolve_total_ms = 0.0;  // rt_resolve_frames_kernel spans of the timed batches
+    uint64_t n_resolve_timed = 0;
     float last_ms = 0.0f;
 
     std::string err;
@@ -515,16 +521,23 @@ int dev_alloc(rt_ctx* ctx, T** p, size_t count) {
 int collect_timing(rt_ctx* ctx) {
     if (ctx->clock_pending.empty()) return RT_OK;
     RT_HIP(ctx, join_aux(ctx));
-    std::vector<unsigned long long> c(2 * (size_t)kClockSlots);
+    std::vector<unsigned long long> c(kClockWords * (size_t)kClockSlots);
     RT_HIP(ctx, hipMemcpyAsync(c.data(), ctx->d_clock, c.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (uint32_t slot : ctx->clock_pending) {
-        const unsigned long long t0 = ~c[2 * (size_t)slot], t1 = c[2 * (size_t)slot + 1];
-        if (c[2 * (size_t)slot] == 0 || t1 < t0) continue;  // no workgroup ran
-        const float ms = (float)((double)(t1 - t0) / ctx->wall_khz);
-        ctx->total_ms += ms;
-        ctx->n_timed += 1;
-        ctx->last_ms = ms;
+        const unsigned long long* w = c.data() + kClockWords * (size_t)slot;
+        const unsigned long long t0 = ~w[0], t1 = w[1];
+        if (w[0] != 0 && t1 >= t0) {  // else no workgroup ran
+            const float ms = (float)((double)(t1 - t0) / ctx->wall_khz);
+            ctx->total_ms += ms;
+            ctx->n_timed += 1;
+            ctx->last_ms = ms;
+        }
+        const unsigned long long r0 = ~w[2], r1 = w[3];
+        if (w[2] != 0 && r1 >= r0) {  // the batch's resolve pass
+            ctx->resolve_total_ms += (double)(r1 - r0) / ctx->wall_khz;
+            ctx->n_resolve_timed += 1;
+        }
     }
     ctx->clock_pending.clear();
     return RT_OK;
@@ -667,7 +680,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
     ctx->k = 1;  // src/renderer.rs:96
 
     if ((rc = dev_alloc(ctx, &ctx->d_rays, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_accum, n_pixels)) ||
-        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, 9 + kDiagWaveRecords)) ||
+        (rc = dev_alloc(ctx, &ctx->d_out, n_pixels)) || (rc = dev_alloc(ctx, &ctx->d_counter, kCounterWords)) ||
         (rc = dev_alloc(ctx, &ctx->d_queue, 4 * kQueueStripesMax * kQueueStride)) ||  // 2 streams x 2 halves
         (rc = dev_alloc(ctx, &ctx->d_slot_sph, 4 * (size_t)info->sphere_count + 4)) ||  // padded groups
         (rc = dev_alloc(ctx, &ctx->d_slot_orig, 4 * (size_t)info->sphere_count + 4)) ||
@@ -1162,7 +1175,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             if (rc) return rc;
         }
         if (!ctx->d_clock) {
-            const int rc = dev_alloc(ctx, &ctx->d_clock, 2 * (size_t)kClockSlots);
+            const int rc = dev_alloc(ctx, &ctx->d_clock, kClockWords * (size_t)kClockSlots);
             if (rc) return rc;
             if (si) {  // the zeroed slots must be in place before an aux launch
                 RT_HIP(ctx, hipEventRecord(ctx->ev_primary, ctx->stream));
@@ -1171,8 +1184,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         const uint32_t slot = ctx->clock_next;
         ctx->clock_next = (ctx->clock_next + 1) % kClockSlots;
-        ka.launch_clock = ctx->d_clock + 2 * (size_t)slot;
-        RT_HIP(ctx, hipMemsetAsync(ka.launch_clock, 0, 16, S));
+        ka.launch_clock = ctx->d_clock + kClockWords * (size_t)slot;
+        RT_HIP(ctx, hipMemsetAsync(ka.launch_clock, 0, kClockWords * 8, S));
         ctx->clock_pending.push_back(slot);
     }
     hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, S);
@@ -1184,7 +1197,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         if (ctx->batches > 0) RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_resolved[(ctx->batches - 1) & 1u], 0));
         e = rt_launch_resolve(ctx->d_accum, ctx->d_out, ka.frame_light, ctx->width, ctx->height, ctx->tiles_x,
                               ctx->owned_tiles, ctx->rank, ctx->world, p.accumulation_index, p.compute_per_frame,
-                              frames, S);
+                              frames, ka.launch_clock ? ka.launch_clock + 2 : nullptr, S);
         if (e != hipSuccess) return hip_fail(ctx, "rt_resolve_frames_kernel launch", e);
         RT_HIP(ctx, hipEventRecord(ctx->ev_resolved[ctx->batches & 1u], S));
         ctx->batches += 1;
@@ -1195,6 +1208,10 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         RT_HIP(ctx, hipEventRecord(ctx->ev_aux_done, S));
         ctx->aux_outstanding = true;
     }
+    // A plain launch (not frame-parallel) reads and writes the accumulation and
+    // the output on the primary stream; a later overlapped batch on the auxiliary
+    // stream must follow it (its resolve writes both), not just the previous batch.
+    if (!frame_par) ctx->primary_dirty = true;
     if (sched) ++ctx->sched_launches[si];
     return RT_OK;
 }
@@ -1452,7 +1469,7 @@ int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
 
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, 9 * sizeof(unsigned long long), ctx->stream));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters) * sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }
 
@@ -1487,12 +1504,24 @@ int rt_dispatch_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed) {
     return RT_OK;
 }
 
+int rt_resolve_time_total(rt_ctx* ctx, double* total_ms, uint64_t* n_timed) {
+    RT_ENTER(ctx);
+    if (!total_ms || !n_timed) return fail(ctx, RT_E_INVALID, "out is NULL");
+    int rc = collect_timing(ctx);
+    if (rc) return rc;
+    *total_ms = ctx->resolve_total_ms;
+    *n_timed = ctx->n_resolve_timed;
+    return RT_OK;
+}
+
 int rt_reset_timing(rt_ctx* ctx) {
     RT_ENTER(ctx);
     int rc = collect_timing(ctx);
     if (rc) return rc;
     ctx->total_ms = 0.0;
     ctx->n_timed = 0;
+    ctx->resolve_total_ms = 0.0;
+    ctx->n_resolve_timed = 0;
     ctx->last_ms = 0.0f;
     return RT_OK;
 }
@@ -1575,7 +1604,7 @@ int rt_unpack_output_ranks(rt_ctx* ctx, const void* src_device, uint64_t stride_
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n) {
     RT_ENTER(ctx);
     if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
-    const size_t m = std::min<size_t>(n, 8 + kDiagWaveRecords);
+    const size_t m = std::min<size_t>(n, kDiagCounters + kDiagWaveRecords);
     RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_counter + 1, m * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return RT_OK;
@@ -1593,6 +1622,8 @@ int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uin
 
 void* rt_stream(rt_ctx* ctx) {
     if (!ctx) return nullptr;
+    // flush_frames may launch and allocate: on the context's device
+    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
     // work the caller orders on this stream follows every frame submitted so far
     if (flush_frames(ctx) != RT_OK || join_aux(ctx) != hipSuccess) return nullptr;
     ctx->primary_dirty = true;

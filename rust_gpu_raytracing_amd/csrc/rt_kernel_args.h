@@ -92,13 +92,17 @@ constexpr uint32_t kOrderBuckets = RT_ORDER_BUCKETS;
 constexpr size_t kLdsTailBytes = 1024 + 160;
 static_assert(kLdsTailBytes >= (kOrderBuckets * 16 + 1) * 4, "sort scratch fits the LDS tail");
 
+// Diagnostic counters ahead of the per-wave records in KernelArgs::diag
+// (RT_DIAG: 10 counters; RT_DIAG_TAIL: 8, then 2 words per wave from here).
+constexpr uint32_t kDiagHeaderWords = 12;
+
 struct KernelArgs {
     // framebuffer (bindings 1, 2, 6)
     const float4* __restrict__ camera_rays;
     float4* __restrict__ accum;
     uint32_t* __restrict__ output;
     unsigned long long* __restrict__ ray_counter;
-    unsigned long long* __restrict__ diag;          // 8 diagnostic counters (RT_DIAG builds)
+    unsigned long long* __restrict__ diag;          // kDiagHeaderWords counters, then per-wave records (diagnostic builds)
     uint32_t* __restrict__ queue;       // this launch's tile-queue stripe counters (zero at launch start)
     uint32_t* __restrict__ queue_next;  // the next launch's counters, zeroed by this launch
     // cost-ordered tile schedule (pathtrace.hip, sort_tiles_by_cost), null when

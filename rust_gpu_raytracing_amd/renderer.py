@@ -291,9 +291,17 @@ class Renderer:
         self._call("rt_set_timing", int(enable))
 
     def dispatch_time_total(self):
-        """(total milliseconds of timed launches, number timed) — HIP events on the ctx stream."""
+        """(total milliseconds of timed path-kernel launches, number timed): each launch's
+        span on the device clock (rt_set_timing)."""
         ms, n = ctypes.c_double(), ctypes.c_uint64()
         self._call("rt_dispatch_time_total", ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
+    def resolve_time_total(self):
+        """(total milliseconds, number) of the timed batches' resolve passes
+        (rt_resolve_frames_kernel), which dispatch_time_total does not include."""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        self._call("rt_resolve_time_total", ctypes.byref(ms), ctypes.byref(n))
         return ms.value, n.value
 
     def reset_timing(self) -> None:

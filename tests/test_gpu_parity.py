@@ -725,6 +725,30 @@ def test_gpu_overlapped_batches_with_updates(gpu, oracle_lib, monkeypatch, overl
     assert np.array_equal(got[1], out_o) and np.array_equal(got[0].view(np.uint32), acc_o.view(np.uint32))
 
 
+def test_gpu_overlapped_batch_after_plain_launch(gpu, oracle_lib, monkeypatch):
+    """A one-frame flush (a bounce change flushing a single queued frame) is a plain
+    launch on the primary stream that reads and writes the accumulation; the next
+    batch lands on the auxiliary stream and its resolve must wait for that launch too
+    (primary_dirty after a plain launch). Sequence: batches on primary,
+    aux, primary, then 1 frame at b, compute_frame(b + 1) flushing it alone, then a
+    full batch at b + 1 on aux -- against the oracle's single frames."""
+    monkeypatch.setenv("RT_BATCH_OVERLAP", "1")
+    scene, b = build_config("c2_rtiow", width=320, height=184)
+    rays = scene.camera.recalculate_ray_directions()
+    seq = [b] * 13 + [b + 1] * 4
+    with Renderer(scene, camera_rays=rays, frame_batch=4) as r:
+        for bb in seq:
+            r.compute_frame(bb)
+        got = r.read_accumulation(), r.read_output(), r.ray_count()
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc = np.zeros((184, 320, 4), np.float32)
+    out = np.zeros((184, 320), np.uint32)
+    n = 0
+    for i, bb in enumerate(seq):
+        n += o.render_frame(scene.params(accumulation_index=i + 1), bb, acc, out)
+    assert_same(*got, acc, out, n)
+
+
 def _fuzz_scene(seed, w, h, with_tris):
     """A random scene that leans on the culling: clustered and far spheres, tiny and huge
     radii, duplicates and overlaps, every material kind, emitters; camera rays with exact

@@ -8,7 +8,7 @@ TAG=${1:-r01}; shift || true
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 20 --no-cpu-baseline $*"  # warmup = steps: every launch renders 20 frames, so per-launch averages are the timed launches
+BENCH="bench.py --steps 20 --warmup 20 --no-cpu-baseline --no-cadences $*"  # warmup = steps: every launch renders 20 frames, so per-launch averages are the timed launches
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $BENCH > /dev/null 2> "$OUT/pmc_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 $BENCH > /dev/null 2> "$OUT/pmc_write.err"

@@ -17,6 +17,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from rust_gpu_raytracing_amd import Renderer  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
+HEADER = 12  # kDiagHeaderWords (csrc/rt_kernel_args.h): counters ahead of the per-wave records
 argv = sys.argv[1:]
 fb = 1
 rank, world = 0, 1
@@ -42,8 +43,8 @@ for name in argv or ["c2_rtiow"]:
             r.synchronize()
             r.set_timing(False)
             kern_ms, _ = r.dispatch_time_total()
-            c = r.debug_counters(8 + 2 * 65536)
-            waves = np.array(c[8:8 + 2 * c[3]], np.float64).reshape(-1, 2)
+            c = r.debug_counters(HEADER + 2 * 65536)
+            waves = np.array(c[HEADER:HEADER + 2 * c[3]], np.float64).reshape(-1, 2)
             t_first = (~np.uint64(c[2])).item()  # stored as the max of ~start
             dry = (waves[:, 0] - t_first) / 100.0   # when the wave first found the queue empty
             dur = (waves[:, 1] - waves[:, 0]) / 100.0  # its drain: queue dry -> wave end
