@@ -179,6 +179,10 @@ def main() -> int:
     ap.add_argument("--gather", choices=["image", "accumulation"], default="image",
                     help="N>1: the payload of the gather in the timed region: the displayed RGBA8 frame "
                          "(4 B/px) or the RGBA32F accumulation (16 B/px)")
+    ap.add_argument("--driver", choices=["torch", "group"], default="torch",
+                    help="N>1 route: torch = one process per GPU (torch.distributed.run, RCCL via ProcessGroupNCCL); "
+                         "group = one process driving --gpus devices through the C ABI (rt_create_multi, "
+                         "rt_gather_frame: RCCL send/recv), the Rust host's route")
     ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
                     help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N, steps)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
@@ -323,10 +327,70 @@ def main() -> int:
          res["t_gather_image_max"], res["rays_total"]) = map(float, stats.tolist())
         return res
 
+    def run_group(frame_batch):
+        """--driver group: this one process drives args.gpus devices through the C ABI
+        (rt_create_multi: a context and a host thread per device, RCCL communicators from
+        ncclCommInitAll) -- the route a Rust host takes to several GPUs. Same timed
+        region as run(): warmup, settle, then exactly args.steps frames and the frame
+        assembled on device 0 (rt_gather_frame: pack -> grouped ncclSend/ncclRecv ->
+        unpack), bracketed by a device synchronize of every device."""
+        from rust_gpu_raytracing_amd.group import RendererGroup
+
+        n = args.gpus
+        scene, default_bounces = build_config(args.config, width=args.width, height=args.height)
+        bounces = args.bounces or default_bounces
+        g = RendererGroup(scene, list(range(n)), frame_batch=frame_batch)
+        for _ in range(args.warmup):
+            g.compute_frame(bounces)
+        g.synchronize()
+        settle_frames = 0
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+            for _ in range(frame_batch):
+                g.compute_frame(bounces)
+            settle_frames += frame_batch
+            g.synchronize()
+        g.gather(0, args.gather)  # untimed: buffers, RCCL peer connections
+        g.synchronize()
+        g.reset_ray_count()
+        views = [g.context_view(i) for i in range(n)]
+        for v in views:
+            v.reset_timing()
+            v.set_timing(True)
+        g.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.compute_frame(bounces)
+        g.gather(0, args.gather)
+        g.synchronize()
+        t_total = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        g.gather(0, args.gather)
+        g.synchronize()
+        t_gather = time.perf_counter() - t1
+        for v in views:
+            v.set_timing(False)
+        v0 = views[0]
+        rays_total = g.ray_count()
+        return dict(r=g, scene=scene, bounces=bounces, width=args.width, height=args.height,
+                    rays=rays_total / n, settle_frames=settle_frames, t_render=t_total - t_gather,
+                    t_gather=t_gather, gathered=True, launch=v0.launch_config(), timing=v0.dispatch_time_total(),
+                    resolve_timing=v0.resolve_time_total(), owned_px=v0.owned_pixel_count(),
+                    t_total_max=t_total, t_render_max=t_total - t_gather, t_gather_max=t_gather,
+                    t_gather_accum_max=t_gather if args.gather == "accumulation" else 0.0,
+                    t_gather_image_max=t_gather if args.gather == "image" else 0.0, rays_total=float(rays_total))
+
+    if args.driver == "group":
+        if world != 1:
+            log("--driver group drives every device from one process: run it without torch.distributed.run")
+            return 2
+        world = args.gpus  # the group's ranks, for default_frame_batch and the report
+        dist_run = True
     fb = args.frame_batch or default_frame_batch(world, args.steps)
-    main_run = run(args.scaling, fb)
+    main_run = run_group(fb) if args.driver == "group" else run(args.scaling, fb)
     r = main_run["r"]
-    if main_run["gathered"] and os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0:
+    if (main_run["gathered"] and os.environ.get("RT_BENCH_VERIFY_GATHER") == "1" and rank == 0
+            and args.driver != "group"):
         # the assembled tile-split image must equal a 1-GPU render of the same frames
         with Renderer(main_run["scene"], device=device) as ref:
             for _ in range(args.warmup + main_run["settle_frames"] + args.steps):
@@ -343,13 +407,13 @@ def main() -> int:
     # >= 5 ms (src/main.rs:88-92, 365-375), i.e. about 6 frames per displayed image,
     # so launches of 6 frames, each materialising its last frame's RGBA8 output.
     cadences = {}
-    if world == 1 and not args.no_cadences:
+    if world == 1 and not args.no_cadences and args.driver != "group":
         for key, batch in (("ms_per_step_f1", 1), ("ms_per_step_display_cadence", DISPLAY_CADENCE_FRAMES)):
             c_run = run(args.scaling, batch)
             c_run["r"].close()
             cadences[key] = c_run["t_total_max"] / args.steps * 1e3
     weak = None
-    if dist_run and args.scaling == "strong" and not args.no_weak:
+    if dist_run and args.scaling == "strong" and not args.no_weak and args.driver != "group":
         w_run = run("weak", args.frame_batch or default_frame_batch(1, args.steps))
         w_run["r"].close()
         weak = {
@@ -442,6 +506,8 @@ def main() -> int:
             result["cadence_note"] = (f"secondary: the same {args.steps} steps in single-frame launches (library "
                                       f"default) and in launches of {DISPLAY_CADENCE_FRAMES} (the reference's "
                                       "0.8 ms compute / 5 ms display pacing); `value` uses frame_batch")
+        if args.driver == "group":
+            result["driver"] = "c-abi group (rt_create_multi + rt_gather_frame, one process)"
         if dist_run:
             result["render_ms_per_step"] = m["t_render_max"] / args.steps * 1e3
             result["gather_ms"] = m["t_gather_max"] * 1e3
@@ -459,7 +525,7 @@ def main() -> int:
             log("cpu baseline ...")
             result["cpu_baseline"] = cpu_baseline(scene, bounces, args.cpu_seconds, args.cpu_sample_world)
         print(json.dumps(result), flush=True)
-    if dist_run:
+    if dist_run and args.driver != "group":
         dist.destroy_process_group()
     return 0
 

@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -377,6 +377,74 @@ RT_API void* rt_stream(rt_ctx* ctx);
 /* The 256-entry sRGB -> linear table the kernel decodes Rgba8UnormSrgb
  * texels with (IEC 61966-2-1, rounded to f32). For tests. */
 RT_API int rt_srgb_table(float out[256]);
+
+/* ---- several GPUs in one process (SURVEY §5, §8b threading row, §8e) -----
+ *
+ * The reference renders on one adapter (src/main.rs:636-665). A group is N
+ * contexts in this process -- rank r on devices[r], world N: 8x8 tile t is
+ * rendered by rank t % N, with global pixel indices for the RNG seeds, so the
+ * assembled frame is bit-identical to one GPU's -- each driven by its own host
+ * thread, plus one RCCL communicator per device (ncclCommInitAll; librccl is
+ * loaded on the first rt_create_multi). Rendering needs no communication;
+ * rt_gather_frame assembles the frame on a root device over xGMI.
+ *
+ * `info` describes the whole frame and scene exactly as for rt_create (rank 0,
+ * world_size 0 or 1; its `device` is ignored). Host arrays passed to group calls
+ * are copied by every device before the call returns. Calls on one group are not
+ * thread-safe. rt_group_compute_frame is asynchronous (each device's thread
+ * queues or launches its share); a failure there is returned by the next
+ * synchronous group call. rt_group_context gives rank r's context for the
+ * single-context entry points -- only while the group is idle (after
+ * rt_group_synchronize or a synchronous group call).
+ * Group errors: rt_group_last_error(g) (rt_last_error(NULL) for rt_create_multi). */
+typedef struct rt_group rt_group;
+
+RT_API int rt_create_multi(const rt_create_info* info, const int32_t* devices, uint32_t n_devices, rt_group** out);
+RT_API void rt_destroy_multi(rt_group* g);
+RT_API const char* rt_group_last_error(const rt_group* g);
+RT_API uint32_t rt_group_size(const rt_group* g);
+RT_API rt_ctx* rt_group_context(rt_group* g, uint32_t rank);
+
+/* Renderer::compute_frame (src/renderer.rs:201-252) on every device's share. */
+RT_API int rt_group_compute_frame(rt_group* g, uint32_t bounces);
+RT_API int rt_group_set_frame_batch(rt_group* g, uint32_t max_frames);
+RT_API int rt_group_flush(rt_group* g);
+RT_API int rt_group_synchronize(rt_group* g);
+RT_API int rt_group_update_params(rt_group* g, const rt_params* params);
+RT_API int rt_group_reset_accumulation(rt_group* g, const rt_params* params);
+RT_API int rt_group_update_camera(rt_group* g, const rt_ray_camera* camera);
+RT_API int rt_group_update_camera_matrices(rt_group* g, const float inverse_projection[16],
+                                           const float inverse_view[16]);
+RT_API int rt_group_update_ray_directions(rt_group* g, const rt_ray* rays, uint32_t count);
+RT_API int rt_group_update_spheres(rt_group* g, const rt_scene_sphere* spheres, uint32_t count);
+RT_API int rt_group_update_triangles(rt_group* g, const rt_scene_triangle* triangles, uint32_t count);
+RT_API int rt_group_update_object_info(rt_group* g, const rt_object_info* objects, uint32_t count);
+RT_API int rt_group_update_sub_object_info(rt_group* g, const rt_sub_object_info* sub_objects, uint32_t count);
+RT_API int rt_group_update_materials(rt_group* g, const rt_scene_material* materials, uint32_t count);
+RT_API int rt_group_upload_textures(rt_group* g, const uint8_t* rgba8, uint32_t width, uint32_t height,
+                                    uint32_t layers);
+RT_API int rt_group_upload_env_map(rt_group* g, const uint8_t* rgba8, uint32_t width, uint32_t height);
+/* Counted rays summed over the devices (rt_ray_count). Synchronous. */
+RT_API int rt_group_ray_count(rt_group* g, uint64_t* out);
+RT_API int rt_group_reset_ray_count(rt_group* g);
+
+/* Gather payloads. */
+#define RT_GATHER_IMAGE 0         /* the packed RGBA8 output, 4 B/px: the frame the reference displays */
+#define RT_GATHER_ACCUMULATION 1  /* the RGBA32F accumulation, 16 B/px (+ the output rebuilt from it) */
+/* Assembles the frame on device `root`: every device packs its tiles
+ * (rt_pack_owned_output / rt_pack_owned_accumulation) on its stream, one grouped
+ * ncclSend / ncclRecv moves every block (the root's own too) into the root's
+ * receive buffer over xGMI, and the root unpacks them all in one launch
+ * (rt_unpack_*_ranks; the accumulation payload re-packs the RGBA8 output with the
+ * last frame's divisor k*c, compute_shader.wgsl:166). Everything is stream-ordered
+ * after the frames submitted so far: the call returns without waiting for the
+ * device. Afterwards the root's output (and, for RT_GATHER_ACCUMULATION, its
+ * accumulation) equals a one-GPU render's; the other devices keep accumulating
+ * their own tiles. */
+RT_API int rt_gather_frame(rt_group* g, uint32_t root, uint32_t payload);
+/* rt_read_output / rt_read_accumulation of device `root`'s context. Synchronous. */
+RT_API int rt_group_read_output(rt_group* g, uint32_t root, uint32_t* rgba8_out);
+RT_API int rt_group_read_accumulation(rt_group* g, uint32_t root, float* rgba_f32_out);
 
 /* ---- scene build and edit: src/triangle_object.rs -----
  *

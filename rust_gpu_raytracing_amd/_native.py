@@ -145,7 +145,38 @@ SIGNATURES = {
     "rt_read_triangles": (ctypes.c_int, [_P, _P, _U32]),
     "rt_read_object_info": (ctypes.c_int, [_P, _P, _U32]),
     "rt_read_sub_object_info": (ctypes.c_int, [_P, _P, _U32]),
+    # several GPUs in one process (rt_multi.cpp)
+    "rt_create_multi": (ctypes.c_int, [ctypes.POINTER(rt_create_info), ctypes.POINTER(ctypes.c_int32), _U32,
+                                       ctypes.POINTER(_P)]),
+    "rt_destroy_multi": (None, [_P]),
+    "rt_group_last_error": (ctypes.c_char_p, [_P]),
+    "rt_group_size": (_U32, [_P]),
+    "rt_group_context": (_P, [_P, _U32]),
+    "rt_group_compute_frame": (ctypes.c_int, [_P, _U32]),
+    "rt_group_set_frame_batch": (ctypes.c_int, [_P, _U32]),
+    "rt_group_flush": (ctypes.c_int, [_P]),
+    "rt_group_synchronize": (ctypes.c_int, [_P]),
+    "rt_group_update_params": (ctypes.c_int, [_P, ctypes.POINTER(rt_params)]),
+    "rt_group_reset_accumulation": (ctypes.c_int, [_P, ctypes.POINTER(rt_params)]),
+    "rt_group_update_camera": (ctypes.c_int, [_P, ctypes.POINTER(rt_ray_camera)]),
+    "rt_group_update_camera_matrices": (ctypes.c_int, [_P, _P, _P]),
+    "rt_group_update_ray_directions": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_group_update_spheres": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_group_update_triangles": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_group_update_object_info": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_group_update_sub_object_info": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_group_update_materials": (ctypes.c_int, [_P, _P, _U32]),
+    "rt_group_upload_textures": (ctypes.c_int, [_P, _P, _U32, _U32, _U32]),
+    "rt_group_upload_env_map": (ctypes.c_int, [_P, _P, _U32, _U32]),
+    "rt_group_ray_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_group_reset_ray_count": (ctypes.c_int, [_P]),
+    "rt_gather_frame": (ctypes.c_int, [_P, _U32, _U32]),
+    "rt_group_read_output": (ctypes.c_int, [_P, _U32, _P]),
+    "rt_group_read_accumulation": (ctypes.c_int, [_P, _U32, _P]),
 }
+
+RT_GATHER_IMAGE = 0
+RT_GATHER_ACCUMULATION = 1
 
 _lib = None
 

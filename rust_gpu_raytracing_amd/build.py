@@ -21,7 +21,7 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 OUT = PKG / "librt_pathtrace.so"
 SOURCES = [CSRC / "pathtrace.hip", CSRC / "scene_edit.hip", CSRC / "rt_abi.cpp", CSRC / "sphere_bvh.cpp",
-           CSRC / "scene_build.cpp"]
+           CSRC / "scene_build.cpp", CSRC / "rt_multi.cpp"]
 HEADERS = [CSRC / "rt_bvh_slab.h", CSRC / "rt_device_math.h", CSRC / "rt_kernel_args.h", CSRC / "sphere_bvh.h",
            CSRC / "rt_scene_math.h", INCLUDE / "rt_abi.h"]
 
@@ -71,6 +71,8 @@ def hipcc_command(out: Path = OUT, extra: list[str] | None = None, build_hash: s
         f'-DRT_BUILD_HASH="{build_hash or source_hash()}"',
         *(extra or []),
         *map(str, SOURCES),
+        "-ldl",  # rt_multi.cpp opens librccl at run time (dlopen), only for rt_create_multi
+        "-pthread",  # rt_multi.cpp: one host thread per device of a group
         "-o",
         str(out),
     ]

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.rt_abi_version() == 5
+    assert native_lib.rt_abi_version() == 6
 
 
 def test_library_built_from_these_sources(native_lib):
@@ -105,3 +105,42 @@ def test_null_context_calls_fail_cleanly(native_lib):
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(N.NativeLibraryError):
         N.load_library(tmp_path / "nope.so")
+
+
+def _multi(native_lib, info, devices):
+    devs = (ctypes.c_int32 * max(len(devices), 1))(*devices)
+    g = ctypes.c_void_p()
+    rc = native_lib.rt_create_multi(ctypes.byref(info) if info is not None else None, devs,
+                                    len(devices), ctypes.byref(g))
+    return rc, g
+
+
+def test_create_multi_validates_arguments_without_device(native_lib):
+    """rt_create_multi (rt_multi.cpp): argument checks come before any device or RCCL
+    call, with the reason in rt_last_error(NULL); a valid request on a machine with
+    no GPU is RT_E_NODEVICE. No group is returned on failure."""
+    info = N.rt_create_info()
+    info.width, info.height = 16, 8
+    rc, g = _multi(native_lib, None, [0])
+    assert rc == N.RT_E_INVALID and not g.value
+    rc, g = _multi(native_lib, info, [])
+    assert rc == N.RT_E_INVALID and not g.value and b"n_devices" in native_lib.rt_last_error(None)
+    rc, g = _multi(native_lib, info, [0, 1, 0])
+    assert rc == N.RT_E_INVALID and not g.value and b"twice" in native_lib.rt_last_error(None)
+    info.world_size, info.rank = 2, 1
+    rc, g = _multi(native_lib, info, [0, 1])
+    assert rc == N.RT_E_INVALID and not g.value and b"whole frame" in native_lib.rt_last_error(None)
+    info.world_size, info.rank = 1, 0
+    rc, g = _multi(native_lib, info, [0])
+    assert rc in (N.RT_E_NODEVICE, N.RT_OK)  # no GPU in the CPU suite: NODEVICE
+    if rc == N.RT_OK:  # pragma: no cover - a box with a GPU
+        native_lib.rt_destroy_multi(g)
+
+
+def test_null_group_calls_fail_cleanly(native_lib):
+    assert native_lib.rt_group_compute_frame(None, 8) == N.RT_E_INVALID
+    assert native_lib.rt_group_synchronize(None) == N.RT_E_INVALID
+    assert native_lib.rt_gather_frame(None, 0, 0) == N.RT_E_INVALID
+    assert native_lib.rt_group_size(None) == 0
+    assert native_lib.rt_group_context(None, 0) is None
+    native_lib.rt_destroy_multi(None)
