@@ -41,9 +41,11 @@ struct Builder {
     std::vector<uint32_t> leaf_order;
     uint32_t leaf_max = kSphereBvhLeafMax;
     bool sweep_sah = true;  // exact SAH over sorted centroids on all three axes (subtrees <= kSweepMax)
+    uint32_t max_depth = 0xffffffffu;
 
-    // Builds the subtree over prims[begin, end) at node index `at` (pre-order).
-    void build(uint32_t begin, uint32_t end) {
+    // Builds the subtree over prims[begin, end) at node index `at` (pre-order),
+    // `depth` levels below the root.
+    void build(uint32_t begin, uint32_t end, uint32_t depth = 0) {
         const uint32_t at = (uint32_t)nodes.size();
         nodes.push_back(SphereBvhNode{});
         Box box, cbox;
@@ -59,6 +61,23 @@ struct Builder {
         if (n <= leaf_max) {
             nodes[at].leaf = (uint32_t)leaf_order.size() | (n << 24);
             for (uint32_t i = begin; i < end; i++) leaf_order.push_back(prims[i].orig);
+            nodes[at].skip = (uint32_t)nodes.size();
+            return;
+        }
+        // levels a balanced split of the rest needs: ceil(log2(ceil(n / leaf_max)))
+        uint32_t need = 0;
+        for (uint64_t c = ((uint64_t)n + leaf_max - 1) / leaf_max; c > 1; c = (c + 1) / 2) need++;
+        if (max_depth != 0xffffffffu && depth + need + 1 >= max_depth) {
+            // median split on the widest centroid axis: depth stays bounded
+            int axis = 0;
+            for (int k = 1; k < 3; k++)
+                if (cbox.hi[k] - cbox.lo[k] > cbox.hi[axis] - cbox.lo[axis]) axis = k;
+            std::stable_sort(prims.begin() + begin, prims.begin() + end,
+                             [&](const Prim& a, const Prim& b) { return a.c[axis] < b.c[axis]; });
+            const uint32_t mid = begin + n / 2;
+            nodes[at].leaf = kSphereBvhInternal;
+            build(begin, mid, depth + 1);
+            build(mid, end, depth + 1);
             nodes[at].skip = (uint32_t)nodes.size();
             return;
         }
@@ -94,8 +113,8 @@ struct Builder {
                              [&](const Prim& a, const Prim& b) { return a.c[best_axis] < b.c[best_axis]; });
             const uint32_t mid = begin + best_i;
             nodes[at].leaf = kSphereBvhInternal;
-            build(begin, mid);
-            build(mid, end);
+            build(begin, mid, depth + 1);
+            build(mid, end, depth + 1);
             nodes[at].skip = (uint32_t)nodes.size();
             return;
         }
@@ -149,8 +168,8 @@ struct Builder {
         }
         if (mid == begin || mid == end) mid = begin + n / 2;
         nodes[at].leaf = kSphereBvhInternal;
-        build(begin, mid);
-        build(mid, end);
+        build(begin, mid, depth + 1);
+        build(mid, end, depth + 1);
         nodes[at].skip = (uint32_t)nodes.size();
     }
 };
@@ -158,7 +177,7 @@ struct Builder {
 }  // namespace
 
 void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, uint32_t leaf_max,
-                   std::vector<SphereBvhNode>* nodes, std::vector<uint32_t>* leaf_order) {
+                   std::vector<SphereBvhNode>* nodes, std::vector<uint32_t>* leaf_order, uint32_t max_depth) {
     const size_t n = lo.size() / 3;
     std::vector<Prim> prims(n);
     for (size_t i = 0; i < n; i++) {
@@ -173,6 +192,7 @@ void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, u
     leaf_order->clear();
     if (n == 0) return;
     Builder b{prims, *nodes, {}, leaf_max};
+    b.max_depth = max_depth;
     b.build(0, (uint32_t)n);
     *leaf_order = std::move(b.leaf_order);
 }

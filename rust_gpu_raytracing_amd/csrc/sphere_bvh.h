@@ -75,8 +75,11 @@ bool box_layout_orderable(const std::vector<SphereBvhNode>& nodes);
 // per primitive), leaves of at most `leaf_max` primitives. Returns depth-first
 // nodes (same layout as SphereBvhNode; leaf = first | count << 24 indexing
 // `leaf_order`) and the primitive order of the leaves.
+// Subtrees that would reach below `max_depth` levels are split at the median
+// instead (balanced: a subtree of n primitives is then ceil(log2 n) levels deep).
 void build_box_bvh(const std::vector<float>& lo, const std::vector<float>& hi, uint32_t leaf_max,
-                   std::vector<SphereBvhNode>* nodes, std::vector<uint32_t>* leaf_order);
+                   std::vector<SphereBvhNode>* nodes, std::vector<uint32_t>* leaf_order,
+                   uint32_t max_depth = 0xffffffffu);
 
 // Triangle side (check_triangles, compute_shader.wgsl:422-517). One primitive
 // per (object, sub-object) pair the reference's sweep visits, in sweep order.
