@@ -56,6 +56,10 @@ struct SceneView {
     const float4* tri_nodes;  // triangle accelerator nodes (LDS in mode 2, else global)
     const uint4* tri_prims;   // triangle accelerator leaves: object, sub-object, sweep position
     float tri_extent;         // triangle margin scale (device memory: a device refit updates it)
+    // the 4-wide accelerator (kWide instances, tri_wide.h)
+    const float4* tri_wide;   // nodes (LDS in mode 2, else global)
+    uint32_t* stk;            // this lane's walk stack in LDS: entry e at stk[e * stk_stride]
+    uint32_t stk_stride;
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -227,7 +231,9 @@ struct TraceState {
     float limit;      // pruning distance: min(best sphere, triangle hit) * 1.00001 + slack (inf: none)
     uint32_t node;
     uint32_t phase;
-    uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf
+    uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf;
+                       // wide walk: leaf_base << 4 | mask of the node's leaves still to test
+    uint32_t sp;       // wide walk: stack entries in use
     bool nan_hit;
     SphereHit sph;
     TriHit tri;
@@ -288,6 +294,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
     ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
     ts.nan_hit = false;
     ts.node = 0;
+    ts.sp = 0;
     ts.pending = kNoLeaf;
     // brute-force sphere set: wave-uniform sweep over groups of 4, then the rest
     // one by one (a sphere's own test is exact, so the visiting order is free)
@@ -350,12 +357,129 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     }
 }
 
+// A leaf of the 4-wide accelerator (tri_wide.h): the reference's object and
+// sub-object ray_in_bounds tests (:431, :441) and its triangle tests (:445-500)
+// for one record of a sub-object's triangles. Compact records recompute each
+// triangle's a, edge_ab, edge_ac and calc_normal from their vertex block with
+// SceneTriangle::new's f32 operations (src/buffers.rs:66-95) -- the record's own
+// bits, verified when the block was built -- so the tests below see exactly the
+// values the triangle buffer holds.
+__device__ __forceinline__ void tri_leaf_wide(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
+                                              uint32_t leaf) {
+    const uint4* lf = ka.tri_leaves + 4u * leaf;
+    const uint4 q0 = lf[0], q1 = lf[1], q2 = lf[2], q3 = lf[3];  // mn first | mx seq | obj count vbase sub | idx
+    const RtObject& ob = sv.obj[q2.x];
+    const float mn[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+    const float mx[3] = {__uint_as_float(q1.x), __uint_as_float(q1.y), __uint_as_float(q1.z)};
+    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) || !ray_in_bounds(o, ts.inv, mn, mx)) return;
+    const uint32_t count = q2.y & 0xffu;
+    const bool compact = (q2.y & kWideLeafCompact) != 0u;
+    uint64_t iw0 = (uint64_t)q3.x | ((uint64_t)q3.y << 32), iw1 = (uint64_t)q3.z | ((uint64_t)q3.w << 32);
+    for (uint32_t j = 0; j < count; ++j) {
+        TriGeom g;
+        if (compact) {
+            const TriVertex* vb = ka.tri_verts + q2.z;
+            const TriVertex va = vb[iw0 & 0xfu], vv = vb[(iw0 >> 4) & 0xfu], vc = vb[(iw0 >> 8) & 0xfu];
+            iw0 = (iw0 >> 12) | (iw1 << 52);
+            iw1 >>= 12;
+            float ab[3], ac[3], cn[3];
+            wide_tri_from_vertices(va, vv, vc, ab, ac, cn);
+            g = TriGeom{mk(va.x, va.y, va.z), mk(ab[0], ab[1], ab[2]), mk(ac[0], ac[1], ac[2]), mk(cn[0], cn[1], cn[2])};
+        } else {
+            g = load_tri(ka.triangles, min(q0.w + j, ka.triangle_count - 1u));
+        }
+        const uint32_t seq = q1.w + j;
+        const float det = -dot(d, g.cn);
+        const float inv_det = 1.0f / det;
+        const f3 ao = o - g.a;
+        const float dist = dot(ao, g.cn) * inv_det;
+        const bool nan_dist = dist != dist;
+        if (dist < 0.0f) continue;
+        if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) continue;
+        const f3 dao = cross(ao, d);
+        const float v = -dot(g.ab, dao) * inv_det;
+        if (v < 0.0f) continue;
+        const float u = dot(g.ac, dao) * inv_det;
+        if (u < 0.0f) continue;
+        const float w = 1.0f - u - v;
+        if (w < 0.0f) continue;
+        if (nan_dist) {
+            ts.nan_hit = true;
+            continue;
+        }
+        ts.tri = TriHit{dist, seq, min(q0.w + j, ka.triangle_count - 1u), q2.x, det > 0.0f};
+    }
+}
+
+// One node of the 4-wide walk (tri_wide.h): the four child boxes, inflated by the
+// ray's margin, tested together (rt_bvh_slab.h). Hit leaves are deferred to the
+// wave's leaf batches (ts.pending: the node's leaf records still to test); the
+// first hit internal child is visited next and the others wait on the lane's LDS
+// stack as one entry (first child, mask). A lane whose leaves are still pending
+// when it reaches another node with hit leaves stays on that node (marked
+// kWideBlocked, so it is not reloaded) until the batch has tested them.
+constexpr uint32_t kWideNone = 0xffffffffu;
+constexpr uint32_t kWideBlocked = 0x80000000u;
+
+__device__ __forceinline__ void wide_node_step(const SceneView& sv, TraceState& ts) {
+    uint32_t n = ts.node;
+    if (n != kWideNone && (n & kWideBlocked)) {
+        if (ts.pending != kNoLeaf) return;
+        n &= ~kWideBlocked;
+    }
+    if (n == kWideNone) {
+        if (ts.sp == 0u) return;  // walk over (phase_end)
+        const uint32_t at = (ts.sp - 1u) * sv.stk_stride;
+        uint32_t e = sv.stk[at];
+        n = (e >> 4) + (uint32_t)__builtin_ctz(e & 0xfu);
+        e &= e - 1u;  // the lowest set bit is the mask's
+        if ((e & 0xfu) == 0u)
+            ts.sp -= 1u;
+        else
+            sv.stk[at] = e;
+    }
+    const float4* nd = sv.tri_wide + 8u * n;
+    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+    const uint4 meta = reinterpret_cast<const uint4*>(nd)[6];  // child_base, leaf_base, slots
+    const uint32_t n_int = meta.z & 0xfu, n_slots = n_int + ((meta.z >> 4) & 0xfu);
+    uint32_t hit = 0;
+    float nt, ft;
+    slab_hit(ts.slab, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, nt, ft);
+    hit |= (nt <= ft && ft >= 0.0f) ? 1u : 0u;
+    slab_hit(ts.slab, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, nt, ft);
+    hit |= (nt <= ft && ft >= 0.0f) ? 2u : 0u;
+    slab_hit(ts.slab, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, nt, ft);
+    hit |= (nt <= ft && ft >= 0.0f) ? 4u : 0u;
+    slab_hit(ts.slab, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, nt, ft);
+    hit |= (nt <= ft && ft >= 0.0f) ? 8u : 0u;
+    hit &= (1u << n_slots) - 1u;
+    const uint32_t hl = hit >> n_int;                   // leaf ranks
+    const uint32_t hi = hit & ((1u << n_int) - 1u);     // internal ranks
+    if (hl != 0u) {
+        if (ts.pending != kNoLeaf) {
+            ts.node = n | kWideBlocked;
+            return;
+        }
+        ts.pending = (meta.y << 4) | hl;
+    }
+    if (hi != 0u) {
+        ts.node = meta.x + (uint32_t)__builtin_ctz(hi);
+        const uint32_t rest = hi & (hi - 1u);
+        if (rest != 0u) {
+            sv.stk[ts.sp * sv.stk_stride] = (meta.x << 4) | rest;
+            ts.sp += 1u;
+        }
+    } else {
+        ts.node = kWideNone;
+    }
+}
+
 // Ends the current BVH walk once its nodes are exhausted and no leaf is pending.
-template <bool kTris>
+template <bool kTris, bool kWide = false>
 __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     if (ts.pending != kNoLeaf) return;
     if (kTris && ts.phase == 0) {
-        if (ts.node < ka.tri_nodes) return;
+        if (kWide ? (ts.node != kWideNone || ts.sp != 0u) : (ts.node < ka.tri_nodes)) return;
 #ifdef RT_DIAG_TAIL
         if (ts.nan_hit) atomicAdd(ka.diag + 6, 1ull);
 #endif
@@ -399,9 +523,13 @@ constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
 template <int kMode, bool kTris>
 constexpr bool kDrainDecouple = kTris && kMode < 2;
 
-template <bool kTris>
+template <bool kTris, bool kWide = false>
 __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     const bool tri = kTris && ts.phase == 0;
+    if (kWide && tri) {
+        wide_node_step(sv, ts);
+        return;
+    }
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
     const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
@@ -429,8 +557,17 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     ts.node = (hit && !at_leaf) ? ts.node + 1u : __float_as_uint(lo.w);
 }
 
-template <bool kTris>
+template <bool kTris, bool kWide = false>
 __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
+    if (kWide && kTris && ts.phase == 0) {
+        // one of the node's pending leaf records per batch
+        const uint32_t m = ts.pending & 0xfu;
+        const uint32_t leaf = (ts.pending >> 4) + (uint32_t)__builtin_ctz(m);
+        const uint32_t rest = m & (m - 1u);
+        ts.pending = rest ? ((ts.pending & ~0xfu) | rest) : kNoLeaf;
+        tri_leaf_wide(sv, ka, o, d, ts, leaf);
+        return;
+    }
     if (kTris && ts.phase == 0)
         tri_leaf(sv, ka, o, d, ts, ts.pending);
     else
@@ -916,7 +1053,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
-template <int kMode, uint32_t kThreads, bool kTris>
+template <int kMode, uint32_t kThreads, bool kTris, bool kWide>
 __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
@@ -925,7 +1062,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
-                 ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f};
+                 ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
+                 ka.tri_wide,     nullptr,        kThreads};
+    if constexpr (kWide) sv.stk = reinterpret_cast<uint32_t*>(lds + ka.lds_stack_offset) + tid;
     if (tid == 0) block_rays = 0;
     if constexpr (kMode >= 1) {
         float4* l_sph = reinterpret_cast<float4*>(lds);
@@ -965,7 +1104,11 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         sv.mat = l_mat;
         sv.obj = l_obj;
     }
-    if constexpr (kMode == 2) {
+    if constexpr (kMode == 2 && kWide) {  // the wide nodes (leaf records stay in global memory)
+        float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
+        for (uint32_t i = tid; i < 8u * ka.tri_nodes; i += kThreads) l_tn[i] = ka.tri_wide[i];
+        sv.tri_wide = l_tn;
+    } else if constexpr (kMode == 2) {
         float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
         uint4* l_tp = reinterpret_cast<uint4*>(lds + ka.lds_tri_prims_offset);
         for (uint32_t i = tid; i < 2u * ka.tri_nodes; i += kThreads) l_tn[i] = ka.tri_bvh[i];
@@ -1221,18 +1364,18 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #endif
             if (mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
                 if (kDeferLeaves<kTris> && leaves)
-                    leaf_step<kTris>(sv, ka, p.o, p.d, ts);
+                    leaf_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
                 else
-                    node_step<kTris>(sv, ka, p.o, p.d, ts);
-                phase_end<kTris>(sv, ka, p.o, p.d, ts);
+                    node_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
                 if (ts.phase == 2) mode = kDone;
                 if (!(kDeferLeaves<kTris> && leaves)) {
                     // further node steps before the next wave-wide check (RT_TRAV_UNROLL)
 #pragma unroll
                     for (int k = 1; k < (kTris ? RT_TRAV_UNROLL_TRI : RT_TRAV_UNROLL); ++k) {
                         if (mode == kTrav) {
-                            node_step<kTris>(sv, ka, p.o, p.d, ts);
-                            phase_end<kTris>(sv, ka, p.o, p.d, ts);
+                            node_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                            phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
                             if (ts.phase == 2) mode = kDone;
                         }
                     }
@@ -1311,13 +1454,18 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 // the size with the most resident waves up to a cap (rt_pathtrace_pick_config).
 // Sphere-only scenes get kernels without the triangle side (fewer live scalar
 // registers: the kernel arguments of the triangle path no longer spill).
-#ifndef RT_EXTRA_CONFIGS  // experiment builds add instances here, e.g. -DRT_EXTRA_CONFIGS(X)="X(1, 640, false)"
+#ifndef RT_EXTRA_CONFIGS  // experiment builds add instances here, e.g. -DRT_EXTRA_CONFIGS(X)="X(1, 640, false, false)"
 #define RT_EXTRA_CONFIGS(X)
 #endif
+// (mode, threads, triangles, 4-wide triangle accelerator)
 #define RT_FOR_EACH_CONFIG(X)                                                                                   \
-    X(0, 256, true) X(0, 512, true) X(0, 1024, true) X(1, 256, true) X(1, 512, true) X(1, 1024, true)           \
-    X(2, 256, true) X(2, 512, true) X(2, 1024, true) X(0, 256, false) X(0, 512, false) X(0, 1024, false)        \
-    X(1, 256, false) X(1, 512, false) X(1, 1024, false) RT_EXTRA_CONFIGS(X)
+    X(0, 256, true, false) X(0, 512, true, false) X(0, 1024, true, false) X(1, 256, true, false)               \
+    X(1, 512, true, false) X(1, 1024, true, false) X(2, 256, true, false) X(2, 512, true, false)               \
+    X(2, 1024, true, false) X(0, 256, true, true) X(0, 512, true, true) X(0, 1024, true, true)                 \
+    X(1, 256, true, true) X(1, 512, true, true) X(1, 1024, true, true) X(2, 256, true, true)                   \
+    X(2, 512, true, true) X(2, 1024, true, true) X(0, 256, false, false) X(0, 512, false, false)               \
+    X(0, 1024, false, false) X(1, 256, false, false) X(1, 512, false, false) X(1, 1024, false, false)          \
+    RT_EXTRA_CONFIGS(X)
 
 namespace {
 // Dynamic LDS above 64 KiB must be opted into per kernel.
@@ -1331,12 +1479,12 @@ hipError_t allow_big_lds(const void* fn) {
 }
 }  // namespace
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes,
-                               uint32_t blocks, hipStream_t stream) {
-#define RT_LAUNCH(M, T, TR)                                                                                  \
-    if (mode == M && threads == T && tris == TR) {                                                          \
-        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T, TR>), dim3(blocks), dim3(T), lds_bytes, stream, ka);  \
-        return hipGetLastError();                                                                           \
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool wide, uint32_t threads,
+                               size_t lds_bytes, uint32_t blocks, hipStream_t stream) {
+#define RT_LAUNCH(M, T, TR, W)                                                                                   \
+    if (mode == M && threads == T && tris == TR && wide == W) {                                                 \
+        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T, TR, W>), dim3(blocks), dim3(T), lds_bytes, stream, ka);   \
+        return hipGetLastError();                                                                               \
     }
     RT_FOR_EACH_CONFIG(RT_LAUNCH)
 #undef RT_LAUNCH
@@ -1349,16 +1497,19 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32
 // add contention), ties to the smaller workgroup.
 constexpr int kDefaultWavesPerCu = 16;
 
-hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, uint32_t force_threads,
-                                    uint32_t waves_cap, uint32_t* threads, int* blocks_per_cu) {
+hipError_t rt_pathtrace_pick_config(int mode, bool tris, bool wide, size_t lds_bytes,
+                                    size_t lds_bytes_per_thread, uint32_t force_threads, uint32_t waves_cap,
+                                    uint32_t* threads, int* blocks_per_cu) {
     const int kTargetWavesPerCu = waves_cap ? (int)waves_cap : kDefaultWavesPerCu;
     int best_waves = -1;
-#define RT_OCC(M, T, TR)                                                                                  \
-    if (mode == M && tris == TR) {                                                                        \
+    // lds_bytes_per_thread: the wide walk's stack (grows with the workgroup size)
+#define RT_OCC(M, T, TR, W)                                                                               \
+    if (mode == M && tris == TR && wide == W) {                                                           \
         int n = 0;                                                                                        \
-        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T, TR>));     \
+        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T, TR, W>));  \
         if (e != hipSuccess) return e;                                                                    \
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T, TR>, T, lds_bytes); \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T, TR, W>, T,        \
+                                                         lds_bytes + (size_t)T * lds_bytes_per_thread);  \
         if (e != hipSuccess) return e;                                                                    \
         const int waves = std::min(n * (int)(T / 64), kTargetWavesPerCu);                                 \
         if (n > 0 && (force_threads ? force_threads == T : waves > best_waves)) {                         \

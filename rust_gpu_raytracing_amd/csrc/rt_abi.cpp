@@ -22,13 +22,20 @@
 #include "rt_kernel_args.h"
 #include "rt_scene_math.h"
 #include "sphere_bvh.h"
+#include "tri_wide.h"
 
 hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
                                    hipStream_t stream);
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes, uint32_t blocks,
-                               hipStream_t stream);
-hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, uint32_t force_threads, uint32_t waves_cap,
-                                    uint32_t* threads, int* blocks_per_cu);
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool wide, uint32_t threads,
+                               size_t lds_bytes, uint32_t blocks, hipStream_t stream);
+hipError_t rt_pathtrace_pick_config(int mode, bool tris, bool wide, size_t lds_bytes, size_t lds_bytes_per_thread,
+                                    uint32_t force_threads, uint32_t waves_cap, uint32_t* threads,
+                                    int* blocks_per_cu);
+hipError_t rt_launch_wide_refresh(TriWideNode* nodes, TriLeaf* leaves, uint32_t n_leaves, const TriVertex* verts_in,
+                                  TriVertex* verts, const uint32_t* vsrc, uint32_t n_verts, const RtSubObject* subs,
+                                  const RtTriangleHot* tris, uint32_t n_tri, const uint32_t* order,
+                                  const uint32_t* level_offsets, uint32_t n_levels, float* extent_out, bool refit,
+                                  hipStream_t stream);
 hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const uint32_t* sub_object,
                           const uint2* object_tris, const rt_scene::Placement* place, uint32_t object_count,
                           uint32_t n_tri, uint32_t n_sub, RtTriangleHot* tris, float4* bounds, RtSubObject* subs,
@@ -64,6 +71,10 @@ namespace {
 
 constexpr size_t kLdsSceneBudget = 64 * 1024;    // mode 1: spheres/materials/objects/sphere BVH per workgroup
 constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerator (one 1024-thread workgroup per CU)
+// Compact leaves (tri_wide.h) by default when the triangle records outgrow one
+// XCD's 4 MB L2 (C5: 64 MB -> 26 MB of vertex blocks); smaller meshes stay L2
+// resident and the recomputation would only add VALU work.
+constexpr size_t kCompactMinTriBytes = 4u << 20;
 // d_counter: [0] the ray counter, [1, 1 + kDiagCounters) the diagnostic
 // counters of RT_DIAG / RT_DIAG_TAIL builds (KernelArgs::diag), then the
 // per-wave (queue dry, end) records of RT_DIAG_TAIL builds: room for 65,536 waves.
@@ -170,6 +181,8 @@ struct rt_ctx {
     size_t occ_lds_bytes = 0;
     int occ_mode = -1;
     bool occ_tris = false;
+    bool occ_wide = false;
+    size_t occ_stack_pt = 0;
     int max_lds_mode = 2;               // RT_LDS_MODE (A/B switch): highest staging mode allowed
     int occ_blocks_per_cu = 0;
     uint32_t occ_threads = 0;
@@ -210,6 +223,17 @@ struct rt_ctx {
     bool tri_dirty = true;
     uint32_t tri_count_built = 0xffffffffu;
     bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
+    // the 4-wide accelerator (tri_wide.h), the default (RT_TRI_WIDE=0: the binary one, A/B switch)
+    bool use_tri_wide = true;
+    int tri_compact = -1;        // RT_TRI_COMPACT: 1 / 0 force compact leaves on / off; -1 by size
+    bool wide_built = false;     // the accelerator on the device is the wide one
+    bool wide_refresh = false;   // triangles uploaded since the compact blocks were checked
+    TriWideNode* d_wide = nullptr;
+    TriLeaf* d_leaves = nullptr;
+    TriVertex* d_verts = nullptr;
+    uint32_t* d_vsrc = nullptr;
+    size_t wide_cap = 0, leaves_cap = 0, verts_cap = 0, vsrc_cap = 0;
+    uint32_t wide_leaves = 0, wide_verts = 0, wide_depth = 0, wide_compact_leaves = 0;
     uint32_t tri_nodes = 0, tri_prim_count = 0;
     float* d_tri_extent = nullptr;   // margin extent, in device memory (refit updates it)
     uint32_t* d_tri_order = nullptr; // node indices by depth, deepest level first (refit)
@@ -410,8 +434,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
     if (!ctx->tri_dirty && ctx->tri_count_built == object_count) return RT_OK;
     int rc0 = sync_host_geometry(ctx);
     if (rc0) return rc0;
-    TriangleAccel acc;
-    build_triangle_accel(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(), &acc);
     auto ensure = [&](void** p, size_t* cap, size_t bytes) -> int {
         if (bytes <= *cap && *p) return RT_OK;
         RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -424,6 +446,54 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         return RT_OK;
     };
     int rc;
+    if (ctx->use_tri_wide) {
+        // compact leaves are built from the triangle records as the device holds them
+        const bool compact = ctx->tri_compact == 1 ||
+                             (ctx->tri_compact == -1 && (size_t)ctx->cap_tri * sizeof(RtTriangleHot) > kCompactMinTriBytes);
+        std::vector<RtTriangleHot> hot;
+        if (compact && ctx->cap_tri) {
+            hot.resize(ctx->cap_tri);
+            RT_HIP(ctx, join_aux(ctx));
+            RT_HIP(ctx, hipMemcpyAsync(hot.data(), ctx->d_tri, hot.size() * sizeof(RtTriangleHot), hipMemcpyDeviceToHost,
+                                       ctx->stream));
+            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        TriWide w;
+        build_triangle_wide(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(),
+                            hot.empty() ? nullptr : reinterpret_cast<const float*>(hot.data()), (uint32_t)hot.size(), &w);
+        if (w.depth <= kWideMaxDepth) {
+            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_wide), &ctx->wide_cap, w.nodes.size() * sizeof(TriWideNode))) ||
+                (rc = ensure(reinterpret_cast<void**>(&ctx->d_leaves), &ctx->leaves_cap, w.leaves.size() * sizeof(TriLeaf))) ||
+                (rc = ensure(reinterpret_cast<void**>(&ctx->d_verts), &ctx->verts_cap, w.verts.size() * sizeof(TriVertex))) ||
+                (rc = ensure(reinterpret_cast<void**>(&ctx->d_vsrc), &ctx->vsrc_cap, w.vsrc.size() * 4)) ||
+                (rc = upload_raw(ctx, ctx->d_wide, w.nodes.data(), w.nodes.size() * sizeof(TriWideNode))) ||
+                (rc = upload_raw(ctx, ctx->d_leaves, w.leaves.data(), w.leaves.size() * sizeof(TriLeaf))) ||
+                (rc = upload_raw(ctx, ctx->d_verts, w.verts.data(), w.verts.size() * sizeof(TriVertex))) ||
+                (rc = upload_raw(ctx, ctx->d_vsrc, w.vsrc.data(), w.vsrc.size() * 4)) ||
+                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_order), &ctx->tri_order_cap, w.order.size() * 4)) ||
+                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_level_off), &ctx->tri_level_cap, w.level_off.size() * 4)) ||
+                (rc = upload_raw(ctx, ctx->d_tri_order, w.order.data(), w.order.size() * 4)) ||
+                (rc = upload_raw(ctx, ctx->d_tri_level_off, w.level_off.data(), w.level_off.size() * 4)) ||
+                (rc = upload_raw(ctx, ctx->d_tri_extent, &w.extent, 4)))
+                return rc;
+            ctx->tri_nodes = (uint32_t)w.nodes.size();
+            ctx->wide_leaves = ctx->tri_prim_count = (uint32_t)w.leaves.size();
+            ctx->wide_verts = (uint32_t)w.verts.size();
+            ctx->wide_depth = w.depth;
+            ctx->wide_compact_leaves = 0;
+            for (const TriLeaf& L : w.leaves) ctx->wide_compact_leaves += (L.count_flags & kWideLeafCompact) ? 1u : 0u;
+            ctx->tri_levels = (uint32_t)w.level_off.size() - 1u;
+            ctx->wide_built = true;
+            ctx->wide_refresh = false;
+            ctx->tri_dirty = false;
+            ctx->tri_count_built = object_count;
+            return RT_OK;
+        }
+        // deeper than the kernel's stack: the binary accelerator below
+    }
+    ctx->wide_built = false;
+    TriangleAccel acc;
+    build_triangle_accel(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(), &acc);
     const size_t nb = acc.nodes.size() * sizeof(SphereBvhNode), pb = acc.prims.size() * sizeof(SubObjectPrim);
     if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_bvh), &ctx->tri_bvh_cap, nb)) ||
         (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_prims), &ctx->tri_prims_cap, pb)) ||
@@ -627,6 +697,10 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->waves_cap = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_TRI_BVH");
         ctx->use_tri_bvh = !(env && env[0] == '0');
+        env = std::getenv("RT_TRI_WIDE");
+        ctx->use_tri_wide = !(env && env[0] == '0');
+        env = std::getenv("RT_TRI_COMPACT");
+        if (env) ctx->tri_compact = env[0] == '0' ? 0 : 1;
         env = std::getenv("RT_SPHERE_LEAF");
         ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
         env = std::getenv("RT_SPHERE_BVH");
@@ -725,7 +799,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
-                    ctx->d_clock};
+                    ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -874,6 +948,7 @@ int rt_update_triangles(rt_ctx* ctx, const rt_scene_triangle* triangles, uint32_
     RT_ENTER(ctx);
     if (count && !triangles) return fail(ctx, RT_E_INVALID, "triangles is NULL");
     if (count > ctx->cap_tri) return fail(ctx, RT_E_CAPACITY, "more triangles than the buffer holds");
+    if (ctx->wide_built) ctx->wide_refresh = true;  // compact leaves rechecked before the next frame
     return upload_triangles(ctx, triangles, count);
 }
 
@@ -947,6 +1022,15 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         if (rc) return rc;
         rc = refresh_tri_accel(ctx, p.object_count);
         if (rc) return rc;
+        if (ctx->wide_built && ctx->wide_refresh) {  // triangles uploaded: vertex blocks and their check
+            RT_HIP(ctx, join_aux(ctx));
+            RT_HIP(ctx, rt_launch_wide_refresh(ctx->d_wide, ctx->d_leaves, ctx->wide_leaves, ctx->d_verts,
+                                               ctx->d_verts, ctx->d_vsrc, ctx->wide_verts, ctx->d_sub, ctx->d_tri,
+                                               ctx->n_tri_dev, ctx->d_tri_order, ctx->d_tri_level_off,
+                                               ctx->tri_levels, ctx->d_tri_extent, false, ctx->stream));
+            ctx->primary_dirty = true;
+            ctx->wide_refresh = false;
+        }
     }
     KernelArgs ka{};
     ka.camera_rays = ctx->d_rays;
@@ -970,6 +1054,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tri_extent = ctx->d_tri_extent;
     ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
     ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);
+    ka.tri_wide = reinterpret_cast<const float4*>(ctx->d_wide);
+    ka.tri_leaves = reinterpret_cast<const uint4*>(ctx->d_leaves);
+    ka.tri_verts = ctx->d_verts;
     ka.materials = ctx->d_mat;
     ka.objects = ctx->d_obj;
     ka.sub_objects = ctx->d_sub;
@@ -1048,6 +1135,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
     const bool tris = p.object_count != 0;  // else the sphere-only kernels
+    const bool wide = tris && ka.tri_accel && ctx->wide_built;
+    // the wide walk's stack: one entry per tree level below the root, per thread
+    const size_t stack_pt = wide ? 4u * std::max<uint32_t>(1u, ctx->wide_depth - 1u) : 0u;
     size_t mode1_bytes = 0, mode2_bytes = 0;
     // lays out the LDS image for `layouts` sphere BVH layouts and returns the LDS mode it fits
     auto carve = [&](uint32_t layouts, size_t mode1_budget) -> int {
@@ -1066,12 +1156,20 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         off = al16(off + (size_t)layouts * ctx->n_nodes * sizeof(SphereBvhNode));
         mode1_bytes = off + kLdsTailBytes;
         ka.lds_tri_nodes_offset = (uint32_t)off;
-        off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
-        ka.lds_tri_prims_offset = (uint32_t)off;
-        off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
+        if (wide) {  // wide nodes only (leaf records stay in global memory)
+            off = al16(off + (size_t)ka.tri_nodes * sizeof(TriWideNode));
+            ka.lds_tri_prims_offset = (uint32_t)off;
+        } else {
+            off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
+            ka.lds_tri_prims_offset = (uint32_t)off;
+            off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
+        }
         mode2_bytes = off + kLdsTailBytes;
         if (ctx->force_global_scene) return 0;
-        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes <= kLdsAccelBudget && ctx->max_lds_mode >= 2) return 2;
+        // (the budget holds one 1024-thread workgroup's stack as well)
+        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes + 1024u * stack_pt <= kLdsAccelBudget &&
+            ctx->max_lds_mode >= 2)
+            return 2;
         if (mode1_bytes <= mode1_budget && ctx->max_lds_mode >= 1) return 1;
         return 0;
     };
@@ -1105,18 +1203,23 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode ||
-        ctx->occ_tris != tris) {
+        ctx->occ_tris != tris || ctx->occ_wide != wide || ctx->occ_stack_pt != stack_pt) {
         int per_cu = 0;
         uint32_t threads = 0;
-        hipError_t oe =
-            rt_pathtrace_pick_config(mode, tris, lds_bytes, ctx->force_threads, ctx->waves_cap, &threads, &per_cu);
+        hipError_t oe = rt_pathtrace_pick_config(mode, tris, wide, lds_bytes, stack_pt, ctx->force_threads,
+                                                 ctx->waves_cap, &threads, &per_cu);
         if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
         ctx->occ_blocks_per_cu = per_cu;
         ctx->occ_threads = threads;
         ctx->occ_lds_bytes = lds_bytes;
         ctx->occ_mode = mode;
         ctx->occ_tris = tris;
+        ctx->occ_wide = wide;
+        ctx->occ_stack_pt = stack_pt;
     }
+    // the stack after the scene image and its tail
+    ka.lds_stack_offset = (uint32_t)al16(lds_bytes);
+    if (wide) lds_bytes = ka.lds_stack_offset + (size_t)ctx->occ_threads * stack_pt;
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
     const uint64_t wanted = ((uint64_t)ka.queue_units + waves_per_block - 1) / waves_per_block;
@@ -1188,7 +1291,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         RT_HIP(ctx, hipMemsetAsync(ka.launch_clock, 0, kClockWords * 8, S));
         ctx->clock_pending.push_back(slot);
     }
-    hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, S);
+    hipError_t e = rt_launch_pathtrace(ka, mode, tris, wide, ctx->occ_threads, lds_bytes, blocks, S);
     ctx->last_blocks = blocks;
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
@@ -1363,8 +1466,15 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
                                count, ctx->model_tris, (uint32_t)ctx->h_sub.size(), ctx->d_tri, ctx->d_tri_bounds,
                                ctx->d_sub, ctx->d_obj, ctx->stream));
     ctx->geom_on_device = true;
-    // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds
-    if (ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty)
+    // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds,
+    // and the wide one's compact leaves are rechecked against the new triangles
+    if (ctx->wide_built && ctx->tri_nodes && !ctx->tri_dirty) {
+        RT_HIP(ctx, rt_launch_wide_refresh(ctx->d_wide, ctx->d_leaves, ctx->wide_leaves, ctx->d_verts, ctx->d_verts,
+                                           ctx->d_vsrc, ctx->wide_verts, ctx->d_sub, ctx->d_tri, ctx->n_tri_dev,
+                                           ctx->d_tri_order, ctx->d_tri_level_off, ctx->tri_levels,
+                                           ctx->d_tri_extent, true, ctx->stream));
+        ctx->wide_refresh = false;
+    } else if (!ctx->wide_built && ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty)
         RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,
                                     ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
     return RT_OK;

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tri_wide.h"
+
 
 struct RtSphere {  // src/buffers.rs:40-45, 32 B
     float position[3];
@@ -124,6 +126,10 @@ struct KernelArgs {
     const RtTriangleHot* __restrict__ triangles;
     const float4* __restrict__ tri_bvh;           // BVH over (object, sub-object) pairs, float4 pairs per node
     const uint4* __restrict__ tri_prims;          // per leaf: object, sub-object, sweep position of its first triangle
+    // 4-wide triangle accelerator (tri_wide.h), used by the kWide instances instead of tri_bvh / tri_prims
+    const float4* __restrict__ tri_wide;          // TriWideNode[tri_nodes] as 8 float4 each
+    const uint4* __restrict__ tri_leaves;         // TriLeaf as 4 uint4 each
+    const TriVertex* __restrict__ tri_verts;      // compact leaves' vertex blocks
     // textures (bindings 9, 11), RGBA8 sRGB, + decode table
     const uint32_t* __restrict__ textures;
     const uint32_t* __restrict__ env;
@@ -198,5 +204,6 @@ struct KernelArgs {
     uint32_t lds_nodes_offset;
     uint32_t lds_tri_nodes_offset;
     uint32_t lds_tri_prims_offset;
+    uint32_t lds_stack_offset;    // kWide: the walk's per-lane stack, tri_stack_depth x threads u32
     uint32_t lds_srgb_offset;
 };

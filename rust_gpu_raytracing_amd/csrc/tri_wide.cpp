@@ -96,7 +96,7 @@ bool wide_leaf_make_compact(const float* hot16, uint32_t n_tri, TriLeaf& leaf, s
         vsrc.push_back(src[f]);
     }
     std::memcpy(leaf.idx, idx, sizeof(idx));
-    leaf.count_flags |= kWideLeafCompact;
+    leaf.count_flags |= kWideLeafCompact | kWideLeafCompactBuilt;
     return true;
 }
 
@@ -166,8 +166,11 @@ void build_triangle_wide(const rt_object_info* objects, uint32_t object_count, c
             kids[best] = c + 1;
             kids[n++] = bin[c + 1].skip;
         }
-        // slot order: keep the binary tree's left-to-right order
-        std::sort(kids, kids + n);
+        // slot order: internal children first, then leaves, each in the binary tree's order
+        std::sort(kids, kids + n, [&](uint32_t x, uint32_t y) {
+            const bool lx = is_leaf(x), ly = is_leaf(y);
+            return lx != ly ? ly : x < y;
+        });
         return n;
     };
     std::vector<TriWideNode>& nodes = out->nodes;
@@ -191,7 +194,7 @@ void build_triangle_wide(const rt_object_info* objects, uint32_t object_count, c
         for (uint32_t s = 0; s < n; s++) n_int += is_leaf(kids[s]) ? 0u : 1u;
         nd.child_base = (uint32_t)nodes.size();
         nd.leaf_base = (uint32_t)out->leaves.size();
-        uint32_t ci = 0;
+        nd.slots = n_int | ((n - n_int) << 4);
         std::vector<uint32_t> to_fill;
         for (uint32_t s = 0; s < n; s++) {
             const uint32_t b = kids[s];
@@ -199,15 +202,10 @@ void build_triangle_wide(const rt_object_info* objects, uint32_t object_count, c
                 nd.lo[k][s] = bin[b].bmin[k];
                 nd.hi[k][s] = bin[b].bmax[k];
             }
-            if (is_leaf(b)) {
-                nd.slots |= 1u << (4 + s);
+            if (is_leaf(b))
                 out->leaves.push_back(leaves[order[bin[b].leaf & 0xffffffu]]);
-            } else {
-                nd.slots |= 1u << s;
-                const uint32_t cw = nd.child_base + ci++;
-                (void)cw;
+            else
                 to_fill.push_back(b);
-            }
         }
         for (uint32_t b : to_fill) {
             nodes.emplace_back();
@@ -220,9 +218,9 @@ void build_triangle_wide(const rt_object_info* objects, uint32_t object_count, c
     fill(0);
     // leaf slot boxes: the exact culling boxes (the binary builder rounded them outward)
     for (TriWideNode& nd : nodes)
-        for (uint32_t s = 0, r = 0; s < kWideArity; s++) {
-            if (!((nd.slots >> (4 + s)) & 1u)) continue;
-            const TriLeaf& L = out->leaves[nd.leaf_base + r++];
+        for (uint32_t r = 0; r < (nd.slots >> 4); r++) {
+            const uint32_t s = (nd.slots & 0xfu) + r;
+            const TriLeaf& L = out->leaves[nd.leaf_base + r];
             float clo[3], chi[3];
             bool finite;
             leaf_cull_box(L.mn, L.mx, clo, chi, &finite);

@@ -33,6 +33,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define RT_WIDE_FN __host__ __device__ __forceinline__
 #else
 #define RT_WIDE_FN inline
@@ -42,16 +43,20 @@ constexpr uint32_t kWideArity = 4;
 constexpr uint32_t kWideLeafTris = 8;       // triangles per leaf record at most (sub-objects split into chunks)
 constexpr uint32_t kWideLeafVerts = 16;     // vertices of a compact leaf at most (4-bit indices)
 constexpr uint32_t kWideMaxDepth = 32;      // stack entries the kernel reserves at most (deeper trees: binary walk)
-constexpr uint32_t kWideLeafCompact = 0x100u;  // TriLeaf::count_flags
+constexpr uint32_t kWideLeafCompact = 0x100u;       // TriLeaf::count_flags: the vertex block is valid now
+constexpr uint32_t kWideLeafCompactBuilt = 0x200u;  // the leaf has a vertex block (validity rechecked on updates)
 
 // 128 B, one L2 line. Boxes structure-of-arrays so the four slab tests read
 // lo[axis] / hi[axis] of the four slots as float4s.
 struct TriWideNode {
     float lo[3][4];       // lo[axis][slot]: the inflation-free box, rounded outward (culling only)
     float hi[3][4];
-    uint32_t child_base;  // first internal child (a node's internal children are contiguous, in slot order)
-    uint32_t leaf_base;   // first leaf record (a node's leaves are contiguous, in slot order)
-    uint32_t slots;       // bit k: slot k is internal; bit 4 + k: slot k is a leaf; neither: empty
+    // slots [0, n_internal) are internal children, child_base + slot;
+    // slots [n_internal, n_internal + n_leaves) are leaves, leaf_base + slot - n_internal;
+    // the rest are empty (their boxes are never tested)
+    uint32_t child_base;
+    uint32_t leaf_base;
+    uint32_t slots;       // n_internal | n_leaves << 4
     uint32_t _pad[5];
 };
 static_assert(sizeof(TriWideNode) == 128, "wide node = one 128-B line");
@@ -63,7 +68,8 @@ struct TriLeaf {
     float mx[3];
     uint32_t seq_base;    // position of that triangle in the reference's sweep order (tie-break, :457)
     uint32_t object;      // object index (its ray_in_bounds, :431; material and uv of a hit, :506, :568)
-    uint32_t count_flags; // bits 0-7: triangles; kWideLeafCompact: vertices + indices below are valid
+    uint32_t count_flags; // bits 0-7: triangles; kWideLeafCompactBuilt / kWideLeafCompact: a vertex block exists /
+                          // reproduces the triangle records (then the leaf test reads it)
     uint32_t vbase;       // compact: first vertex of the leaf's block in the vertex array
     uint32_t sub;         // sub-object index (the device refit copies its bounds)
     uint32_t idx[4];      // compact: triangle j's vertex k is nibble 3j + k (idx[0] bits 0-3 first)
@@ -96,7 +102,7 @@ RT_WIDE_FN uint32_t wide_leaf_index(const uint32_t* idx, uint32_t j, uint32_t k)
     return (idx[n >> 3] >> ((n & 7u) * 4u)) & 0xfu;
 }
 
-#if !defined(__HIP_DEVICE_COMPILE__)
+// ---- host side -----------------------------------------------------------
 #include <vector>
 
 #include "rt_abi.h"
@@ -126,4 +132,3 @@ void build_triangle_wide(const rt_object_info* objects, uint32_t object_count, c
 // returns whether it did.
 bool wide_leaf_make_compact(const float* hot16, uint32_t n_tri, TriLeaf& leaf, std::vector<TriVertex>& verts,
                             std::vector<uint32_t>& vsrc);
-#endif

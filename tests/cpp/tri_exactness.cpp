@@ -2,17 +2,23 @@
 // kernel's BVH traversal logic (same f32 operation order, -ffp-contract=off)
 // must return exactly the triangle, object and distance of the reference's
 // sequential sweep (check_triangles, compute_shader.wgsl:422-517).
+// The 4-wide accelerator (tri_wide.h: 4-slot nodes, stack walk, compact vertex-
+// block leaves) is checked the same way, ray by ray.
 // usage: tri_exactness <objects.bin> <subs.bin> <tris.bin> <rays.f32> [margin_scale]
-//   -> "ok <rays> <hits> <avg_tri_tests> <avg_nodes> <nan_fallbacks>" or the first mismatch
+//   -> "ok <rays> <hits> <avg_tri_tests> <avg_nodes> <nan_fallbacks>"
+//      "wide <avg_tri_tests> <avg_node_loads> <compact_leaves> <leaves> <depth> <max_stack>"
+//   or the first mismatch
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
 #include "rt_bvh_slab.h"
 #include "sphere_bvh.h"
+#include "tri_wide.h"
 
 static const float F32_MAX_ = 3.4028235e+38f;
 struct V { float x, y, z; };
@@ -132,6 +138,103 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     return r;
 }
 
+static long w_tests = 0, w_nodes = 0;
+static uint32_t w_max_stack = 0;
+
+// The kernel's wide walk (pathtrace.hip: wide_node_step / tri_leaf_wide), leaves
+// tested as soon as they are reached (the kernel's batching only reorders leaf
+// tests, which the lexicographic minimum does not see).
+static Res wide(const TriWide& W, const std::vector<rt_object_info>& ob, const std::vector<rt_scene_triangle>& tr, V o,
+                V d, float scale) {
+    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    float m = scale * (std::sqrt(dot(o, o)) + W.extent) + 1.0e-30f;
+    float best = F32_MAX_;
+    uint32_t best_seq = 0;
+    Res r{F32_MAX_, -1, -1, 0};
+    bool nan_hit = false;
+    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
+    if (W.nodes.empty()) return r;
+    std::vector<uint32_t> stack;
+    uint32_t node = 0;
+    while (true) {
+        if (node == 0xffffffffu) {
+            if (stack.empty()) break;
+            uint32_t& e = stack.back();
+            node = (e >> 4) + (uint32_t)__builtin_ctz(e & 0xfu);
+            e &= e - 1u;
+            if ((e & 0xfu) == 0u) stack.pop_back();
+        }
+        w_nodes++;
+        const TriWideNode& nd = W.nodes[node];
+        const uint32_t n_int = nd.slots & 0xfu, n_slots = n_int + ((nd.slots >> 4) & 0xfu);
+        uint32_t hit = 0;
+        for (uint32_t k = 0; k < 4; k++) {
+            float nt, ft;
+            slab_hit(sr, nd.lo[0][k], nd.lo[1][k], nd.lo[2][k], nd.hi[0][k], nd.hi[1][k], nd.hi[2][k], nt, ft);
+            if (nt <= ft && ft >= 0.0f) hit |= 1u << k;
+        }
+        hit &= (1u << n_slots) - 1u;
+        const uint32_t hl = hit >> n_int, hi = hit & ((1u << n_int) - 1u);
+        for (uint32_t q = 0; q < 4; q++) {
+            if (!((hl >> q) & 1u)) continue;
+            const TriLeaf& L = W.leaves[nd.leaf_base + q];
+            const rt_object_info& OB = ob[L.object];
+            if (!rib(o, inv, OB.min_bounds, OB.max_bounds) || !rib(o, inv, L.mn, L.mx)) continue;
+            const uint32_t count = L.count_flags & 0xffu;
+            const bool compact = (L.count_flags & kWideLeafCompact) != 0u;
+            for (uint32_t j = 0; j < count; j++) {
+                w_tests++;
+                const uint32_t ti = L.first_tri + j, seq = L.seq_base + j;
+                V a, eab, eac, cn;
+                if (compact) {
+                    const TriVertex& va = W.verts[L.vbase + wide_leaf_index(L.idx, j, 0)];
+                    const TriVertex& vb = W.verts[L.vbase + wide_leaf_index(L.idx, j, 1)];
+                    const TriVertex& vc = W.verts[L.vbase + wide_leaf_index(L.idx, j, 2)];
+                    float ab3[3], ac3[3], cn3[3];
+                    wide_tri_from_vertices(va, vb, vc, ab3, ac3, cn3);
+                    a = {va.x, va.y, va.z};
+                    eab = ld(ab3);
+                    eac = ld(ac3);
+                    cn = ld(cn3);
+                } else {
+                    const rt_scene_triangle& t = tr[ti];
+                    a = ld(t.a);
+                    eab = ld(t.edge_ab);
+                    eac = ld(t.edge_ac);
+                    cn = ld(t.calc_normal);
+                }
+                float det = -dot(d, cn), inv_det = 1.0f / det;
+                V ao = sub(o, a);
+                float dist = dot(ao, cn) * inv_det;
+                bool nan_dist = dist != dist;
+                if (dist < 0.0f) continue;
+                if (!nan_dist && !(dist < best || (dist == best && seq < best_seq))) continue;
+                V dao = cross(ao, d);
+                float v = -dot(eab, dao) * inv_det;
+                if (v < 0.0f) continue;
+                float u = dot(eac, dao) * inv_det;
+                if (u < 0.0f) continue;
+                float w = 1.0f - u - v;
+                if (w < 0.0f) continue;
+                if (nan_dist) { nan_hit = true; continue; }
+                best = dist;
+                best_seq = seq;
+                r = {dist, (int)ti, (int)L.object, det > 0.0f};
+            }
+        }
+        if (hi != 0u) {
+            const uint32_t rest = hi & (hi - 1u);
+            if (rest) stack.push_back((nd.child_base << 4) | rest);
+            node = nd.child_base + (uint32_t)__builtin_ctz(hi);
+        } else {
+            node = 0xffffffffu;
+        }
+        w_max_stack = std::max<uint32_t>(w_max_stack, (uint32_t)stack.size());
+    }
+    if (nan_hit) return {F32_MAX_, -2, -2, 0};  // the kernel reruns the sweep: checked by the caller
+    return r;
+}
+
 int main(int argc, char** argv) {
     if (argc < 5) return 2;
     auto ob = load<rt_object_info>(argv[1]);
@@ -141,20 +244,41 @@ int main(int argc, char** argv) {
     float scale = argc > 5 ? (float)atof(argv[5]) : 1.0e-5f;
     TriangleAccel A;
     build_triangle_accel(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), &A);
+    // the wide accelerator, with compact leaves from the records in the kernel's 64-B layout
+    std::vector<float> hot(16 * tr.size());
+    for (size_t i = 0; i < tr.size(); i++) {
+        const rt_scene_triangle& t = tr[i];
+        const float f[16] = {t.a[0], t.a[1], t.a[2], t.edge_ab[0], t.edge_ab[1], t.edge_ab[2], t.edge_ac[0], t.edge_ac[1],
+                             t.edge_ac[2], t.calc_normal[0], t.calc_normal[1], t.calc_normal[2], t.face_normal[0],
+                             t.face_normal[1], t.face_normal[2], 0.0f};
+        memcpy(&hot[16 * i], f, sizeof(f));
+    }
+    TriWide W;
+    build_triangle_wide(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), hot.data(), (uint32_t)tr.size(),
+                        &W);
     long n = (long)rays.size() / 6, hits = 0;
     for (long i = 0; i < n; i++) {
         V o = ld(&rays[6 * i]), d = ld(&rays[6 * i + 3]);
         Res a = sweep(ob, sb, tr, o, d), b = accel(A, ob, sb, tr, o, d, scale);
-        uint32_t ta, tb;
-        memcpy(&ta, &a.t, 4);
-        memcpy(&tb, &b.t, 4);
-        if (ta != tb || a.tri != b.tri || a.obj != b.obj || a.front != b.front) {
-            printf("MISMATCH ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n", i, o.x,
-                   o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, b.obj, b.tri, b.t);
-            return 1;
+        Res c = wide(W, ob, tr, o, d, scale);
+        if (c.tri == -2) c = sweep(ob, sb, tr, o, d);  // NaN distance met: the kernel's sweep fallback
+        for (const Res* x : {&b, &c}) {
+            uint32_t ta, tb;
+            memcpy(&ta, &a.t, 4);
+            memcpy(&tb, &x->t, 4);
+            if (ta != tb || a.tri != x->tri || a.obj != x->obj || a.front != x->front) {
+                printf("MISMATCH (%s) ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n",
+                       x == &b ? "binary" : "wide", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
+                       x->t);
+                return 1;
+            }
         }
         hits += a.tri >= 0;
     }
+    long compact = 0;
+    for (const TriLeaf& L : W.leaves) compact += (L.count_flags & kWideLeafCompact) ? 1 : 0;
     printf("ok %ld %ld %.2f %.2f %ld\n", n, hits, (double)g_tests / n, (double)g_nodes / n, g_nan);
+    printf("wide %.2f %.2f %ld %zu %u %u\n", (double)w_tests / n, (double)w_nodes / n, compact, W.leaves.size(), W.depth,
+           w_max_stack);
     return 0;
 }

@@ -607,6 +607,60 @@ def test_gpu_reference_sweep_without_accelerator(gpu, oracle_lib, monkeypatch, c
     assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
 
 
+@pytest.mark.parametrize("wide,compact", [("0", None), ("1", "0"), ("1", "1")])
+@pytest.mark.parametrize("config,kw", [("c3_chess", dict(env_size=(512, 256))), ("c4_mixed", dict(env_size=(256, 128))),
+                                       ("c5_heightfield", dict(nx=60, nz=30))])
+def test_gpu_triangle_accelerators(gpu, oracle_lib, monkeypatch, config, kw, wide, compact):
+    """Both triangle accelerators against the oracle: the binary stackless walk
+    (RT_TRI_WIDE=0) and the 4-wide stack walk (tri_wide.h), whose leaves either read
+    the triangle records (RT_TRI_COMPACT=0) or recompute them from vertex blocks
+    (RT_TRI_COMPACT=1; by default only for meshes beyond one XCD's L2)."""
+    monkeypatch.setenv("RT_TRI_WIDE", wide)
+    if compact is not None:
+        monkeypatch.setenv("RT_TRI_COMPACT", compact)
+    scene, bounces = build_config(config, width=96, height=64, **kw)
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
+    assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
+
+
+def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
+    """rt_update_triangles with records a compact leaf cannot reproduce (calc_normal
+    off by a few ulp): the device recheck turns those leaves back to reading the
+    records, and restores compactness when consistent records return -- the image
+    follows the oracle given the same records each time."""
+    monkeypatch.setenv("RT_TRI_COMPACT", "1")
+    scene, bounces = build_config("c5_heightfield", width=80, height=48, nx=50, nz=25)
+    objs, subs, tris = scene.flatten()
+    bad = tris.copy()
+    sel = np.arange(0, bad.shape[0], 5)
+    bad["calc_normal"][sel] *= np.float32(1.0000002)
+    with Renderer(scene) as r:
+        r.compute_frame(bounces)
+        r._call("rt_update_triangles", N.ptr(bad), bad.shape[0])
+        r.reset_accumulation()
+        r.compute_frame(bounces)
+        got_bad = r.read_accumulation(), r.read_output(), r.ray_count()
+        r._call("rt_update_triangles", N.ptr(tris), tris.shape[0])
+        r.reset_accumulation()
+        r.reset_ray_count()
+        r.compute_frame(bounces)
+        got_good = r.read_accumulation(), r.read_output(), r.ray_count()
+    o = oracle_lib.Oracle(scene)
+    acc = np.zeros((48, 80, 4), np.float32)
+    out = np.zeros((48, 80), np.uint32)
+    n = o.render_frame(scene.params(accumulation_index=1), bounces, acc, out)
+    assert_same(*got_good, acc, out, n)
+    # the inconsistent records, through the oracle
+    bad_scene, _ = build_config("c5_heightfield", width=80, height=48, nx=50, nz=25)
+    bad_scene.objects[0].triangles = bad
+    ob = oracle_lib.Oracle(bad_scene)
+    acc_b = np.zeros((48, 80, 4), np.float32)
+    out_b = np.zeros((48, 80), np.uint32)
+    nb = ob.render_frame(bad_scene.params(accumulation_index=1), bounces, acc_b, out_b)
+    assert np.array_equal(got_bad[1], out_b)
+    assert np.array_equal(got_bad[0].view(np.uint32), acc_b.view(np.uint32))
+
+
 def _pcg_f32(seed):
     state = (seed * 747796405 + 2891336453) & 0xFFFFFFFF
     word = (((state >> ((state >> 28) + 4)) ^ state) * 277803737) & 0xFFFFFFFF

@@ -24,7 +24,8 @@ def harness(tmp_path_factory):
     exe = tmp_path_factory.mktemp("tri") / "tri_exactness"
     subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", f"-I{ROOT / 'include'}",
                     f"-I{ROOT / 'rust_gpu_raytracing_amd' / 'csrc'}", str(ROOT / "tests" / "cpp" / "tri_exactness.cpp"),
-                    str(ROOT / "rust_gpu_raytracing_amd" / "csrc" / "sphere_bvh.cpp"), "-o", str(exe)], check=True)
+                    str(ROOT / "rust_gpu_raytracing_amd" / "csrc" / "sphere_bvh.cpp"),
+                    str(ROOT / "rust_gpu_raytracing_amd" / "csrc" / "tri_wide.cpp"), "-o", str(exe)], check=True)
     return exe
 
 
@@ -65,8 +66,12 @@ def test_heightfield_and_grazing_rays(harness, tmp_path):
     d = np.stack([rng.uniform(-1, 1, n), rng.uniform(0.0, 0.2, n) ** 3, rng.uniform(-1, 1, n)], axis=1)  # grazing
     out = run(harness, tmp_path, objs, subs, tris, np.concatenate([o, d], axis=1))
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
-    _, nr, hits, tests, nodes, _ = out.stdout.split()
+    _, nr, hits, tests, nodes, _ = out.stdout.splitlines()[0].split()
     assert float(tests) < 0.05 * tris.shape[0]  # the accelerator culls
+    _, w_tests, w_nodes, compact, leaves, depth, max_stack = out.stdout.splitlines()[1].split()
+    assert int(compact) == int(leaves)  # every heightfield strip is a compact leaf
+    assert float(w_nodes) < 0.75 * float(nodes)  # 4-wide: fewer node loads than the binary walk's box tests
+    assert int(max_stack) < int(depth) <= 32
 
 
 def test_shared_subobjects_duplicates_and_ties(harness, tmp_path):
@@ -90,7 +95,7 @@ def test_shared_subobjects_duplicates_and_ties(harness, tmp_path):
     rays = random_rays(rng, 40000, [-2, -3, -2], [2, 1, 2])
     out = run(harness, tmp_path, objs, subs, tris, rays)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
-    assert int(out.stdout.split()[2]) > 1000  # plenty of hits exercised the tie rule
+    assert int(out.stdout.splitlines()[0].split()[2]) > 1000  # plenty of hits exercised the tie rule
 
 
 def test_nan_distance_falls_back_to_the_sweep(harness, tmp_path):
@@ -108,7 +113,7 @@ def test_nan_distance_falls_back_to_the_sweep(harness, tmp_path):
     rays = np.array([[-3, 0.5, 0.1, 1, 0, 0], [0.2, 0.5, -3, 0, 0, 1], [0, 0, 0, 0, 1, 0.01]], np.float32)
     out = run(harness, tmp_path, objs, o.sub_object_info.astype(B.SUB_OBJECT_INFO), t, rays)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
-    assert int(out.stdout.split()[-1]) >= 1  # the fallback ran
+    assert int(out.stdout.splitlines()[0].split()[-1]) >= 1  # the fallback ran
 
 
 def test_margin_is_load_bearing(harness, tmp_path):
@@ -117,3 +122,24 @@ def test_margin_is_load_bearing(harness, tmp_path):
     rays = random_rays(np.random.default_rng(3), 40000, [-12, -8, -12], [12, 8, 12])
     out = run(harness, tmp_path, objs, subs, tris, rays, margin="-0.02")  # shrunken boxes must be caught
     assert out.returncode == 1 and "MISMATCH" in out.stdout
+
+
+def test_wide_large_sub_objects_and_inconsistent_records(harness, tmp_path):
+    """Sub-objects of 20 triangles (split into leaf records of 8 sharing one box) and
+    triangle records whose calc_normal does not follow from their edges (uploaded data
+    need not be consistent: those leaves must read the records, not recompute)."""
+    scene, _ = build_config("c5_heightfield", width=8, height=8, nx=40, nz=20)
+    obj = scene.objects[0]
+    obj.create_sub_objects(0, 0, n=20)
+    objs, subs, tris = scene.flatten()
+    tris = tris.copy()
+    bad = np.arange(0, tris.shape[0], 97)
+    tris["calc_normal"][bad] *= np.float32(1.0000001)  # one ulp-ish off: not SceneTriangle::new's result
+    rng = np.random.default_rng(5)
+    n = 30000
+    o = np.stack([rng.uniform(-20, 20, n), rng.uniform(-3, 0.4, n), rng.uniform(-20, 10, n)], axis=1)
+    d = np.stack([rng.uniform(-1, 1, n), rng.uniform(0.0, 1.0, n), rng.uniform(-1, 1, n)], axis=1)
+    out = run(harness, tmp_path, objs, subs, tris, np.concatenate([o, d], axis=1))
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
+    _, w_tests, w_nodes, compact, leaves, depth, max_stack = out.stdout.splitlines()[1].split()
+    assert 0 < int(compact) < int(leaves)  # both kinds of leaves exercised

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--frame-batch", type=int, default=1, help="frames per launch (rt_set_frame_batch)")
     args = ap.parse_args()
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     dirs = scene.camera.recalculate_ray_directions()
@@ -36,11 +37,12 @@ def main():
         for kv in spec.split():
             k, v = kv.split("=", 1)
             os.environ[k] = v
-        rs.append(Renderer(scene, camera_rays=dirs))
+        rs.append(Renderer(scene, camera_rays=dirs, frame_batch=args.frame_batch))
         os.environ.clear()
         os.environ.update(saved)
     for r in rs:
-        r.compute_frame(bounces)
+        for _ in range(args.frame_batch):
+            r.compute_frame(bounces)
         r.synchronize()
     times = {s: [] for s in args.specs}
     rays = {}
@@ -54,12 +56,13 @@ def main():
             r.synchronize()
             r.set_timing(False)
             ms, n = r.dispatch_time_total()
-            times[s].append(ms / n)
+            rms, _ = r.resolve_time_total()
+            times[s].append((ms + rms) / args.frames)  # device time per frame (path kernel + resolve)
             rays[s] = r.ray_count() / args.frames
     ref = rs[0].read_accumulation().view(np.uint32)
     for (s, t), r in zip(times.items(), rs):
         med = statistics.median(t)
-        print(json.dumps({"spec": s, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+        print(json.dumps({"config": args.config, "spec": s, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
                           "mray_s": round(rays[s] / med / 1e3, 1),
                           "bit_identical_to_first": bool(np.array_equal(r.read_accumulation().view(np.uint32), ref)),
                           "launch": r.launch_config()}))
