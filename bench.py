@@ -183,6 +183,9 @@ def main() -> int:
                     help="N>1 route: torch = one process per GPU (torch.distributed.run, RCCL via ProcessGroupNCCL); "
                          "group = one process driving --gpus devices through the C ABI (rt_create_multi, "
                          "rt_gather_frame: RCCL send/recv), the Rust host's route")
+    ap.add_argument("--brute-force", action="store_true",
+                    help="the reference's own sweeps, LDS-tiled (rt_set_brute_force; BASELINE config 5's stress "
+                         "mode) instead of the acceleration structures")
     ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
                     help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N, steps)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
@@ -238,6 +241,8 @@ def main() -> int:
         scene, default_bounces = build_config(args.config, width=width, height=height)
         bounces = args.bounces or default_bounces
         r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=frame_batch)
+        if args.brute_force:
+            r.set_brute_force(True)
 
         def barrier_sync():
             r.synchronize()
@@ -311,6 +316,7 @@ def main() -> int:
             t_gather = t_gather_image if args.gather == "image" else t_gather_accum
         t_render = t_total - t_gather
         res = dict(r=r, scene=scene, bounces=bounces, width=width, height=height, rays=r.ray_count(),
+                   streamed=r.streamed_bytes(),
                    settle_frames=settle_frames,
                    t_render=t_render, t_gather=t_gather, gathered=gathered, launch=r.launch_config(),
                    timing=r.dispatch_time_total(), resolve_timing=r.resolve_time_total(),
@@ -440,9 +446,15 @@ def main() -> int:
         frames_per_launch = args.steps / max(n_timed, 1)
         rays_per_launch = m["rays"] / max(n_timed, 1)
         b_launch = algorithmic_bytes(m["owned_px"], rays_per_launch, scene_bytes(scene), frames_per_launch)
+        # brute-force launches also stream the sub-object records through LDS once per
+        # workgroup and bounce: SURVEY §8d's tile-streaming term, counted by the kernel
+        stream_launch = m.get("streamed", 0) / max(n_timed, 1)
+        b_launch += stream_launch
         achieved = b_launch / avg_kernel_s / 1e9
         eff_launch_s = m["t_render"] / max(n_timed, 1)  # wall time per launch: overlapped launches pipeline
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
+        if args.brute_force:
+            workload += ", brute-force LDS-tiled sweeps"
         build_hash = native_build.source_hash()
         pmc, pmc_why = pmc_entry(f"{workload} | frame_batch {fb}", build_hash) if world == 1 else (None, "N>1")
         result = {
@@ -496,6 +508,7 @@ def main() -> int:
                 "frames_per_launch": frames_per_launch,
                 "launch": m["launch"],
                 "bytes_per_launch": b_launch,
+                "tile_stream_bytes_per_launch": stream_launch,
                 "note": "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction",
                 "valu": pmc_issue(pmc),
                 "build_hash": build_hash,

@@ -116,6 +116,8 @@ SIGNATURES = {
     "rt_ray_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_reset_ray_count": (ctypes.c_int, [_P]),
     "rt_accumulation_index": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_set_brute_force": (ctypes.c_int, [_P, ctypes.c_int]),
+    "rt_streamed_bytes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_set_tile_schedule": (ctypes.c_int, [_P, _U32]),
     "rt_tile_schedule_state": (ctypes.c_int, [_P, _P, _P]),
     "rt_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),

@@ -1467,6 +1467,199 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     X(0, 1024, false, false) X(1, 256, false, false) X(1, 512, false, false) X(1, 1024, false, false)          \
     RT_EXTRA_CONFIGS(X)
 
+// ---- the reference's brute-force sweep, LDS-tiled (BASELINE.json config 5) -----
+//
+// rt_brute_kernel renders a batch of frames the way compute_shader.wgsl does --
+// one invocation per pixel (:146-189), every sphere tested (:355-404), every
+// object's box and every sub-object's box tested in order and the triangles of
+// the sub-objects hit (:422-517) -- with no acceleration structure. What is
+// MI355X-specific is how the sub-object array reaches the lanes: a workgroup of
+// 256 pixels steps through its paths one bounce at a time, and for each bounce
+// streams the object's sub-object records through LDS in tiles of
+// kBruteTileSubs (coalesced 16-B loads, one pass per workgroup and bounce instead
+// of one per pixel); every lane then tests the tile's boxes with LDS broadcast
+// reads (all lanes read the same record), and a sub-object's triangles are loaded
+// only for the lanes whose box test passed (the wave's exec mask is the ballot of
+// the per-lane hits). Same arithmetic and order as the reference's sweep: the
+// first of equal distances wins (`>=` rejects, :457), a NaN distance is accepted
+// and makes later candidates accepted (:449-481), spheres by (t, index).
+// HBM traffic: the framebuffer (SURVEY §8d, 52 B/px/frame), texels, and the
+// tile-streaming term -- 32 B x sub-objects per workgroup and bounce, counted in
+// KernelArgs::stream_bytes.
+constexpr uint32_t kBruteThreads = 256;     // 4 8x8 tiles per workgroup
+constexpr uint32_t kBruteTileSubs = 1024;   // sub-object records per LDS tile (32 KB)
+
+template <bool kTris>
+__global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t block_rays;
+    const uint32_t tid = threadIdx.x;
+    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
+    // scene staging as the persistent kernel's mode 1 (spheres in slot order, materials + glass
+    // constants, objects, sRGB table), then the sub-object tile
+    float4* l_sph = reinterpret_cast<float4*>(lds);
+    RtMaterial* l_mat = reinterpret_cast<RtMaterial*>(lds + ka.lds_mat_offset);
+    float4* l_aux = reinterpret_cast<float4*>(lds + ka.lds_mat_aux_offset);
+    RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
+    uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
+    uint32_t* l_smat = reinterpret_cast<uint32_t*>(lds + ka.lds_smat_offset);
+    float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
+    RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_stack_offset);
+    for (uint32_t i = tid; i < ka.sphere_slot_count; i += kBruteThreads) {
+        l_sph[i] = ka.sphere_slots[i];
+        l_orig[i] = ka.sphere_orig[i];
+    }
+    for (uint32_t i = tid; i < ka.sphere_count; i += kBruteThreads) l_smat[i] = ka.sphere_material[i];
+    for (uint32_t i = tid; i < ka.material_count; i += kBruteThreads) {
+        const RtMaterial m = ka.materials[i];
+        l_mat[i] = m;
+        const float ior_front = 1.0f / m.refraction_index;
+        float r0f = (1.0f - ior_front) / (1.0f + ior_front);
+        float r0b = (1.0f - m.refraction_index) / (1.0f + m.refraction_index);
+        r0f = r0f * r0f;
+        r0b = r0b * r0b;
+        l_aux[2u * i] = make_float4(ior_front, r0f, r0b, div_const(m.roughness, 10.0f, kInv10));
+        const f4 c = decode_texel(ka.textures[min(m.texture_index, ka.tex_layers - 1u)], ka.srgb);
+        l_aux[2u * i + 1u] = make_float4(c.x, c.y, c.z, c.w);
+    }
+    if constexpr (kTris)
+        for (uint32_t i = tid; i < ka.object_count; i += kBruteThreads) l_obj[i] = ka.objects[i];
+    for (uint32_t i = tid; i < 256u; i += kBruteThreads) l_srgb[i] = ka.srgb[i];
+    float* l_cam = l_srgb + 256;  // camera block for device-side primary rays
+    if (tid < 16u) {
+        l_cam[tid] = ka.inv_proj[tid];
+        l_cam[16u + tid] = ka.inv_view[tid];
+    }
+    if (tid == 0) {
+        l_cam[32] = ka.aspect;
+        block_rays = 0;
+    }
+    __syncthreads();
+    SceneView sv{l_sph, l_orig, l_smat, nullptr, l_mat, l_aux, l_obj, l_srgb, nullptr, nullptr, 0.0f,
+                 nullptr, nullptr, 0u};
+
+    // this thread's pixel: local tile blockIdx * 4 + tid / 64 (global tile local * world + rank)
+    const uint32_t local_tile = blockIdx.x * (kBruteThreads / 64u) + (tid >> 6);
+    const uint32_t slot = tid & 63u;
+    const uint32_t gt = local_tile * ka.world_size + ka.rank;
+    const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);
+    const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
+    const bool valid = local_tile < ka.owned_tiles && x < ka.width && y < ka.height;
+    const uint32_t index = valid ? y * ka.width + x : 0u;
+    const bool accumulate = ka.accumulate == 1u;
+    const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;
+    uint32_t rays = 0;
+    uint64_t streamed = 0;  // sub-object records this workgroup loaded (tid 0 counts)
+    float4 pix = valid && accumulate ? ka.accum[index] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const f3 cam = valid ? pixel_ray(ka, l_cam, index, x, y) : mk(0.f, 0.f, 1.f);
+    Path p;
+    for (uint32_t frame = 0; frame < ka.frames; ++frame) {
+        for (uint32_t sample = 0; sample < samples; ++sample) {
+            const uint32_t random_index = ka.accumulation_index + (accumulate ? frame : 0u) + sample;
+            start_sample(ka, index, random_index, cam, p);
+            bool alive = valid && p.bounce < ka.bounces;
+            while (true) {
+                // the workgroup traces together while any of its paths is alive
+                if (!__syncthreads_or(alive)) break;
+                // check_spheres (:355-404), every sphere (the (t, index) rule makes slot order free)
+                TraceState ts;
+                ts.sph = SphereHit{kF32Max, 0u, 0u};
+                ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
+                const f3 o = p.o, d = p.d;
+                const float a = dot(d, d);
+                if (alive) {
+                    for (uint32_t i = 0; i < ka.sphere_slot_count; i += 4u)
+                        test_sphere_group(sv, i, o, d, 4.0f * a, 2.0f * a, ts.sph);
+                }
+                // check_triangles (:422-517): objects, then their sub-objects through LDS tiles
+                if constexpr (kTris) {
+                    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                    float closest = kF32Max;
+                    for (uint32_t oi = 0; oi < ka.object_count; ++oi) {
+                        const RtObject& ob = l_obj[oi];
+                        const bool in_obj = alive && ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds);
+                        if (!__syncthreads_or(in_obj)) continue;  // no lane of the workgroup enters the object
+                        const uint32_t first = ob.first_sub_object_index, n_sub = ob.sub_object_count;
+                        for (uint32_t t0 = 0; t0 < n_sub; t0 += kBruteTileSubs) {
+                            const uint32_t nt = min(kBruteTileSubs, n_sub - t0);
+                            __syncthreads();  // the previous tile's readers are done
+                            const uint4* src = reinterpret_cast<const uint4*>(ka.sub_objects);
+                            uint4* dst = reinterpret_cast<uint4*>(l_sub);
+                            for (uint32_t q = tid; q < 2u * nt; q += kBruteThreads) {
+                                const uint32_t si = min(first + t0 + (q >> 1), ka.sub_object_count - 1u);
+                                dst[q] = src[2u * si + (q & 1u)];
+                            }
+                            if (tid == 0) streamed += nt;
+                            __syncthreads();
+                            if (!in_obj) continue;
+                            for (uint32_t k = 0; k < nt; ++k) {
+                                const RtSubObject& sub = l_sub[k];  // broadcast read
+                                if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
+                                for (uint32_t j = 0; j < sub.triangle_count; ++j) {
+                                    const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
+                                    const TriGeom g = load_tri(ka.triangles, ti);
+                                    const float det = -dot(d, g.cn);
+                                    const float inv_det = 1.0f / det;
+                                    const f3 ao = o - g.a;
+                                    const float dist = dot(ao, g.cn) * inv_det;
+                                    if (dist < 0.0f || dist >= closest) continue;
+                                    const f3 dao = cross(ao, d);
+                                    const float v = -dot(g.ab, dao) * inv_det;
+                                    if (v < 0.0f) continue;
+                                    const float u = dot(g.ac, dao) * inv_det;
+                                    if (u < 0.0f) continue;
+                                    const float w = 1.0f - u - v;
+                                    if (w < 0.0f) continue;
+                                    closest = dist;
+                                    ts.tri = TriHit{dist, 0u, ti, oi, det > 0.0f};
+                                }
+                            }
+                        }
+                    }
+                }
+                if (alive) {
+                    ++rays;
+                    const Hit h = trace_end<kTris>(sv, ka, o, d, ts);
+                    if (shade<true>(sv, ka, p, h)) alive = false;
+                }
+            }
+            if (accumulate && valid) {
+                pix.x = pix.x + p.light.x;
+                pix.y = pix.y + p.light.y;
+                pix.z = pix.z + p.light.z;
+                pix.w = pix.w + p.light.w;
+            }
+        }
+    }
+    if (valid) {  // the last frame's accumulation and output (:164-178)
+        float r, g, b, al;
+        if (accumulate) {
+            const float div = (float)((ka.accumulation_index + ka.frames - 1u) * ka.compute_per_frame);
+            r = clamp01(pix.x / div);
+            g = clamp01(pix.y / div);
+            b = clamp01(pix.z / div);
+            al = clamp01(pix.w / div);
+            ka.accum[index] = pix;
+        } else {
+            r = clamp01(p.light.x);
+            g = clamp01(p.light.y);
+            b = clamp01(p.light.z);
+            al = clamp01(p.light.w);
+        }
+        ka.output[index] = pack_rgba8(r, g, b, al);
+    }
+    atomicAdd(&block_rays, rays);
+    __syncthreads();
+    if (tid == 0) {
+        if (block_rays) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
+        if (streamed && ka.stream_bytes) atomicAdd(ka.stream_bytes, (unsigned long long)streamed * 32ull);
+    }
+    if (ka.launch_clock) {
+        __syncthreads();
+        if (tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
+    }
+}
+
 namespace {
 // Dynamic LDS above 64 KiB must be opted into per kernel.
 hipError_t allow_big_lds(const void* fn) {
@@ -1490,6 +1683,22 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool w
 #undef RT_LAUNCH
     return hipErrorInvalidValue;
 }
+
+hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream) {
+    const uint32_t blocks = (ka.owned_tiles + kBruteThreads / 64u - 1u) / (kBruteThreads / 64u);
+    if (blocks == 0) return hipSuccess;
+    const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_kernel<true>)
+                          : reinterpret_cast<const void*>(&rt_brute_kernel<false>);
+    hipError_t e = allow_big_lds(fn);
+    if (e != hipSuccess) return e;
+    if (tris)
+        hipLaunchKernelGGL(rt_brute_kernel<true>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+    else
+        hipLaunchKernelGGL(rt_brute_kernel<false>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+    return hipGetLastError();
+}
+
+size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
 
 // Picks the workgroup size for this LDS mode and footprint: the most resident
 // waves per CU up to kTargetWavesPerCu (measured on C2: 16 waves/CU beat 18

@@ -43,6 +43,8 @@ hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const 
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
+hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
+size_t rt_brute_tile_bytes();
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
                              uint32_t samples, uint32_t frames, unsigned long long* clock, hipStream_t stream);
@@ -234,6 +236,9 @@ struct rt_ctx {
     uint32_t* d_vsrc = nullptr;
     size_t wide_cap = 0, leaves_cap = 0, verts_cap = 0, vsrc_cap = 0;
     uint32_t wide_leaves = 0, wide_verts = 0, wide_depth = 0, wide_compact_leaves = 0;
+    // rt_set_brute_force: the reference's own sweeps, LDS-tiled (rt_brute_kernel; BASELINE config 5)
+    bool brute = false;
+    unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
     uint32_t tri_nodes = 0, tri_prim_count = 0;
     float* d_tri_extent = nullptr;   // margin extent, in device memory (refit updates it)
     uint32_t* d_tri_order = nullptr; // node indices by depth, deepest level first (refit)
@@ -699,6 +704,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         ctx->use_tri_bvh = !(env && env[0] == '0');
         env = std::getenv("RT_TRI_WIDE");
         ctx->use_tri_wide = !(env && env[0] == '0');
+        env = std::getenv("RT_BRUTE_FORCE");
+        ctx->brute = env && env[0] == '1';
         env = std::getenv("RT_TRI_COMPACT");
         if (env) ctx->tri_compact = env[0] == '0' ? 0 : 1;
         env = std::getenv("RT_SPHERE_LEAF");
@@ -763,7 +770,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
         (rc = dev_alloc(ctx, &ctx->d_tri_bounds, 2 * (size_t)ctx->n_tri_dev)) ||
-        (rc = dev_alloc(ctx, &ctx->d_tri_extent, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_tri_extent, 1)) || (rc = dev_alloc(ctx, &ctx->d_stream, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_srgb, 256)) || (rc = dev_alloc(ctx, &ctx->d_tex, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_env, 1)))
         return bail(rc);
@@ -799,7 +806,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
-                    ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc};
+                    ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1184,6 +1191,46 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         else
             carve(1, kLdsSceneBudget);
     }
+    if (ctx->brute) {
+        // the reference's sweeps (rt_brute_kernel): the mode-1 scene image, then one
+        // LDS tile of sub-object records; frames of a batch run back to back per pixel
+        carve(1, kLdsSceneBudget);
+        ka.lds_srgb_offset = (uint32_t)(mode1_bytes - kLdsTailBytes);
+        ka.lds_stack_offset = (uint32_t)al16(mode1_bytes);
+        const size_t lds = ka.lds_stack_offset + rt_brute_tile_bytes();
+        int dev = 0, max_optin = 0;
+        RT_HIP(ctx, hipGetDevice(&dev));
+        RT_HIP(ctx, hipDeviceGetAttribute(&max_optin, hipDeviceAttributeSharedMemPerBlockOptin, dev));
+        if (lds > (size_t)max_optin - 256)
+            return fail(ctx, RT_E_CAPACITY, "brute-force mode: spheres, materials and objects must fit in LDS");
+        ka.sphere_octant_stride = 0;
+        ka.sphere_boxes_ordered = 0;
+        ka.stream_bytes = ctx->d_stream;
+        ka.frame_light = nullptr;
+        RT_HIP(ctx, join_aux(ctx));
+        ka.launch_clock = nullptr;
+        if (ctx->timing) {
+            if (ctx->clock_pending.size() >= kClockSlots) {
+                const int rc = collect_timing(ctx);
+                if (rc) return rc;
+            }
+            if (!ctx->d_clock) {
+                const int rc = dev_alloc(ctx, &ctx->d_clock, kClockWords * (size_t)kClockSlots);
+                if (rc) return rc;
+            }
+            const uint32_t slot = ctx->clock_next;
+            ctx->clock_next = (ctx->clock_next + 1) % kClockSlots;
+            ka.launch_clock = ctx->d_clock + kClockWords * (size_t)slot;
+            RT_HIP(ctx, hipMemsetAsync(ka.launch_clock, 0, kClockWords * 8, ctx->stream));
+            ctx->clock_pending.push_back(slot);
+        }
+        RT_HIP(ctx, rt_launch_brute(ka, tris, lds, ctx->stream));
+        ctx->last_blocks = (ctx->owned_tiles + 3u) / 4u;
+        ctx->last_lds = (uint32_t)lds;
+        ctx->occ_threads = 256;
+        ctx->primary_dirty = true;
+        return RT_OK;
+    }
     ka.sphere_nodes = layouts * ctx->n_nodes;
     ka.sphere_octant_stride = layouts == 8 ? ctx->n_nodes : 0u;
     ka.sphere_boxes_ordered = (layouts == 8 && ctx->sphere_boxes_ordered && !tris) ? 1u : 0u;
@@ -1543,6 +1590,22 @@ int rt_ray_count(rt_ctx* ctx, uint64_t* out) {
     return RT_OK;
 }
 
+int rt_set_brute_force(rt_ctx* ctx, int enable) {
+    RT_ENTER(ctx);
+    ctx->brute = enable != 0;
+    return RT_OK;
+}
+
+int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out) {
+    RT_ENTER(ctx);
+    if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    unsigned long long v = 0;
+    RT_HIP(ctx, hipMemcpyAsync(&v, ctx->d_stream, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *out = v;
+    return RT_OK;
+}
+
 int rt_set_tile_schedule(rt_ctx* ctx, uint32_t schedule) {
     RT_ENTER(ctx);
     if (schedule > 1) return fail(ctx, RT_E_INVALID, "tile schedule must be 0 (index order) or 1 (cost-ordered)");
@@ -1580,6 +1643,7 @@ int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
     RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters) * sizeof(unsigned long long), ctx->stream));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_stream, 0, sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }
 

@@ -170,6 +170,8 @@ struct KernelArgs {
     // launch timing (rt_set_timing), null otherwise: {~earliest workgroup start, latest
     // workgroup end} on the device wall clock
     unsigned long long* __restrict__ launch_clock;
+    // brute-force launches (rt_brute_kernel): bytes of sub-object records streamed through LDS
+    unsigned long long* __restrict__ stream_bytes;
     uint32_t texture_width;
     uint32_t texture_height;
     uint32_t env_map_width;

@@ -297,6 +297,17 @@ class Renderer:
         self._call("rt_dispatch_time_total", ctypes.byref(ms), ctypes.byref(n))
         return ms.value, n.value
 
+    def set_brute_force(self, enable: bool) -> None:
+        """rt_set_brute_force: the reference's own sphere and triangle sweeps, LDS-tiled
+        (BASELINE config 5's stress mode), instead of the acceleration structures."""
+        self._call("rt_set_brute_force", int(enable))
+
+    def streamed_bytes(self) -> int:
+        """Sub-object bytes the brute-force launches streamed through LDS."""
+        v = ctypes.c_uint64()
+        self._call("rt_streamed_bytes", ctypes.byref(v))
+        return v.value
+
     def resolve_time_total(self):
         """(total milliseconds, number) of the timed batches' resolve passes
         (rt_resolve_frames_kernel), which dispatch_time_total does not include."""

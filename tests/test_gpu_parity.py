@@ -661,6 +661,39 @@ def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
     assert np.array_equal(got_bad[0].view(np.uint32), acc_b.view(np.uint32))
 
 
+@pytest.mark.parametrize("config,kw,batch,world", [
+    ("c1_four_spheres", {}, 1, 1),
+    ("c2_rtiow", {}, 3, 1),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 1),
+    ("c4_mixed", dict(env_size=(256, 128)), 2, 3),
+    ("c5_heightfield", dict(nx=60, nz=30), 2, 1),
+])
+def test_gpu_brute_force_mode(gpu, oracle_lib, config, kw, batch, world):
+    """rt_set_brute_force: the reference's own sphere and object -> sub-object ->
+    triangle sweeps, sub-objects streamed through LDS tiles (BASELINE config 5's
+    stress mode) -- bit-identical to the oracle, in frame batches and tile splits."""
+    scene, bounces = build_config(config, width=96, height=64, **kw)
+    rays = scene.camera.recalculate_ray_directions()
+    acc_o, out_o, n_o = oracle_frames(oracle_lib, scene, bounces, 4, rays)
+    acc = np.zeros_like(acc_o)
+    out = np.zeros_like(out_o)
+    n = 0
+    streamed = 0
+    for rank in range(world):
+        with Renderer(scene, camera_rays=rays, frame_batch=batch, rank=rank, world_size=world) as r:
+            r.set_brute_force(True)
+            for _ in range(4):
+                r.compute_frame(bounces)
+            a, o, k = r.read_accumulation(), r.read_output(), r.ray_count()
+            streamed += r.streamed_bytes()
+        mask = owned_mask(96, 64, rank, world)
+        acc[mask] = a[mask]
+        out[mask] = o[mask]
+        n += k
+    assert_same(acc, out, n, acc_o, out_o, n_o)
+    assert (streamed > 0) == bool(scene.objects)
+
+
 def _pcg_f32(seed):
     state = (seed * 747796405 + 2891336453) & 0xFFFFFFFF
     word = (((state >> ((state >> 28) + 4)) ^ state) * 277803737) & 0xFFFFFFFF

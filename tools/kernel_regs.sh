@@ -8,4 +8,4 @@ cd "$(dirname "$0")/.." || exit 1
   -Rpass-analysis=kernel-resource-usage rust_gpu_raytracing_amd/csrc/pathtrace.hip 2>&1 |
   grep -E "Function Name|VGPRs:|SGPRs Spill|VGPRs Spill|Occupancy" |
   sed -E 's/.*remark: //' | paste - - - - - | grep pathtrace_kernel |
-  sed -E 's/Function Name: _Z19rt_pathtrace_kernelIL(i[0-9])ELj([0-9]+)ELb([01])EEv10KernelArgs/mode \1 threads \2 tris \3/'
+  sed -E "s/Function Name: _Z19rt_pathtrace_kernelIL(i[0-9])ELj([0-9]+)ELb([01])ELb([01])EEv10KernelArgs/mode \1 threads \2 tris \3 wide \4/"
