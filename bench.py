@@ -149,7 +149,7 @@ def default_frame_batch(world: int, steps: int) -> int:
     64 steps two of 32. A persistent launch pays one fill and one drain (about one
     path at full iteration cost) whatever its size, and a tile split
     over N GPUs needs N x the frames per launch for the same units per GPU. Measured
-    at 20 steps, per frame (profiles/r02_s3/r02_s3n, r02_s3o): C2 8 -> 20 frames
+    at 20 steps, per frame (profiles/archive/r02_s3/r02_s3n, r02_s3o): C2 8 -> 20 frames
     0.337 -> 0.329 ms, C3 0.333 -> 0.290, C5 17.5 -> 15.5; 64 steps, C2 batches of
     8 -> 32: 0.318 -> 0.310."""
     cap = min(64, 32 * world)
@@ -258,7 +258,7 @@ def main() -> int:
         # Clock settle: the GPU's power management raises its clocks only after tens of
         # ms of sustained load (a 20-frame C2 launch: 6.2 ms right after a 5-frame
         # warmup, 5.75 ms from the fourth launch on, 6.2 ms again after a 100 ms idle
-        # gap; DESIGN.md §6, profiles/r02_s4d). A display loop renders continuously, so
+        # gap; DESIGN.md §6, profiles/archive/r02_s4d). A display loop renders continuously, so
         # the steady rate is the one to time: after the W warmup steps, more untimed
         # frames until --settle-ms of wall time have passed (on every rank alike).
         settle_frames = 0

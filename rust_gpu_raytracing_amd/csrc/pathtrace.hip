@@ -826,6 +826,36 @@ __device__ __forceinline__ uint32_t pack_rgba8(float r, float g, float b, float 
 
 }  // namespace
 
+// Trace result of a path's first segment, from rt_primary_kernel (below).
+struct PrimaryRecord {  // 16 B: {t, id, object | front << 31 | kind << 30, original sphere index}
+    float t;
+    uint32_t id;     // triangle index, or sphere slot
+    uint32_t meta;   // bit 30: sphere; bit 31: front face (triangle); bits 0-29: object
+    uint32_t orig;   // sphere: original index
+};
+
+template <bool kTris>
+__device__ __forceinline__ PrimaryRecord primary_record(const TraceState& ts) {
+    // the winner exactly as trace_end picks it: the triangle unless the sphere is strictly closer
+    const float tt = kTris ? ts.tri.t : kF32Max;
+    if (ts.sph.t < (tt != kF32Max ? tt : kF32Max))
+        return PrimaryRecord{ts.sph.t, ts.sph.slot, 1u << 30, ts.sph.orig};
+    return PrimaryRecord{tt, ts.tri.tri, (ts.tri.obj & 0x3fffffffu) | (ts.tri.front ? 0x80000000u : 0u), 0u};
+}
+
+// The TraceState trace_end rebuilds the same hit from.
+__device__ __forceinline__ void primary_state(const PrimaryRecord& r, TraceState& ts) {
+    ts.sph = SphereHit{kF32Max, 0u, 0u};
+    ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
+    if (r.meta & (1u << 30)) {
+        ts.sph = SphereHit{r.t, r.orig, r.id};
+    } else {
+        ts.tri = TriHit{r.t, 0u, r.id, r.meta & 0x3fffffffu, (r.meta & 0x80000000u) != 0u};
+    }
+}
+
+constexpr uint32_t kPrimaryThreads = 1024;  // 16 units per workgroup, sharing one LDS image of the scene
+
 // The tile queue, striped over the XCDs. One device-scope atomic counter on a
 // single address serialises at the memory side (~15 ns per claim measured:
 // that alone capped C1 at 4x below a static schedule). Local tile t belongs to
@@ -1154,6 +1184,16 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // (advanced per frame by the host only when accumulating, src/renderer.rs:216-235)
     // plus the sample number.
     auto random_index = [&]() { return ka.accumulation_index + (accumulate ? frame : 0u) + sample; };
+    // A sample just started: with the primary pre-pass (rt_primary_kernel) its first
+    // segment's trace result is read back and the lane goes straight to shading it;
+    // else the trace starts at the next setup step.
+    auto primary_start = [&]() -> uint32_t {
+        if (!ka.primary || p.bounce >= ka.bounces) return kSetup;
+        const uint4 r = ka.primary[(size_t)(frame * samples + sample) * ((size_t)ka.owned_tiles * 64u) +
+                                   (size_t)lane_tile * 64u + lane_slot];
+        primary_state(PrimaryRecord{__uint_as_float(r.x), r.y, r.z, r.w}, ts);
+        return kDone;
+    };
 
     // A finished sample: pixel_color += per_pixel(...) (:161); then the pixel's
     // next sample (random_index += 1, :162), its next frame (a multi-frame
@@ -1191,7 +1231,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             if (sample < samples) {
                 start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, index % ka.width, index / ka.width),
                              p);
-                mode = kSetup;
+                mode = primary_start();
             } else {
                 mode = kIdle;
             }
@@ -1213,7 +1253,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         }
         if (sample < samples) {
             start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, index % ka.width, index / ka.width), p);
-            mode = kSetup;
+            mode = primary_start();
         } else {
             store_frame();
             mode = kIdle;
@@ -1284,6 +1324,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                         mode = kSetup;
                         if (accumulate && !frame_par) pix = ka.accum[index];  // :156
                         start_sample(ka, index, random_index(), pixel_ray(ka, l_cam, index, x, y), p);
+                        mode = primary_start();
                     }
                 }
             }
@@ -1660,6 +1701,144 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
     }
 }
 
+// ---- coherent primary rays: a packet pre-pass -----------------------------------
+//
+// The first segment of every path starts at the camera, and the 64 primary rays
+// of an 8x8 tile (one wave here) differ only by the pixel step and the reference's
+// +-0.0005 jitter (compute_shader.wgsl:212-222): they reach nearly the same nodes
+// and leaves. The path kernel's walk is per lane and asynchronous, so each lane
+// loads its own copy of every node, sub-object and triangle record (C5: ~1,750 L1
+// accesses per ray, the TCP's tag lookups being the binding unit). rt_primary_kernel
+// instead walks each unit's rays as one packet: the node index is wave-uniform,
+// a node is entered when any lane's ray enters it (each lane still applies its own
+// culling test and its own exact leaf tests, so every lane gets exactly its own
+// result: the lexicographic minimum over a superset of its own candidate set),
+// and the node, sub-object and triangle records are read at wave-uniform
+// addresses -- one scalar load or LDS broadcast for the whole wave. It writes
+// each (frame, sample, pixel)'s trace result (the winner of trace_ray, :342-353:
+// sphere or triangle, distance, index, object, facing) as one 16-B record; the
+// path kernel starts those paths from the record instead of tracing their first
+// segment. Everything after the first segment is unchanged.
+template <int kMode, bool kTris>
+__global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x;
+    float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
+    float* l_cam = l_srgb + 256;
+    SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
+                 ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
+                 nullptr,         nullptr,        0u};
+    if constexpr (kMode >= 1) {  // what the walks read (the path kernel's mode 1 / 2 image)
+        float4* l_sph = reinterpret_cast<float4*>(lds);
+        RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
+        uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
+        float4* l_nodes = reinterpret_cast<float4*>(lds + ka.lds_nodes_offset);
+        for (uint32_t i = tid; i < ka.sphere_slot_count; i += kPrimaryThreads) {
+            l_sph[i] = ka.sphere_slots[i];
+            l_orig[i] = ka.sphere_orig[i];
+        }
+        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kPrimaryThreads) l_nodes[i] = ka.sphere_bvh[i];
+        if constexpr (kTris)
+            for (uint32_t i = tid; i < ka.object_count; i += kPrimaryThreads) l_obj[i] = ka.objects[i];
+        sv.sph = l_sph;
+        sv.orig = l_orig;
+        sv.nodes = l_nodes;
+        sv.obj = l_obj;
+    }
+    if constexpr (kMode == 2) {
+        float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
+        uint4* l_tp = reinterpret_cast<uint4*>(lds + ka.lds_tri_prims_offset);
+        for (uint32_t i = tid; i < 2u * ka.tri_nodes; i += kPrimaryThreads) l_tn[i] = ka.tri_bvh[i];
+        for (uint32_t i = tid; i < ka.tri_prim_count; i += kPrimaryThreads) l_tp[i] = ka.tri_prims[i];
+        sv.tri_nodes = l_tn;
+        sv.tri_prims = l_tp;
+    }
+    if (tid < 16u) {
+        l_cam[tid] = ka.inv_proj[tid];
+        l_cam[16u + tid] = ka.inv_view[tid];
+    }
+    if (tid == 0) l_cam[32] = ka.aspect;
+    __syncthreads();
+
+    // one wave per (frame, local tile) unit, frame-major
+    const uint32_t unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (kPrimaryThreads / 64u) + (tid >> 6));
+    if (unit >= ka.queue_units) return;  // the whole wave
+    const uint32_t frame = unit / ka.owned_tiles, local_tile = unit - frame * ka.owned_tiles;
+    const uint32_t slot = tid & 63u;
+    const uint32_t gt = local_tile * ka.world_size + ka.rank;
+    const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);
+    const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
+    const bool valid = x < ka.width && y < ka.height;
+    const uint32_t index = valid ? y * ka.width + x : 0u;
+    const bool accumulate = ka.accumulate == 1u;
+    const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;
+    const size_t owned_px = (size_t)ka.owned_tiles * 64u;
+    const f3 cam = pixel_ray(ka, l_cam, index, x, y);
+    for (uint32_t sample = 0; sample < samples; ++sample) {
+        Path p;
+        start_sample(ka, index, ka.accumulation_index + (accumulate ? frame : 0u) + sample, cam, p);
+        const f3 o = p.o, d = p.d;
+        TraceState ts;
+        trace_begin<kTris>(sv, ka, o, d, ts);  // brute-force spheres, slab constants, phase
+        if constexpr (kTris) {
+            if (ts.phase == 0) {
+                // the triangle accelerator as a packet: wave-uniform node, per-lane culling
+                uint32_t node = 0;
+                while (node < ka.tri_nodes) {
+                    const float4 lo = sv.tri_nodes[2u * node], hi = sv.tri_nodes[2u * node + 1u];
+                    float near_t, far_t;
+                    slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+                    const bool hit = valid && near_t <= far_t && far_t >= 0.0f;
+                    const bool any = __ballot(hit) != 0;
+                    const uint32_t leaf = __float_as_uint(hi.w);
+                    if (any && leaf != 0xffffffffu && hit) tri_leaf(sv, ka, o, d, ts, leaf & 0xffffffu);
+                    node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
+                }
+                if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
+                ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
+                ts.node = 0;
+                if (ts.phase == 1) phase_setup<kTris>(sv, ka, o, ts.a2 * 0.5f, 1, ts);
+            }
+        }
+        if (ts.phase == 1) {
+            // the sphere BVH as a packet over layout 0 (a complete walk whatever the octant,
+            // boxes stored as min/max there): per-lane culling and pruning
+            const uint32_t n0 = ka.sphere_octant_stride ? ka.sphere_octant_stride : ka.sphere_nodes;
+            SlabRay sr = slab_ray(o.x, o.y, o.z, ts.inv.x, ts.inv.y, ts.inv.z, 0.0f);
+            {
+                // the lane's own margin (phase_setup's), without the octant pairing
+                const float r = sqrt_up(dot(o, o));
+                float m, slack;
+                sphere_cull_bounds(r, ka.sphere_extent, ka.sphere_rmin, ka.sphere_rmax,
+                                   __builtin_amdgcn_rsqf(ts.a2 * 0.5f), m, slack);
+                sr = slab_ray(o.x, o.y, o.z, ts.inv.x, ts.inv.y, ts.inv.z, m);
+                ts.slack = slack;
+                ts.limit = prune_limit(ts);
+            }
+            uint32_t node = 0;
+            while (node < n0) {
+                const float4 lo = sv.nodes[2u * node], hi = sv.nodes[2u * node + 1u];
+                float near_t, far_t;
+                slab_hit(sr, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+                const bool hit = valid && near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
+                const bool any = __ballot(hit) != 0;
+                const uint32_t leaf = __float_as_uint(hi.w);
+                if (any && leaf != 0xffffffffu && hit) {
+                    test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
+                    ts.limit = prune_limit(ts);
+                }
+                node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
+            }
+        }
+        if (valid)
+            reinterpret_cast<uint4*>(ka.primary)[(size_t)(frame * samples + sample) * owned_px +
+                                                 (size_t)local_tile * 64u + slot] = [&] {
+                const PrimaryRecord r = primary_record<kTris>(ts);
+                return make_uint4(__float_as_uint(r.t), r.id, r.meta, r.orig);
+            }();
+    }
+}
+
 namespace {
 // Dynamic LDS above 64 KiB must be opted into per kernel.
 hipError_t allow_big_lds(const void* fn) {
@@ -1687,10 +1866,12 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool w
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream) {
     const uint32_t blocks = (ka.owned_tiles + kBruteThreads / 64u - 1u) / (kBruteThreads / 64u);
     if (blocks == 0) return hipSuccess;
-    const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_kernel<true>)
-                          : reinterpret_cast<const void*>(&rt_brute_kernel<false>);
-    hipError_t e = allow_big_lds(fn);
-    if (e != hipSuccess) return e;
+    if (lds_bytes > 64u * 1024u) {  // dynamic LDS above 64 KiB must be opted into
+        const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_kernel<true>)
+                              : reinterpret_cast<const void*>(&rt_brute_kernel<false>);
+        hipError_t e = allow_big_lds(fn);
+        if (e != hipSuccess) return e;
+    }
     if (tris)
         hipLaunchKernelGGL(rt_brute_kernel<true>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
     else
@@ -1699,6 +1880,24 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 }
 
 size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
+
+hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, hipStream_t stream) {
+    const uint32_t per = kPrimaryThreads / 64u;
+    const uint32_t blocks = (ka.queue_units + per - 1u) / per;
+    if (blocks == 0) return hipSuccess;
+#define RT_PRIMARY(M, TR)                                                                                      \
+    if (mode == M && tris == TR) {                                                                             \
+        if (lds_bytes > 64u * 1024u) {                                                                         \
+            hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_primary_kernel<M, TR>));           \
+            if (e != hipSuccess) return e;                                                                     \
+        }                                                                                                      \
+        hipLaunchKernelGGL((rt_primary_kernel<M, TR>), dim3(blocks), dim3(kPrimaryThreads), lds_bytes, stream, ka); \
+        return hipGetLastError();                                                                              \
+    }
+    RT_PRIMARY(1, true) RT_PRIMARY(2, true) RT_PRIMARY(1, false)
+#undef RT_PRIMARY
+    return hipErrorInvalidValue;
+}
 
 // Picks the workgroup size for this LDS mode and footprint: the most resident
 // waves per CU up to kTargetWavesPerCu (measured on C2: 16 waves/CU beat 18

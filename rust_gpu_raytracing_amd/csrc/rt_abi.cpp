@@ -44,6 +44,7 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
+hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, hipStream_t stream);
 size_t rt_brute_tile_bytes();
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
@@ -101,7 +102,7 @@ uint32_t trav_threshold_for(int lds_mode, bool tris) {
 // Triangle scenes test deferred leaves once this many eighths of the
 // traversing lanes hold one (pathtrace.hip, leaf_step): later for an LDS
 // accelerator, earlier when the leaf's loads go to global memory anyway.
-// Re-measured with 20-frame launches (profiles/r02_s4/r02_s4k, r02_s4l):
+// Re-measured with 20-frame launches (profiles/archive/r02_s4/r02_s4k, r02_s4l):
 // mode 2 at 6 (C4 -2.3% against 7, C3 within 0.3%), modes 0/1 at 5 (C5 -2.9%
 // against 6; 4 and 3 within 0.4% of 5).
 uint32_t leaf_batch_for(int lds_mode) { return lds_mode == 2 ? 6 : 5; }
@@ -164,7 +165,7 @@ struct rt_ctx {
     bool batch_overlap = true;        // RT_BATCH_OVERLAP=0: every batch on the primary stream (A/B switch)
     bool batch_schedule = false;      // RT_BATCH_SCHEDULE=1: cost-ordered claims in batches too (A/B switch)
     // a tile's frames claimed one after another (C3 -12%, C4 -8%, C5 -4%, C2 -1.8% per frame
-    // against frame-major, profiles/r02_knobs2); RT_UNIT_TILE_MAJOR=0: frame-major (A/B switch)
+    // against frame-major, profiles/archive/r02_knobs2); RT_UNIT_TILE_MAJOR=0: frame-major (A/B switch)
     bool unit_tile_major = true;
 
     uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
@@ -225,8 +226,9 @@ struct rt_ctx {
     bool tri_dirty = true;
     uint32_t tri_count_built = 0xffffffffu;
     bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
-    // the 4-wide accelerator (tri_wide.h), the default (RT_TRI_WIDE=0: the binary one, A/B switch)
-    bool use_tri_wide = true;
+    // the 4-wide accelerator (tri_wide.h), RT_TRI_WIDE=1 (A/B switch): measured slower than the
+    // binary one on C3-C5, so off by default
+    bool use_tri_wide = false;
     int tri_compact = -1;        // RT_TRI_COMPACT: 1 / 0 force compact leaves on / off; -1 by size
     bool wide_built = false;     // the accelerator on the device is the wide one
     bool wide_refresh = false;   // triangles uploaded since the compact blocks were checked
@@ -238,6 +240,10 @@ struct rt_ctx {
     uint32_t wide_leaves = 0, wide_verts = 0, wide_depth = 0, wide_compact_leaves = 0;
     // rt_set_brute_force: the reference's own sweeps, LDS-tiled (rt_brute_kernel; BASELINE config 5)
     bool brute = false;
+    // coherent primary rays (rt_primary_kernel): RT_PRIMARY_PASS 1 / 0 force on / off, -1 by scene
+    int primary_pass = -1;
+    uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
+    size_t primary_cap = 0;
     unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
     uint32_t tri_nodes = 0, tri_prim_count = 0;
     float* d_tri_extent = nullptr;   // margin extent, in device memory (refit updates it)
@@ -703,7 +709,9 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         env = std::getenv("RT_TRI_BVH");
         ctx->use_tri_bvh = !(env && env[0] == '0');
         env = std::getenv("RT_TRI_WIDE");
-        ctx->use_tri_wide = !(env && env[0] == '0');
+        if (env) ctx->use_tri_wide = env[0] == '1';
+        env = std::getenv("RT_PRIMARY_PASS");
+        if (env) ctx->primary_pass = env[0] == '0' ? 0 : 1;
         env = std::getenv("RT_BRUTE_FORCE");
         ctx->brute = env && env[0] == '1';
         env = std::getenv("RT_TRI_COMPACT");
@@ -806,7 +814,8 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
-                    ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream};
+                    ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
+                    ctx->d_primary[0], ctx->d_primary[1]};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1278,7 +1287,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // Frame-parallel batches claim in index order: with the drain paid once per batch
     // (and overlapped) the cost order's recording and sort cost more than they save,
     // and index order keeps neighbouring tiles together (C2 -5.2%, C3 -2.7% per frame
-    // measured, profiles/r02_knobs); RT_BATCH_SCHEDULE=1 sorts them too (A/B switch).
+    // measured, profiles/archive/r02_knobs); RT_BATCH_SCHEDULE=1 sorts them too (A/B switch).
     const bool sched = ctx->tile_schedule && (!frame_par || ctx->batch_schedule) &&
                        (uint64_t)ka.queue_units >= kSchedMinTilesPerWave * blocks * waves_per_block;
     // Overlapped batches: frame-parallel batches alternate between
@@ -1337,6 +1346,34 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.launch_clock = ctx->d_clock + kClockWords * (size_t)slot;
         RT_HIP(ctx, hipMemsetAsync(ka.launch_clock, 0, kClockWords * 8, S));
         ctx->clock_pending.push_back(slot);
+    }
+    // Coherent primary rays: the first segment of every (frame, sample, pixel) of the launch
+    // traced by rt_primary_kernel as 8x8 packets, stream-ordered before the path kernel
+    // (scene image in LDS, binary triangle accelerator; by default for triangle scenes)
+    const bool primary = bounces > 0 && mode >= 1 && !wide && ka.compute_per_frame > 0 &&
+                         (ctx->primary_pass == 1 || (ctx->primary_pass == -1 && tris));
+    ka.primary = nullptr;
+    if (primary) {
+        const int pi = (int)(ctx->batches & 1u);
+        const size_t need = (size_t)owned_px * frames * std::max<uint32_t>(1u, p.accumulate == 1u ? p.compute_per_frame : 1u);
+        if (need > ctx->primary_cap) {
+            RT_HIP(ctx, join_aux(ctx));
+            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            const size_t want = std::max<size_t>(need, (size_t)owned_px * ctx->frame_batch);
+            for (uint4*& b : ctx->d_primary) {
+                if (b) RT_HIP(ctx, hipFree(b));
+                b = nullptr;
+            }
+            ctx->primary_cap = 0;
+            for (uint4*& b : ctx->d_primary) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&b), want * 16));
+            ctx->primary_cap = want;
+        }
+        KernelArgs pka = ka;
+        pka.primary = ctx->d_primary[pi];
+        pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile), frame-major
+        const size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
+        RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, S));
+        ka.primary = pka.primary;
     }
     hipError_t e = rt_launch_pathtrace(ka, mode, tris, wide, ctx->occ_threads, lds_bytes, blocks, S);
     ctx->last_blocks = blocks;

@@ -170,6 +170,9 @@ struct KernelArgs {
     // launch timing (rt_set_timing), null otherwise: {~earliest workgroup start, latest
     // workgroup end} on the device wall clock
     unsigned long long* __restrict__ launch_clock;
+    // coherent primary rays (rt_primary_kernel): one 16-B trace result per (frame, sample, owned
+    // pixel), indexed like frame_light; the path kernel starts its paths from them. Null: off.
+    uint4* __restrict__ primary;
     // brute-force launches (rt_brute_kernel): bytes of sub-object records streamed through LDS
     unsigned long long* __restrict__ stream_bytes;
     uint32_t texture_width;

@@ -661,6 +661,49 @@ def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
     assert np.array_equal(got_bad[0].view(np.uint32), acc_b.view(np.uint32))
 
 
+@pytest.mark.parametrize("config,kw,spp,accumulate,batch,world,env", [
+    ("c2_rtiow", {}, 1, 1, 4, 1, {"RT_PRIMARY_PASS": "1"}),          # forced on a sphere scene
+    ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {}),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {}),           # non-accumulating batch
+    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 4, 3, {}),           # tile split
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 2, 1, {"RT_FRAME_PARALLEL": "0"}),
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 1, 1, {}),
+])
+def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumulate, batch, world, env):
+    """rt_primary_kernel traces every path's first segment as 8x8 packets (wave-uniform
+    node walk, per-lane culling and exact leaf tests); the path kernel starts from its
+    records. Results must equal the oracle's (and therefore the per-lane walk's) in
+    batches, with several samples, without accumulation and in tile splits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scene, bounces = build_config(config, width=96, height=64, **kw)
+    rays = scene.camera.recalculate_ray_directions()
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((64, 96, 4), np.float32)
+    out_o = np.zeros((64, 96), np.uint32)
+    n_o = 0
+    for k in range(1, 5):
+        n_o += o.render_frame(scene.params(accumulate=accumulate, compute_per_frame=spp,
+                                           accumulation_index=k if accumulate else 1), bounces, acc_o, out_o)
+    acc = np.zeros_like(acc_o)
+    out = np.zeros_like(out_o)
+    n = 0
+    for rank in range(world):
+        with Renderer(scene, camera_rays=rays, frame_batch=batch, rank=rank, world_size=world,
+                      compute_per_frame=spp, accumulate=bool(accumulate)) as r:
+            for _ in range(4):
+                r.compute_frame(bounces)
+            a, oo, k = r.read_accumulation(), r.read_output(), r.ray_count()
+        mask = owned_mask(96, 64, rank, world)
+        acc[mask] = a[mask]
+        out[mask] = oo[mask]
+        n += k
+    if accumulate:
+        assert_same(acc, out, n, acc_o, out_o, n_o)
+    else:
+        assert n == n_o and np.array_equal(out, out_o)
+
+
 @pytest.mark.parametrize("config,kw,batch,world", [
     ("c1_four_spheres", {}, 1, 1),
     ("c2_rtiow", {}, 3, 1),
