@@ -1866,11 +1866,11 @@ hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool w
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream) {
     const uint32_t blocks = (ka.owned_tiles + kBruteThreads / 64u - 1u) / (kBruteThreads / 64u);
     if (blocks == 0) return hipSuccess;
-    if (lds_bytes > 64u * 1024u) {  // dynamic LDS above 64 KiB must be opted into
+    if (lds_bytes > 64u * 1024u) {  // dynamic LDS above 64 KiB must be opted into (exactly what is used)
         const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_kernel<true>)
                               : reinterpret_cast<const void*>(&rt_brute_kernel<false>);
-        hipError_t e = allow_big_lds(fn);
-        if (e != hipSuccess) return e;
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        if (e != hipSuccess) return hipErrorInvalidConfiguration;  // (distinguishes the opt-in from the launch)
     }
     if (tris)
         hipLaunchKernelGGL(rt_brute_kernel<true>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);

@@ -19,6 +19,20 @@ for s in $STEPS; do
     all)   timeout -k 10 600 python3 tools/bench_all.py --no-cpu --frames 20 > "$OUT/bench_all.jsonl" 2> "$OUT/bench_all.err" ;;
     strong) timeout -k 10 300 python3 tools/strong_probe.py --steps 20 > "$OUT/strong_probe.jsonl" 2> "$OUT/strong_probe.err" ;;
     prof)  bash tools/profile.sh "$TAG" ;;  # then locally: python tools/update_traffic.py gpurun_out/prof_<tag> profiles/<tag>
+    srcbuild) # provenance: compile the library from source on this box (its own hipcc) into a
+           # scratch path and run the golden + smoke-size parity tests against that build
+           timeout -k 10 600 python3 -c "
+import subprocess, sys
+from rust_gpu_raytracing_amd import build as b
+out = '/tmp/librt_srcbuild.so'
+subprocess.run(b.hipcc_command(__import__('pathlib').Path(out)), check=True)
+print('built', out, 'hash', b.source_hash())" > "$OUT/srcbuild.log" 2>&1 &&
+           RT_LIB=/tmp/librt_srcbuild.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v \
+             --timeout 200 --timeout-method thread -k "golden or full_frame_baseline_size" >> "$OUT/srcbuild.log" 2>&1 &&
+           RT_LIB=/tmp/librt_srcbuild.so python3 -c "
+from rust_gpu_raytracing_amd import _native as N, build as b
+lib = N.load_library(); import socket
+print('srcbuild library hash', lib.rt_build_hash().decode(), '== tree', b.source_hash(), 'on', socket.gethostname())" >> "$OUT/srcbuild.log" 2>&1 ;;
     multi) # N-rank rehearsal on the one GPU of the box (gloo; the real run is RCCL, one GPU per rank)
            for n in 2 4 8; do
              RT_BENCH_ONE_DEVICE=1 RT_DIST_BACKEND=gloo RT_BENCH_VERIFY_GATHER=1 timeout -k 10 300 \
