@@ -1175,7 +1175,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;  // :158-175
 
     // Lane states. A lane owns one pixel at a time and one ray of its path.
-    constexpr uint32_t kIdle = 0, kSetup = 1, kTrav = 2, kDone = 3;
+    constexpr uint32_t kIdle = 0, kSetup = 1, kTrav = 2, kDone = 3, kPrimary = 4;
     uint32_t rays = 0;
     uint32_t lane_tile = 0;  // local tile of the lane's pixel (tile costs)
     uint32_t lane_slot = 0;  // the pixel's slot in its tile (frame-parallel light stores)
@@ -1203,12 +1203,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // A sample just started: with the primary pre-pass (rt_primary_kernel) its first
     // segment's trace result is read back and the lane goes straight to shading it;
     // else the trace starts at the next setup step.
+    // (The record is read at the next shading step, where it is used: kPrimary.)
     auto primary_start = [&]() -> uint32_t {
-        if (!ka.primary || p.bounce >= ka.bounces) return kSetup;
-        const uint4 r = ka.primary[(size_t)(frame * samples + sample) * ((size_t)ka.owned_tiles * 64u) +
-                                   (size_t)lane_tile * 64u + lane_slot];
-        primary_state(PrimaryRecord{__uint_as_float(r.x), r.y, r.z, r.w}, ts);
-        return kDone;
+        return (ka.primary && p.bounce < ka.bounces) ? kPrimary : kSetup;
     };
 
     // A finished sample: pixel_color += per_pixel(...) (:161); then the pixel's
@@ -1297,9 +1294,16 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         ++iters;
         const unsigned long long ts0 = stamp();
 #endif
-        // 1. Shade the lanes whose trace has finished (:228-311).
+        // 1. Shade the lanes whose trace has finished (:228-311); a sample started by
+        // the primary pre-pass has its first trace result in ka.primary.
         bool fin = false;      // a sample finished: its rays go to the tile's cost
         uint32_t fin_rays = 0;
+        if (mode == kPrimary) {
+            const uint4 r = ka.primary[(size_t)(frame * samples + sample) * ((size_t)ka.owned_tiles * 64u) +
+                                       (size_t)lane_tile * 64u + lane_slot];
+            primary_state(PrimaryRecord{__uint_as_float(r.x), r.y, r.z, r.w}, ts);
+            mode = kDone;
+        }
         if (mode == kDone) {
             const Hit h = trace_end<kTris>(sv, ka, p.o, p.d, ts);
             ++rays;
