@@ -186,7 +186,7 @@ __device__ __forceinline__ TriFront tri_front(const RtTriangleHot* __restrict__ 
     f.dist = dot(f.ao, f.cn) * f.inv_det;
     return f;
 }
-// The barycentric half: true when v, u and w = 1 - u - v are all >= 0 (:459-481).
+// The barycentric half: true unless v, u or w = 1 - u - v is < 0 (:459-481; NaN passes).
 __device__ __forceinline__ bool tri_back(const RtTriangleHot* __restrict__ t, uint32_t i, const TriFront& f, f3 d) {
     const float4 p2 = t[i].p2;
     const f3 ab = mk(f.ab_x, f.ab_y, p2.x), ac = mk(p2.y, p2.z, p2.w);
@@ -196,7 +196,7 @@ __device__ __forceinline__ bool tri_back(const RtTriangleHot* __restrict__ t, ui
     const float u = dot(ac, dao) * f.inv_det;
     if (u < 0.0f) return false;
     const float w = 1.0f - u - v;
-    return w >= 0.0f;
+    return !(w < 0.0f);  // not `w >= 0`: a NaN w passes, as the reference's `continue` lets it (:479)
 }
 
 // check_triangles, compute_shader.wgsl:422-517: the reference's own sweep over

@@ -663,11 +663,12 @@ def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
 
 @pytest.mark.parametrize("config,kw,spp,accumulate,batch,world,env", [
     ("c2_rtiow", {}, 1, 1, 4, 1, {"RT_PRIMARY_PASS": "1"}),          # forced on a sphere scene
-    ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {}),
-    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {}),           # non-accumulating batch
-    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 4, 3, {}),           # tile split
-    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 2, 1, {"RT_FRAME_PARALLEL": "0"}),
-    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 1, 1, {}),
+    ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {"RT_PRIMARY_PASS": "1"}),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {"RT_PRIMARY_PASS": "1"}),  # non-accumulating batch
+    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 4, 3, {"RT_PRIMARY_PASS": "1"}),  # tile split
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 2, 1, {"RT_FRAME_PARALLEL": "0", "RT_PRIMARY_PASS": "1"}),
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 1, 1, {"RT_PRIMARY_PASS": "1", "RT_LDS_MODE": "1"}),
+    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 2, 1, {}),       # default: on (accelerator in global memory)
 ])
 def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumulate, batch, world, env):
     """rt_primary_kernel traces every path's first segment as 8x8 packets (wave-uniform
@@ -744,11 +745,15 @@ def _pcg_f32(seed):
     return seed, np.float32(seed) / np.float32(4294967296.0)
 
 
-def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib):
+@pytest.mark.parametrize("primary", ["0", "1"])
+def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib, monkeypatch, primary):
     """Rays lying exactly in a triangle's plane (det == 0, origin on the plane) give a NaN
     distance that the reference's sweep accepts (:449-481, :457); the accelerator hands such
     lanes to the sweep itself. Primary directions are chosen so that d.y + jitter.y == 0
-    exactly (the jitter is the kernel's own PCG draw, :217-219)."""
+    exactly (the jitter is the kernel's own PCG draw, :217-219). Such a hit has NaN
+    barycentrics too, which pass the reference's `< 0` rejections (:467-481). With and
+    without the primary pre-pass."""
+    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
     from rust_gpu_raytracing_amd.camera import Camera
     from rust_gpu_raytracing_amd.scene import SceneObject
 
