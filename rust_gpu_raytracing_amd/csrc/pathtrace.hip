@@ -161,42 +161,7 @@ struct TriGeom {
 };
 __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t, uint32_t i) {
     const float4 p0 = t[i].p0, p1 = t[i].p1, p2 = t[i].p2;
-    return TriGeom{mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w), mk(p0.x, p0.y, p0.z)};
-}
-
-// One triangle test of the reference's sweep (check_triangles, :445-500) in two
-// halves, as the record is laid out (rt_kernel_args.h): the determinant and the
-// distance from calc_normal and a (p0, p1), then -- only for a candidate whose
-// distance the caller accepts -- edge_ab and edge_ac (p2) for the barycentric
-// tests. The arithmetic and its order are the reference's.
-struct TriFront {
-    f3 cn, ao;
-    float ab_x, ab_y;
-    float det, inv_det, dist;
-};
-__device__ __forceinline__ TriFront tri_front(const RtTriangleHot* __restrict__ t, uint32_t i, f3 o, f3 d) {
-    const float4 p0 = t[i].p0, p1 = t[i].p1;
-    TriFront f;
-    f.cn = mk(p0.x, p0.y, p0.z);
-    f.ao = o - mk(p0.w, p1.x, p1.y);
-    f.ab_x = p1.z;
-    f.ab_y = p1.w;
-    f.det = -dot(d, f.cn);
-    f.inv_det = 1.0f / f.det;
-    f.dist = dot(f.ao, f.cn) * f.inv_det;
-    return f;
-}
-// The barycentric half: true unless v, u or w = 1 - u - v is < 0 (:459-481; NaN passes).
-__device__ __forceinline__ bool tri_back(const RtTriangleHot* __restrict__ t, uint32_t i, const TriFront& f, f3 d) {
-    const float4 p2 = t[i].p2;
-    const f3 ab = mk(f.ab_x, f.ab_y, p2.x), ac = mk(p2.y, p2.z, p2.w);
-    const f3 dao = cross(f.ao, d);
-    const float v = -dot(ab, dao) * f.inv_det;
-    if (v < 0.0f) return false;
-    const float u = dot(ac, dao) * f.inv_det;
-    if (u < 0.0f) return false;
-    const float w = 1.0f - u - v;
-    return !(w < 0.0f);  // not `w >= 0`: a NaN w passes, as the reference's `continue` lets it (:479)
+    return TriGeom{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w)};
 }
 
 // check_triangles, compute_shader.wgsl:422-517: the reference's own sweep over
@@ -219,14 +184,24 @@ __device__ __forceinline__ TriHit sweep_triangles(const SceneView& sv, const Ker
             if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
             for (uint32_t j = 0; j < sub.triangle_count; ++j) {
                 const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
-                const TriFront f = tri_front(ka.triangles, ti, o, d);
-                if (f.dist < 0.0f || f.dist >= closest) continue;
-                if (!tri_back(ka.triangles, ti, f, d)) continue;
-                closest = f.dist;
-                th.t = f.dist;
+                const TriGeom g = load_tri(ka.triangles, ti);
+                const float det = -dot(d, g.cn);
+                const float inv_det = 1.0f / det;
+                const f3 ao = o - g.a;
+                const float dist = dot(ao, g.cn) * inv_det;
+                if (dist < 0.0f || dist >= closest) continue;
+                const f3 dao = cross(ao, d);
+                const float v = -dot(g.ab, dao) * inv_det;
+                if (v < 0.0f) continue;
+                const float u = dot(g.ac, dao) * inv_det;
+                if (u < 0.0f) continue;
+                const float w = 1.0f - u - v;
+                if (w < 0.0f) continue;
+                closest = dist;
+                th.t = dist;
                 th.tri = ti;
                 th.obj = oi;
-                th.front = f.det > 0.0f;
+                th.front = det > 0.0f;
             }
         }
     }
@@ -359,17 +334,26 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     for (uint32_t j = 0; j < sub.triangle_count; ++j) {
         const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
         const uint32_t seq = pr.z + j;
-        const TriFront f = tri_front(ka.triangles, ti, o, d);
-        const float dist = f.dist;
+        const TriGeom g = load_tri(ka.triangles, ti);
+        const float det = -dot(d, g.cn);
+        const float inv_det = 1.0f / det;
+        const f3 ao = o - g.a;
+        const float dist = dot(ao, g.cn) * inv_det;
         const bool nan_dist = dist != dist;
         if (dist < 0.0f) continue;
         if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) continue;
-        if (!tri_back(ka.triangles, ti, f, d)) continue;
+        const f3 dao = cross(ao, d);
+        const float v = -dot(g.ab, dao) * inv_det;
+        if (v < 0.0f) continue;
+        const float u = dot(g.ac, dao) * inv_det;
+        if (u < 0.0f) continue;
+        const float w = 1.0f - u - v;
+        if (w < 0.0f) continue;
         if (nan_dist) {
             ts.nan_hit = true;
             continue;
         }
-        ts.tri = TriHit{dist, seq, ti, pr.x, f.det > 0.0f};
+        ts.tri = TriHit{dist, seq, ti, pr.x, det > 0.0f};
     }
 }
 
@@ -1658,11 +1642,21 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
                                 if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
                                 for (uint32_t j = 0; j < sub.triangle_count; ++j) {
                                     const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
-                                    const TriFront f = tri_front(ka.triangles, ti, o, d);
-                                    if (f.dist < 0.0f || f.dist >= closest) continue;
-                                    if (!tri_back(ka.triangles, ti, f, d)) continue;
-                                    closest = f.dist;
-                                    ts.tri = TriHit{f.dist, 0u, ti, oi, f.det > 0.0f};
+                                    const TriGeom g = load_tri(ka.triangles, ti);
+                                    const float det = -dot(d, g.cn);
+                                    const float inv_det = 1.0f / det;
+                                    const f3 ao = o - g.a;
+                                    const float dist = dot(ao, g.cn) * inv_det;
+                                    if (dist < 0.0f || dist >= closest) continue;
+                                    const f3 dao = cross(ao, d);
+                                    const float v = -dot(g.ab, dao) * inv_det;
+                                    if (v < 0.0f) continue;
+                                    const float u = dot(g.ac, dao) * inv_det;
+                                    if (u < 0.0f) continue;
+                                    const float w = 1.0f - u - v;
+                                    if (w < 0.0f) continue;
+                                    closest = dist;
+                                    ts.tri = TriHit{dist, 0u, ti, oi, det > 0.0f};
                                 }
                             }
                         }

@@ -45,37 +45,33 @@ struct RtSubObject {  // src/buffers.rs:124-129, 32 B
     uint32_t triangle_count;
 };
 
-// The SceneTriangle fields the kernel reads (src/buffers.rs:49-64), 64 B, in the
-// order the intersection test consumes them: calc_normal and a first (the
-// determinant and the distance, :445-457, which reject most candidates), then
-// edge_ab and edge_ac (the barycentric tests, :459-481), face_normal (read only
-// for the closest hit) last. The test loads p0 and p1, and p2 only for a
-// candidate whose distance passed: a rejected candidate costs two 16-B L1
-// accesses instead of three (the L1 tag lookups bind triangle-heavy scenes,
-// DESIGN.md §5.3a). A record never straddles a 128-B line.
+// The SceneTriangle fields the kernel reads (src/buffers.rs:49-64), 64 B: the
+// four vectors of the intersection test packed into the first 48 B (three
+// 16-B loads), face_normal (read only for the closest hit) last. A record never
+// straddles a 128-B line, and a sub-object's 7 triangles span 448 B.
 struct RtTriangleHot {
-    float4 p0;  // calc_normal.x calc_normal.y calc_normal.z a.x
-    float4 p1;  // a.y a.z edge_ab.x edge_ab.y
-    float4 p2;  // edge_ab.z edge_ac.x edge_ac.y edge_ac.z
+    float4 p0;  // a.x a.y a.z edge_ab.x
+    float4 p1;  // edge_ab.y edge_ab.z edge_ac.x edge_ac.y
+    float4 p2;  // edge_ac.z calc_normal.x calc_normal.y calc_normal.z
     float4 fn;  // face_normal.x face_normal.y face_normal.z 0
 };
 
 __host__ __device__ inline RtTriangleHot pack_triangle(const float* a, const float* ab, const float* ac,
                                                        const float* cn, const float* fn) {
     RtTriangleHot h;
-    h.p0 = make_float4(cn[0], cn[1], cn[2], a[0]);
-    h.p1 = make_float4(a[1], a[2], ab[0], ab[1]);
-    h.p2 = make_float4(ab[2], ac[0], ac[1], ac[2]);
+    h.p0 = make_float4(a[0], a[1], a[2], ab[0]);
+    h.p1 = make_float4(ab[1], ab[2], ac[0], ac[1]);
+    h.p2 = make_float4(ac[2], cn[0], cn[1], cn[2]);
     h.fn = make_float4(fn[0], fn[1], fn[2], 0.f);
     return h;
 }
 
 __host__ __device__ inline void unpack_triangle(const RtTriangleHot& h, float* a, float* ab, float* ac, float* cn,
                                                 float* fn) {
-    cn[0] = h.p0.x, cn[1] = h.p0.y, cn[2] = h.p0.z;
-    a[0] = h.p0.w, a[1] = h.p1.x, a[2] = h.p1.y;
-    ab[0] = h.p1.z, ab[1] = h.p1.w, ab[2] = h.p2.x;
-    ac[0] = h.p2.y, ac[1] = h.p2.z, ac[2] = h.p2.w;
+    a[0] = h.p0.x, a[1] = h.p0.y, a[2] = h.p0.z;
+    ab[0] = h.p0.w, ab[1] = h.p1.x, ab[2] = h.p1.y;
+    ac[0] = h.p1.z, ac[1] = h.p1.w, ac[2] = h.p2.x;
+    cn[0] = h.p2.y, cn[1] = h.p2.z, cn[2] = h.p2.w;
     fn[0] = h.fn.x, fn[1] = h.fn.y, fn[2] = h.fn.z;
 }
 

@@ -199,11 +199,10 @@ extern "C" __global__ void __launch_bounds__(kRefitThreads) rt_refit_tri_bvh_ker
 // device edit, exact without a host rebuild.
 
 __device__ __forceinline__ TriVertex hot_corner(const RtTriangleHot& t, uint32_t k) {
-    float a[3], ab[3], ac[3], cn[3], fn[3];
-    unpack_triangle(t, a, ab, ac, cn, fn);
-    if (k == 1u) return TriVertex{a[0] + ab[0], a[1] + ab[1], a[2] + ab[2]};
-    if (k == 2u) return TriVertex{a[0] + ac[0], a[1] + ac[1], a[2] + ac[2]};
-    return TriVertex{a[0], a[1], a[2]};
+    const float ax = t.p0.x, ay = t.p0.y, az = t.p0.z;
+    if (k == 1u) return TriVertex{ax + t.p0.w, ay + t.p1.x, az + t.p1.y};
+    if (k == 2u) return TriVertex{ax + t.p1.z, ay + t.p1.w, az + t.p2.x};
+    return TriVertex{ax, ay, az};
 }
 
 extern "C" __global__ void __launch_bounds__(256) rt_wide_vertices_kernel(const RtTriangleHot* __restrict__ tris,

@@ -41,14 +41,14 @@ float box_area(const float* lo, const float* hi) {
     return (float)(2.0 * (dx * dy + dy * dz + dz * dx));
 }
 
-// a, ab, ac, cn of triangle i in the 64-B hot layout (16 floats: cn.xyz a.x |
-// a.yz ab.xy | ab.z ac.xyz | fn.xyz 0), rt_kernel_args.h RtTriangleHot.
+// a, ab, ac, cn of triangle i in the 64-B hot layout (16 floats: a.xyz ab.x |
+// ab.yz ac.xy | ac.z cn.xyz | fn.xyz 0), rt_kernel_args.h RtTriangleHot.
 void hot_fields(const float* hot16, uint32_t i, float* a, float* ab, float* ac, float* cn) {
     const float* p = hot16 + 16 * (size_t)i;
-    cn[0] = p[0], cn[1] = p[1], cn[2] = p[2];
-    a[0] = p[3], a[1] = p[4], a[2] = p[5];
-    ab[0] = p[6], ab[1] = p[7], ab[2] = p[8];
-    ac[0] = p[9], ac[1] = p[10], ac[2] = p[11];
+    a[0] = p[0], a[1] = p[1], a[2] = p[2];
+    ab[0] = p[3], ab[1] = p[4], ab[2] = p[5];
+    ac[0] = p[6], ac[1] = p[7], ac[2] = p[8];
+    cn[0] = p[9], cn[1] = p[10], cn[2] = p[11];
 }
 
 bool same_bits(const float* x, const float* y, int n) { return std::memcmp(x, y, sizeof(float) * n) == 0; }

@@ -248,9 +248,9 @@ int main(int argc, char** argv) {
     std::vector<float> hot(16 * tr.size());
     for (size_t i = 0; i < tr.size(); i++) {
         const rt_scene_triangle& t = tr[i];
-        const float f[16] = {t.calc_normal[0], t.calc_normal[1], t.calc_normal[2], t.a[0], t.a[1], t.a[2],
-                             t.edge_ab[0], t.edge_ab[1], t.edge_ab[2], t.edge_ac[0], t.edge_ac[1], t.edge_ac[2],
-                             t.face_normal[0], t.face_normal[1], t.face_normal[2], 0.0f};  // RtTriangleHot
+        const float f[16] = {t.a[0], t.a[1], t.a[2], t.edge_ab[0], t.edge_ab[1], t.edge_ab[2], t.edge_ac[0], t.edge_ac[1],
+                             t.edge_ac[2], t.calc_normal[0], t.calc_normal[1], t.calc_normal[2], t.face_normal[0],
+                             t.face_normal[1], t.face_normal[2], 0.0f};
         memcpy(&hot[16 * i], f, sizeof(f));
     }
     TriWide W;

@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
-    ap.add_argument("--env", nargs="*", default=[])
+    ap.add_argument("--env", nargs="*", default=[], help="KNOB=V settings for every build (before its own :knobs)")
     ap.add_argument("--device-rays", action="store_true", help="generate primary rays on the device")
     ap.add_argument("--frame-batch", type=int, default=8, help="rt_set_frame_batch (frames is rounded to a multiple)")
     ap.add_argument("--world", type=int, default=1, help="time rank --rank's share of an N-way tile split")
@@ -49,7 +49,7 @@ def main():
         # "path.so" or "path.so:KNOB=V,KNOB2=V": env knobs are read when the context is created
         p, _, knobs = spec.partition(":")
         saved = dict(os.environ)
-        for kv in filter(None, knobs.split(",")):
+        for kv in [*args.env, *filter(None, knobs.split(","))]:  # --env applies to every build
             k, _, v = kv.partition("=")
             os.environ[k] = v
         lib = N.load_library(Path(p).resolve())
