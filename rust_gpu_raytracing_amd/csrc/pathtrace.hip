@@ -1189,7 +1189,9 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // else the trace starts at the next setup step.
     // (The record is read at the next shading step, where it is used: kPrimary.)
     auto primary_start = [&]() -> uint32_t {
-        return (ka.primary && p.bounce < ka.bounces) ? kPrimary : kSetup;
+        // (triangle instances only: on a sphere scene the pass measured slower, and the
+        // sphere-only kernel keeps none of its code)
+        return (kTris && ka.primary && p.bounce < ka.bounces) ? kPrimary : kSetup;
     };
 
     // A finished sample: pixel_color += per_pixel(...) (:161); then the pixel's
@@ -1282,7 +1284,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         // the primary pre-pass has its first trace result in ka.primary.
         bool fin = false;      // a sample finished: its rays go to the tile's cost
         uint32_t fin_rays = 0;
-        if (mode == kPrimary) {
+        if (kTris && mode == kPrimary) {
             const uint4 r = ka.primary[(size_t)(frame * samples + sample) * ((size_t)ka.owned_tiles * 64u) +
                                        (size_t)lane_tile * 64u + lane_slot];
             primary_state(PrimaryRecord{__uint_as_float(r.x), r.y, r.z, r.w}, ts);
@@ -1898,7 +1900,7 @@ hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t l
         hipLaunchKernelGGL((rt_primary_kernel<M, TR>), dim3(blocks), dim3(kPrimaryThreads), lds_bytes, stream, ka); \
         return hipGetLastError();                                                                              \
     }
-    RT_PRIMARY(1, true) RT_PRIMARY(2, true) RT_PRIMARY(1, false)
+    RT_PRIMARY(1, true) RT_PRIMARY(2, true)
 #undef RT_PRIMARY
     return hipErrorInvalidValue;
 }

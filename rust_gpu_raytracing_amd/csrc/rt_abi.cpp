@@ -1353,8 +1353,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // accelerator stays in global memory (mode 1 with triangles, C5: wall -12%); with the
     // accelerator in LDS (C3, C4) or no triangles (C2) the pass costs more wall time than it
     // takes off the path kernel (+13%, +13%, +23%: profiles/r03_i/ab_primary.jsonl)
-    const bool primary = bounces > 0 && mode >= 1 && !wide && ka.compute_per_frame > 0 &&
-                         (ctx->primary_pass == 1 || (ctx->primary_pass == -1 && tris && mode == 1));
+    const bool primary = bounces > 0 && mode >= 1 && tris && !wide && ka.compute_per_frame > 0 &&
+                         (ctx->primary_pass == 1 || (ctx->primary_pass == -1 && mode == 1));
     ka.primary = nullptr;
     if (primary) {
         const int pi = (int)(ctx->batches & 1u);

@@ -662,7 +662,6 @@ def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
 
 
 @pytest.mark.parametrize("config,kw,spp,accumulate,batch,world,env", [
-    ("c2_rtiow", {}, 1, 1, 4, 1, {"RT_PRIMARY_PASS": "1"}),          # forced on a sphere scene
     ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {"RT_PRIMARY_PASS": "1"}),
     ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {"RT_PRIMARY_PASS": "1"}),  # non-accumulating batch
     ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 4, 3, {"RT_PRIMARY_PASS": "1"}),  # tile split
