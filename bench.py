@@ -53,6 +53,8 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mray/s (primary+bounce) at 1920x1080, 8 bounces; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+KERNEL_NAMES = {"path": "rt_pathtrace_kernel", "primary": "rt_primary_kernel", "resolve": "rt_resolve_frames_kernel",
+                "brute": "rt_brute_kernel"}
 # The reference computes a frame every >= 0.8 ms and displays every >= 5 ms
 # (src/main.rs:88-92, 365-375): about 6 computed frames per displayed image.
 DISPLAY_CADENCE_FRAMES = 6
@@ -319,6 +321,7 @@ def main() -> int:
                    streamed=r.streamed_bytes(),
                    settle_frames=settle_frames,
                    t_render=t_render, t_gather=t_gather, gathered=gathered, launch=r.launch_config(),
+                   passes=r.last_launch_passes(),
                    timing=r.dispatch_time_total(), resolve_timing=r.resolve_time_total(),
                    owned_px=r.owned_pixel_count())
         stats = torch.tensor([t_total, t_render, t_gather, t_gather_accum, t_gather_image, float(res["rays"])],
@@ -380,7 +383,8 @@ def main() -> int:
         rays_total = g.ray_count()
         return dict(r=g, scene=scene, bounces=bounces, width=args.width, height=args.height,
                     rays=rays_total / n, settle_frames=settle_frames, t_render=t_total - t_gather,
-                    t_gather=t_gather, gathered=True, launch=v0.launch_config(), timing=v0.dispatch_time_total(),
+                    t_gather=t_gather, gathered=True, launch=v0.launch_config(), passes=v0.last_launch_passes(),
+                    timing=v0.dispatch_time_total(),
                     resolve_timing=v0.resolve_time_total(), owned_px=v0.owned_pixel_count(),
                     t_total_max=t_total, t_render_max=t_total - t_gather, t_gather_max=t_gather,
                     t_gather_accum_max=t_gather if args.gather == "accumulation" else 0.0,
@@ -494,12 +498,12 @@ def main() -> int:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": pmc_traffic(pmc),
                 "traffic_source": pmc["source"] if pmc else pmc_why,
-                "kernel": "rt_pathtrace_kernel + rt_resolve_frames_kernel",
+                "kernel": " + ".join(KERNEL_NAMES[p] for p in m.get("passes", ["path", "resolve"])),
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "path_kernel_ms_avg": avg_path_s * 1e3,
                 "resolve_ms_avg": avg_resolve_s * 1e3,
-                "kernel_timing": ("device-clock span per launch (first workgroup start to last end), rt_set_timing: "
-                                  "path kernel + the batch's resolve pass"),
+                "kernel_timing": ("device-clock span per launch (first workgroup start to last end, the primary "
+                                  "pre-pass included when it runs), rt_set_timing, plus the batch's resolve pass"),
                 "counter_frac": (pmc_traffic(pmc) / avg_path_s / 1e9 / HBM_PEAK_GBS) if pmc else None,  # PMC: path kernel
                 "valu_frac": ((pmc["valu_issue_util"] * pmc["valu_lane_util"])
                               if pmc and pmc.get("valu_issue_util") is not None else None),
@@ -509,7 +513,9 @@ def main() -> int:
                 "launch": m["launch"],
                 "bytes_per_launch": b_launch,
                 "tile_stream_bytes_per_launch": stream_launch,
-                "note": "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction",
+                "note": ("the reference's sweeps: VALU-bound on sub-object box tests (DESIGN §5.5)"
+                         if args.brute_force else
+                         "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction"),
                 "valu": pmc_issue(pmc),
                 "build_hash": build_hash,
             },

@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -368,6 +368,15 @@ RT_API int rt_unpack_output_ranks(rt_ctx* ctx, const void* src_device, uint64_t 
  * BVH staged in LDS, 2: also the triangle accelerator). */
 RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
                             uint32_t* scene_in_lds);
+
+/* The kernels the last rt_dispatch ran (diagnostics, ABI 7), a mask of RT_PASS_*:
+ * the path kernel, the coherent primary-ray pre-pass, the batch resolve pass, or the
+ * brute-force sweep kernel instead of the path kernel. */
+#define RT_PASS_PATH 1u
+#define RT_PASS_PRIMARY 2u
+#define RT_PASS_RESOLVE 4u
+#define RT_PASS_BRUTE 8u
+RT_API int rt_last_launch_passes(const rt_ctx* ctx, uint32_t* passes);
 
 /* Diagnostic counters (filled only by builds compiled with -DRT_DIAG or
  * -DRT_DIAG_TAIL, zeros otherwise): out[0..n) receives up to 8 u64 counters

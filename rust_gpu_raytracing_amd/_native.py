@@ -133,6 +133,7 @@ SIGNATURES = {
     "rt_unpack_accumulation_ranks": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _U32, _U32, _U32]),
     "rt_unpack_output_ranks": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _U32, _U32]),
     "rt_launch_config": (ctypes.c_int, [_P] + [ctypes.POINTER(ctypes.c_uint32)] * 4),
+    "rt_last_launch_passes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_debug_counters": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), _U32]),
     "rt_math_selftest": (ctypes.c_int, [_U32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     "rt_stream": (_P, [_P]),

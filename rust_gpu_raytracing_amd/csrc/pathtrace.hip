@@ -29,6 +29,14 @@
 #include "rt_device_math.h"
 #include "rt_kernel_args.h"
 
+// Analysis builds (tools/isa_loops.py, -DRT_ISA_MARKS) tag kernel regions with an
+// assembly comment so the tool can find the loop around each; product builds emit nothing.
+#ifdef RT_ISA_MARKS
+#define RT_ISA_MARK(name) asm volatile("; RT_MARK " name)
+#else
+#define RT_ISA_MARK(name)
+#endif
+
 #pragma clang fp contract(off)
 
 using namespace rtk;
@@ -1293,6 +1301,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         if (mode == kDone) {
             const Hit h = trace_end<kTris>(sv, ka, p.o, p.d, ts);
             ++rays;
+            RT_ISA_MARK("shade");
             if (shade<(kMode >= 1)>(sv, ka, p, h)) {
                 // rays of the sample: one per bounce, plus the escaping one unless the limit ended it
                 fin = true;
@@ -1401,6 +1410,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             // Test the deferred leaves once enough of the traversing lanes
             // hold one (ka.leaf_batch eighths); otherwise advance every lane by
             // one node.
+            RT_ISA_MARK("traversal");
             bool leaves = false;
             if constexpr (kDeferLeaves<kTris>) {
                 const uint32_t n_pend = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
@@ -1410,10 +1420,13 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             const unsigned long long tl0 = stamp();
 #endif
             if (mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
-                if (kDeferLeaves<kTris> && leaves)
+                if (kDeferLeaves<kTris> && leaves) {
+                    RT_ISA_MARK("leaf_batch");
                     leaf_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
-                else
+                } else {
+                    RT_ISA_MARK("node_step");
                     node_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                }
                 phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
                 if (ts.phase == 2) mode = kDone;
                 if (!(kDeferLeaves<kTris> && leaves)) {
@@ -1729,6 +1742,8 @@ template <int kMode, bool kTris>
 __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t tid = threadIdx.x;
+    // rt_set_timing: the pre-pass opens the launch's device span (the path kernel closes it)
+    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     float* l_cam = l_srgb + 256;
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,

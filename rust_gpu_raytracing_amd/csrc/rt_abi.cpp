@@ -203,6 +203,7 @@ struct rt_ctx {
     uint32_t* d_tile_sched[2] = {};    // costs[2][n], orders[2][n], flags[2] (n = owned tiles)
     uint64_t sched_launches[2] = {};   // launches since the schedule was (re)set
     uint32_t last_blocks = 0, last_lds = 0;
+    uint32_t last_passes = 0;  // RT_PASS_* of the last dispatch
     float4* d_slot_sph = nullptr;        // kernel-ordered spheres (sphere_bvh.h)
     uint32_t* d_slot_orig = nullptr;
     uint32_t* d_sph_mat = nullptr;       // by original index
@@ -1235,6 +1236,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         RT_HIP(ctx, rt_launch_brute(ka, tris, lds, ctx->stream));
         ctx->last_blocks = (ctx->owned_tiles + 3u) / 4u;
+        ctx->last_passes = RT_PASS_BRUTE;
         ctx->last_lds = (uint32_t)lds;
         ctx->occ_threads = 256;
         ctx->primary_dirty = true;
@@ -1380,6 +1382,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     hipError_t e = rt_launch_pathtrace(ka, mode, tris, wide, ctx->occ_threads, lds_bytes, blocks, S);
     ctx->last_blocks = blocks;
+    ctx->last_passes = RT_PASS_PATH | (primary ? RT_PASS_PRIMARY : 0u) | (frame_par ? RT_PASS_RESOLVE : 0u);
     ctx->last_lds = (uint32_t)lds_bytes;
     if (e != hipSuccess) return hip_fail(ctx, "rt_pathtrace_kernel launch", e);
     if (frame_par) {
@@ -1831,6 +1834,12 @@ int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uin
     *blocks = ctx->last_blocks;
     *lds_bytes = ctx->last_lds;
     *scene_in_lds = ctx->occ_mode < 0 ? 0u : (uint32_t)ctx->occ_mode;
+    return RT_OK;
+}
+
+int rt_last_launch_passes(const rt_ctx* ctx, uint32_t* passes) {
+    if (!ctx || !passes) return RT_E_INVALID;
+    *passes = ctx->last_passes;
     return RT_OK;
 }
 

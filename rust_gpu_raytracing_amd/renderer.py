@@ -371,6 +371,13 @@ class Renderer:
         N.check(self._ctx, self._lib.rt_launch_config(self._ctx, *[ctypes.byref(x) for x in v]), self._lib)
         return dict(zip(("threads", "blocks", "lds_bytes", "scene_in_lds"), (x.value for x in v)))
 
+    def last_launch_passes(self) -> list:
+        """Kernels the last launch ran: "path", "primary" (pre-pass), "resolve", "brute"."""
+        v = ctypes.c_uint32()
+        N.check(self._ctx, self._lib.rt_last_launch_passes(self._ctx, ctypes.byref(v)), self._lib)
+        names = ((1, "path"), (2, "primary"), (4, "resolve"), (8, "brute"))
+        return [n for bit, n in names if v.value & bit]
+
     @property
     def stream_handle(self) -> int:
         return self._lib.rt_stream(self._ctx) or 0

@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--ns", type=int, nargs="*", default=[1, 2, 4, 8])
     ap.add_argument("--settle-ms", type=float, default=150.0, help="as bench.py --settle-ms")
     ap.add_argument("--frame-batch", type=int, default=0, help="override bench.default_frame_batch(N)")
+    ap.add_argument("--repeats", type=int, default=3, help="timed runs per rank (the median is used)")
     ap.add_argument("--gather", choices=["image", "accumulation"], default="image",
                     help="the gather payload priced (bench.py --gather; default image, 4 B/px)")
     ap.add_argument("--link-gbs", type=float, default=50.0,
@@ -85,7 +86,13 @@ def main():
     base = None
     for n in args.ns:
         fb = args.frame_batch or bench.default_frame_batch(n, args.steps)
-        per = [time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms, args.gather) for r in range(n)]
+        per = []
+        for r in range(n):
+            # the median of --repeats timed runs per rank (one 20-frame run is under 1 ms at N=8:
+            # a single launch-latency hiccup would move it by several percent)
+            runs = sorted((time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms, args.gather)
+                           for _ in range(args.repeats)), key=lambda x: x[0])
+            per.append(runs[len(runs) // 2])
         t_max = max(p[0] for p in per)
         rays = sum(p[1] for p in per)
         # gather estimate: packs run in parallel (max), rank 0 receives N-1 blocks over N-1 links
@@ -105,6 +112,7 @@ def main():
             "wall_ms_per_rank": [round(p[0] * 1e3, 4) for p in per],
             "steps": args.steps, "launch": per[0][7], "gather_payload": args.gather,
             "pack_ms_max": max(p[2] for p in per) * 1e3,
+            "rays_per_rank": [p[1] for p in per], "repeats": args.repeats,
         }), flush=True)
 
 
