@@ -68,6 +68,7 @@ struct SceneView {
     const float4* tri_wide;   // nodes (LDS in mode 2, else global)
     uint32_t* stk;            // this lane's walk stack in LDS: entry e at stk[e * stk_stride]
     uint32_t stk_stride;
+    const RtSubObject* sub;   // sub-object records (LDS in mode 2 when they fit, else global)
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -188,7 +189,7 @@ __device__ __forceinline__ TriHit sweep_triangles(const SceneView& sv, const Ker
         const uint32_t n_sub = ob.sub_object_count;
         for (uint32_t i = 0; i < n_sub; ++i) {
             const uint32_t si = min(first_sub + i, ka.sub_object_count - 1u);
-            const RtSubObject sub = ka.sub_objects[si];
+            const RtSubObject sub = sv.sub[si];
             if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
             for (uint32_t j = 0; j < sub.triangle_count; ++j) {
                 const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
@@ -335,7 +336,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
                                          uint32_t prim) {
     const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base
     const RtObject& ob = sv.obj[pr.x];
-    const RtSubObject sub = ka.sub_objects[pr.y];
+    const RtSubObject sub = sv.sub[pr.y];
     if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) ||
         !ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds))
         return;
@@ -1101,7 +1102,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
                  ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
-                 ka.tri_wide,     nullptr,        kThreads};
+                 ka.tri_wide,     nullptr,        kThreads,       ka.sub_objects};
     if constexpr (kWide) sv.stk = reinterpret_cast<uint32_t*>(lds + ka.lds_stack_offset) + tid;
     if (tid == 0) block_rays = 0;
     if constexpr (kMode >= 1) {
@@ -1153,6 +1154,11 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         for (uint32_t i = tid; i < ka.tri_prim_count; i += kThreads) l_tp[i] = ka.tri_prims[i];
         sv.tri_nodes = l_tn;
         sv.tri_prims = l_tp;
+        if (ka.lds_sub_offset) {  // the leaves' sub-object records too, when they fit
+            RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_sub_offset);
+            for (uint32_t i = tid; i < ka.sub_object_count; i += kThreads) l_sub[i] = ka.sub_objects[i];
+            sv.sub = l_sub;
+        }
     }
     for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];
     float* l_cam = l_srgb + 256;  // camera block for device-side primary rays
@@ -1596,7 +1602,7 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
     }
     __syncthreads();
     SceneView sv{l_sph, l_orig, l_smat, nullptr, l_mat, l_aux, l_obj, l_srgb, nullptr, nullptr, 0.0f,
-                 nullptr, nullptr, 0u};
+                 nullptr, nullptr, 0u,     ka.sub_objects};
 
     // this thread's pixel: local tile blockIdx * 4 + tid / 64 (global tile local * world + rank)
     const uint32_t local_tile = blockIdx.x * (kBruteThreads / 64u) + (tid >> 6);
@@ -1748,7 +1754,7 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
     float* l_cam = l_srgb + 256;
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
                  ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
-                 nullptr,         nullptr,        0u};
+                 nullptr,         nullptr,        0u,             ka.sub_objects};
     if constexpr (kMode >= 1) {  // what the walks read (the path kernel's mode 1 / 2 image)
         float4* l_sph = reinterpret_cast<float4*>(lds);
         RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
@@ -1773,6 +1779,11 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
         for (uint32_t i = tid; i < ka.tri_prim_count; i += kPrimaryThreads) l_tp[i] = ka.tri_prims[i];
         sv.tri_nodes = l_tn;
         sv.tri_prims = l_tp;
+        if (ka.lds_sub_offset) {
+            RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_sub_offset);
+            for (uint32_t i = tid; i < ka.sub_object_count; i += kPrimaryThreads) l_sub[i] = ka.sub_objects[i];
+            sv.sub = l_sub;
+        }
     }
     if (tid < 16u) {
         l_cam[tid] = ka.inv_proj[tid];
@@ -2008,6 +2019,13 @@ extern "C" __global__ void __launch_bounds__(256) rt_unpack_tiles_kernel(
 // -- so the sum is bit-identical to the frames rendered one after another; then
 // the accumulation and the last frame's packed output (:166-178). One thread per
 // owned pixel slot, coalesced: HBM-bound (16 + 16 * frames * samples + 20 B/px).
+// A 16-B load of data read once (nontemporal: it does not displace cached lines).
+typedef float StreamF4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_stream(const float4* p) {
+    const StreamF4 v = __builtin_nontemporal_load(reinterpret_cast<const StreamF4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ void resolve_pixel(float4* __restrict__ accum, uint32_t* __restrict__ output,
                                               const float4* __restrict__ light, uint32_t width, uint32_t height,
                                               uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world,
@@ -2023,8 +2041,25 @@ __device__ __forceinline__ void resolve_pixel(float4* __restrict__ accum, uint32
     const size_t idx = (size_t)y * width + x;
     float4 pix = accum[idx];
     const uint32_t n = frames * samples;
-    for (uint32_t i = 0; i < n; i++) {
-        const float4 l = light[(size_t)i * owned_px + gid];
+    // the lights are read once: groups of kGroup loads in flight together (streaming,
+    // nontemporal), then added in the reference's order
+    constexpr uint32_t kGroup = 8;
+    const float4* src = light + gid;
+    uint32_t i = 0;
+    for (; i + kGroup <= n; i += kGroup) {
+        float4 l[kGroup];
+#pragma unroll
+        for (uint32_t k = 0; k < kGroup; k++) l[k] = ld_stream(src + (size_t)(i + k) * owned_px);
+#pragma unroll
+        for (uint32_t k = 0; k < kGroup; k++) {
+            pix.x = pix.x + l[k].x;
+            pix.y = pix.y + l[k].y;
+            pix.z = pix.z + l[k].z;
+            pix.w = pix.w + l[k].w;
+        }
+    }
+    for (; i < n; i++) {
+        const float4 l = ld_stream(src + (size_t)i * owned_px);
         pix.x = pix.x + l.x;
         pix.y = pix.y + l.y;
         pix.z = pix.z + l.z;

@@ -163,6 +163,7 @@ struct rt_ctx {
     bool primary_dirty = true;        // primary-stream work since then that an aux batch must follow
     uint64_t batches = 0;             // frame-parallel batches launched
     bool batch_overlap = true;        // RT_BATCH_OVERLAP=0: every batch on the primary stream (A/B switch)
+    bool stage_subs = true;           // RT_STAGE_SUBS=0: mode 2 leaves read sub-objects from global (A/B switch)
     bool batch_schedule = false;      // RT_BATCH_SCHEDULE=1: cost-ordered claims in batches too (A/B switch)
     // a tile's frames claimed one after another (C3 -12%, C4 -8%, C5 -4%, C2 -1.8% per frame
     // against frame-major, profiles/archive/r02_knobs2); RT_UNIT_TILE_MAJOR=0: frame-major (A/B switch)
@@ -739,6 +740,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
         env = std::getenv("RT_FRAME_PARALLEL");
         if (env) ctx->frame_parallel = env[0] != '0';
+        env = std::getenv("RT_STAGE_SUBS");
+        if (env) ctx->stage_subs = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
         if (env) ctx->frame_batch = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxFrameBatch, (uint32_t)std::strtoul(env, nullptr, 10)));
         env = std::getenv("RT_BATCH_OVERLAP");
@@ -1180,6 +1183,16 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
             ka.lds_tri_prims_offset = (uint32_t)off;
             off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
+        }
+        // the sub-object records the leaves read, when they fit the mode-2 budget too
+        // (one dependent global load less per leaf test; RT_STAGE_SUBS=0 switches it off)
+        ka.lds_sub_offset = 0;
+        if (!wide && ctx->stage_subs && ka.sub_object_count != 0) {
+            const size_t with = al16(off + (size_t)ka.sub_object_count * sizeof(RtSubObject));
+            if (with + kLdsTailBytes <= kLdsAccelBudget) {
+                ka.lds_sub_offset = (uint32_t)off;
+                off = with;
+            }
         }
         mode2_bytes = off + kLdsTailBytes;
         if (ctx->force_global_scene) return 0;

@@ -209,6 +209,7 @@ struct KernelArgs {
     uint32_t lds_nodes_offset;
     uint32_t lds_tri_nodes_offset;
     uint32_t lds_tri_prims_offset;
+    uint32_t lds_sub_offset;  // mode 2: sub-object records staged in LDS at this offset; 0: read from global
     uint32_t lds_stack_offset;    // kWide: the walk's per-lane stack, tri_stack_depth x threads u32
     uint32_t lds_srgb_offset;
 };

@@ -362,6 +362,47 @@ def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, 
     assert_same(*end, acc, out, n)
 
 
+@pytest.mark.parametrize("stage", ["0", "1"])
+def test_gpu_sub_objects_in_lds(gpu, oracle_lib, monkeypatch, stage):
+    """Mode 2 stages the leaves' sub-object records in LDS when they fit (RT_STAGE_SUBS);
+    both ways, and through the in-plane sweep fallback that reads them too, the result is
+    the oracle's."""
+    monkeypatch.setenv("RT_STAGE_SUBS", stage)
+    scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
+    rays = scene.camera.recalculate_ray_directions()
+    acc, out, n = gpu_render(scene, bounces, 3, rays=rays)
+    with Renderer(scene, camera_rays=rays) as r:
+        r.compute_frame(bounces)
+        assert r.launch_config()["scene_in_lds"] == 2
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((64, 96, 4), np.float32)
+    out_o = np.zeros((64, 96), np.uint32)
+    n_o = sum(o.render_frame(scene.params(accumulation_index=k), bounces, acc_o, out_o) for k in (1, 2, 3))
+    assert_same(acc, out, n, acc_o, out_o, n_o)
+
+
+def test_gpu_last_launch_passes(gpu):
+    """rt_last_launch_passes names the kernels a dispatch ran (the bench's roofline uses it)."""
+    scene, bounces = build_config("c2_rtiow", width=64, height=48)
+    with Renderer(scene, frame_batch=2) as r:
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["path"]  # a single frame: no resolve pass
+        r.compute_frame(bounces)
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["path", "resolve"]
+    scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
+    with Renderer(scene) as r:
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["path", "primary"]  # accelerator in global memory
+        r.set_brute_force(True)
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["brute"]
+
+
 def test_gpu_update_scene_and_reset(gpu, oracle_lib):
     scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
     with Renderer(scene) as r:
