@@ -69,6 +69,9 @@ struct SceneView {
     uint32_t* stk;            // this lane's walk stack in LDS: entry e at stk[e * stk_stride]
     uint32_t stk_stride;
     const RtSubObject* sub;   // sub-object records (LDS in mode 2 when they fit, else global)
+    // the quantized triangle nodes (modes 0/1; null: the 32-B nodes) and their grid
+    const uint4* tri_q;
+    float qox, qoy, qoz, qsx, qsy, qsz;
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -541,9 +544,22 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     }
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
-    const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
-    const float4 lo = nodes[2u * ts.node];
-    const float4 hi = nodes[2u * ts.node + 1u];
+    float4 lo, hi;
+    if (kTris && !kWide && tri && sv.tri_q) {
+        // 16-B quantized node: the box decoded exactly (a superset of the 32-B node's box)
+        const uint4 q = sv.tri_q[ts.node];
+        lo = make_float4(fmaf((float)(q.x & 0xffffu), sv.qsx, sv.qox), fmaf((float)(q.x >> 16), sv.qsy, sv.qoy),
+                         fmaf((float)(q.y & 0xffffu), sv.qsz, sv.qoz), 0.0f);
+        hi = make_float4(fmaf((float)(q.y >> 16), sv.qsx, sv.qox), fmaf((float)(q.z & 0xffffu), sv.qsy, sv.qoy),
+                         fmaf((float)(q.z >> 16), sv.qsz, sv.qoz), 0.0f);
+        const bool is_leaf = (q.w & 0x80000000u) != 0u;
+        lo.w = __uint_as_float(is_leaf ? ts.node + 1u : q.w);  // a leaf's skip link is node + 1 (pre-order)
+        hi.w = __uint_as_float(is_leaf ? (q.w & 0xffffffu) : 0xffffffffu);
+    } else {
+        const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
+        lo = nodes[2u * ts.node];
+        hi = nodes[2u * ts.node + 1u];
+    }
     float near_t, far_t;
     if (!kTris && ka.sphere_boxes_ordered)  // (near, far) corners: no min/max per axis (6 VALU per node step)
         slab_hit_ordered(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
@@ -1104,6 +1120,20 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                  ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
                  ka.tri_wide,     nullptr,        kThreads,       ka.sub_objects};
     if constexpr (kWide) sv.stk = reinterpret_cast<uint32_t*>(lds + ka.lds_stack_offset) + tid;
+    if constexpr (kTris && !kWide && kMode <= 1) {
+        if (ka.tri_qnodes) {
+            const float4 g0 = ka.tri_qgrid[0], g1 = ka.tri_qgrid[1];
+            if (g0.w != 0.0f) {
+                sv.tri_q = ka.tri_qnodes;
+                sv.qox = g0.x;
+                sv.qoy = g0.y;
+                sv.qoz = g0.z;
+                sv.qsx = g1.x;
+                sv.qsy = g1.y;
+                sv.qsz = g1.z;
+            }
+        }
+    }
     if (tid == 0) block_rays = 0;
     if constexpr (kMode >= 1) {
         float4* l_sph = reinterpret_cast<float4*>(lds);

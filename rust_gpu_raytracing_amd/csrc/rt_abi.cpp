@@ -40,6 +40,8 @@ hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const 
                           const uint2* object_tris, const rt_scene::Placement* place, uint32_t object_count,
                           uint32_t n_tri, uint32_t n_sub, RtTriangleHot* tris, float4* bounds, RtSubObject* subs,
                           RtObject* objects, hipStream_t stream);
+hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, uint4* q, float4* grid,
+                                        hipStream_t stream);
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
@@ -164,6 +166,12 @@ struct rt_ctx {
     uint64_t batches = 0;             // frame-parallel batches launched
     bool batch_overlap = true;        // RT_BATCH_OVERLAP=0: every batch on the primary stream (A/B switch)
     bool stage_subs = true;           // RT_STAGE_SUBS=0: mode 2 leaves read sub-objects from global (A/B switch)
+    // 16-B quantized triangle nodes for walks from global memory (RT_TRI_QNODES=0: the 32-B nodes)
+    bool use_qnodes = true;
+    bool qnodes_dirty = true;          // the binary accelerator changed since the copy was made
+    uint4* d_tri_qnodes = nullptr;
+    float4* d_tri_qgrid = nullptr;
+    size_t qnodes_cap = 0;
     bool batch_schedule = false;      // RT_BATCH_SCHEDULE=1: cost-ordered claims in batches too (A/B switch)
     // a tile's frames claimed one after another (C3 -12%, C4 -8%, C5 -4%, C2 -1.8% per frame
     // against frame-major, profiles/archive/r02_knobs2); RT_UNIT_TILE_MAJOR=0: frame-major (A/B switch)
@@ -513,6 +521,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         (rc = upload_raw(ctx, ctx->d_tri_bvh, acc.nodes.data(), nb)) ||
         (rc = upload_raw(ctx, ctx->d_tri_prims, acc.prims.data(), pb)))
         return rc;
+    ctx->qnodes_dirty = true;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
     ctx->tri_prim_count = (uint32_t)acc.prims.size();
     // depth levels for the device refit (preorder: a node precedes its children)
@@ -740,6 +749,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
         env = std::getenv("RT_FRAME_PARALLEL");
         if (env) ctx->frame_parallel = env[0] != '0';
+        env = std::getenv("RT_TRI_QNODES");
+        if (env) ctx->use_qnodes = env[0] != '0';
         env = std::getenv("RT_STAGE_SUBS");
         if (env) ctx->stage_subs = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
@@ -819,7 +830,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
-                    ctx->d_primary[0], ctx->d_primary[1]};
+                    ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1260,6 +1271,30 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.sphere_boxes_ordered = (layouts == 8 && ctx->sphere_boxes_ordered && !tris) ? 1u : 0u;
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
     ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);
+    // walks of the binary triangle accelerator from global memory read its 16-B quantized copy
+    ka.tri_qnodes = nullptr;
+    ka.tri_qgrid = nullptr;
+    if (tris && !wide && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0 && ctx->use_qnodes) {
+        if (ctx->qnodes_cap < ka.tri_nodes) {
+            RT_HIP(ctx, join_aux(ctx));
+            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->d_tri_qnodes) RT_HIP(ctx, hipFree(ctx->d_tri_qnodes));
+            ctx->d_tri_qnodes = nullptr;
+            ctx->qnodes_cap = 0;
+            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qnodes), (size_t)ka.tri_nodes * sizeof(uint4)));
+            if (!ctx->d_tri_qgrid) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qgrid), 2 * sizeof(float4)));
+            ctx->qnodes_cap = ka.tri_nodes;
+            ctx->qnodes_dirty = true;
+        }
+        if (ctx->qnodes_dirty) {  // after the accelerator's upload or refit (primary stream)
+            RT_HIP(ctx, rt_launch_quantize_tri_nodes(reinterpret_cast<const SphereBvhNode*>(ctx->d_tri_bvh),
+                                                     ka.tri_nodes, ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->stream));
+            ctx->qnodes_dirty = false;
+            ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
+        }
+        ka.tri_qnodes = ctx->d_tri_qnodes;
+        ka.tri_qgrid = ctx->d_tri_qgrid;
+    }
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
@@ -1577,9 +1612,11 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
                                            ctx->d_tri_order, ctx->d_tri_level_off, ctx->tri_levels,
                                            ctx->d_tri_extent, true, ctx->stream));
         ctx->wide_refresh = false;
-    } else if (!ctx->wide_built && ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty)
+    } else if (!ctx->wide_built && ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty) {
         RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,
                                     ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
+        ctx->qnodes_dirty = true;
+    }
     return RT_OK;
 }
 

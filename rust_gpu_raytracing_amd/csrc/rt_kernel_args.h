@@ -126,6 +126,10 @@ struct KernelArgs {
     const RtTriangleHot* __restrict__ triangles;
     const float4* __restrict__ tri_bvh;           // BVH over (object, sub-object) pairs, float4 pairs per node
     const uint4* __restrict__ tri_prims;          // per leaf: object, sub-object, sweep position of its first triangle
+    // 16-B quantized copy of tri_bvh (rt_quantize_tri_nodes_kernel) for walks from global memory
+    // (LDS modes 0/1); tri_qgrid = {origin.xyz, valid}, {scale.xyz, 0}. Null: the 32-B nodes.
+    const uint4* __restrict__ tri_qnodes;
+    const float4* __restrict__ tri_qgrid;
     // 4-wide triangle accelerator (tri_wide.h), used by the kWide instances instead of tri_bvh / tri_prims
     const float4* __restrict__ tri_wide;          // TriWideNode[tri_nodes] as 8 float4 each
     const uint4* __restrict__ tri_leaves;         // TriLeaf as 4 uint4 each

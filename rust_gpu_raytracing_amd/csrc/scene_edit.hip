@@ -28,6 +28,7 @@
 #include "rt_kernel_args.h"
 #include "rt_scene_math.h"
 #include "sphere_bvh.h"
+#include "tri_qnode.h"
 #include "tri_wide.h"
 
 #pragma clang fp contract(off)
@@ -368,5 +369,31 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            hipStream_t stream) {
     hipLaunchKernelGGL(rt_refit_tri_bvh_kernel, dim3(1), dim3(kRefitThreads), 0, stream, nodes, prims, subs, order,
                        level_offsets, n_levels, extent_out);
+    return hipGetLastError();
+}
+
+// ---- 16-B quantized copy of the binary triangle accelerator (tri_qnode.h) ----
+// grid[0] = {origin.xyz, valid}, grid[1] = {scale.xyz, 0}; with valid = 0 the walk reads the
+// 32-B nodes.
+extern "C" __global__ void __launch_bounds__(256) rt_quantize_tri_nodes_kernel(const SphereBvhNode* __restrict__ nodes,
+                                                                              uint32_t n, uint4* __restrict__ q,
+                                                                              float4* __restrict__ grid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    TriQGrid g{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, false};
+    if (n != 0) g = tri_qgrid(nodes[0]);
+    if (i == 0) {
+        grid[0] = make_float4(g.origin[0], g.origin[1], g.origin[2], g.valid ? 1.f : 0.f);
+        grid[1] = make_float4(g.scale[0], g.scale[1], g.scale[2], 0.f);
+    }
+    if (!g.valid || i >= n) return;
+    uint32_t w[4];
+    tri_qnode(nodes[i], g, w);
+    q[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, uint4* q, float4* grid,
+                                        hipStream_t stream) {
+    const uint32_t blocks = n ? (n + 255u) / 256u : 1u;
+    hipLaunchKernelGGL(rt_quantize_tri_nodes_kernel, dim3(blocks), dim3(256), 0, stream, nodes, n, q, grid);
     return hipGetLastError();
 }

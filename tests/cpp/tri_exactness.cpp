@@ -3,10 +3,12 @@
 // must return exactly the triangle, object and distance of the reference's
 // sequential sweep (check_triangles, compute_shader.wgsl:422-517).
 // The 4-wide accelerator (tri_wide.h: 4-slot nodes, stack walk, compact vertex-
-// block leaves) is checked the same way, ray by ray.
+// block leaves) and the binary walk over the 16-B quantized nodes (tri_qnode.h) are
+// checked the same way, ray by ray; every quantized box must contain its node's box.
 // usage: tri_exactness <objects.bin> <subs.bin> <tris.bin> <rays.f32> [margin_scale]
 //   -> "ok <rays> <hits> <avg_tri_tests> <avg_nodes> <nan_fallbacks>"
 //      "wide <avg_tri_tests> <avg_node_loads> <compact_leaves> <leaves> <depth> <max_stack>"
+//      "qnodes <valid> <avg_nodes>"
 //   or the first mismatch
 #include <cmath>
 #include <cstdint>
@@ -18,6 +20,7 @@
 
 #include "rt_bvh_slab.h"
 #include "sphere_bvh.h"
+#include "tri_qnode.h"
 #include "tri_wide.h"
 
 static const float F32_MAX_ = 3.4028235e+38f;
@@ -83,6 +86,10 @@ static Res sweep(const std::vector<rt_object_info>& ob, const std::vector<rt_sub
     return r;
 }
 
+static long g_qnodes = 0;
+static const std::vector<uint32_t>* g_q = nullptr;  // quantized records (4 words per node), or null
+static TriQGrid g_grid;
+
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
     V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
@@ -94,8 +101,17 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
     uint32_t node = 0, n = (uint32_t)A.nodes.size();
     while (node < n) {
-        g_nodes++;
-        const SphereBvhNode& nd = A.nodes[node];
+        SphereBvhNode nd = A.nodes[node];
+        if (g_q) {  // the kernel's quantized-node walk: the decoded box and the link word
+            g_qnodes++;
+            const uint32_t* q = &(*g_q)[4 * (size_t)node];
+            tri_qnode_box(q, g_grid, nd.bmin, nd.bmax);
+            const bool is_leaf = (q[3] & 0x80000000u) != 0u;
+            nd.leaf = is_leaf ? (q[3] & 0xffffffu) : kSphereBvhInternal;
+            nd.skip = is_leaf ? node + 1 : q[3];
+        } else {
+            g_nodes++;
+        }
         float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
         slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
         bool hit = nt <= ft && ft >= 0.0f;
@@ -105,7 +121,7 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
             const rt_sub_object_info& s = sb[p.sub];
             if (rib(o, inv, OB.min_bounds, OB.max_bounds) && rib(o, inv, s.min_bounds, s.max_bounds)) {
                 for (uint32_t j = 0; j < s.triangle_count; j++) {
-                    g_tests++;
+                    if (!g_q) g_tests++;
                     uint32_t ti = s.first_triangle_index + j, seq = p.seq_base + j;
                     const rt_scene_triangle& t = tr[ti];
                     V cn = ld(t.calc_normal);
@@ -256,19 +272,41 @@ int main(int argc, char** argv) {
     TriWide W;
     build_triangle_wide(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), hot.data(), (uint32_t)tr.size(),
                         &W);
+    // the quantized copy, as rt_quantize_tri_nodes_kernel makes it; each box must contain its node's
+    std::vector<uint32_t> qn(4 * A.nodes.size());
+    g_grid = A.nodes.empty() ? TriQGrid{} : tri_qgrid(A.nodes[0]);
+    if (g_grid.valid) {
+        for (size_t i = 0; i < A.nodes.size(); i++) {
+            tri_qnode(A.nodes[i], g_grid, &qn[4 * i]);
+            float lo[3], hi[3];
+            tri_qnode_box(&qn[4 * i], g_grid, lo, hi);
+            for (int k = 0; k < 3; k++)
+                if (!(lo[k] <= A.nodes[i].bmin[k] && hi[k] >= A.nodes[i].bmax[k])) {
+                    printf("QNODE BOX node %zu axis %d: [%.9g %.9g] does not contain [%.9g %.9g]\n", i, k, lo[k], hi[k],
+                           A.nodes[i].bmin[k], A.nodes[i].bmax[k]);
+                    return 1;
+                }
+        }
+    }
     long n = (long)rays.size() / 6, hits = 0;
     for (long i = 0; i < n; i++) {
         V o = ld(&rays[6 * i]), d = ld(&rays[6 * i + 3]);
         Res a = sweep(ob, sb, tr, o, d), b = accel(A, ob, sb, tr, o, d, scale);
         Res c = wide(W, ob, tr, o, d, scale);
         if (c.tri == -2) c = sweep(ob, sb, tr, o, d);  // NaN distance met: the kernel's sweep fallback
-        for (const Res* x : {&b, &c}) {
+        Res e = b;
+        if (g_grid.valid) {
+            g_q = &qn;
+            e = accel(A, ob, sb, tr, o, d, scale);
+            g_q = nullptr;
+        }
+        for (const Res* x : {&b, &c, &e}) {
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
             memcpy(&tb, &x->t, 4);
             if (ta != tb || a.tri != x->tri || a.obj != x->obj || a.front != x->front) {
                 printf("MISMATCH (%s) ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n",
-                       x == &b ? "binary" : "wide", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
+                       x == &b ? "binary" : x == &c ? "wide" : "qnodes", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
                        x->t);
                 return 1;
             }
@@ -280,5 +318,6 @@ int main(int argc, char** argv) {
     printf("ok %ld %ld %.2f %.2f %ld\n", n, hits, (double)g_tests / n, (double)g_nodes / n, g_nan);
     printf("wide %.2f %.2f %ld %zu %u %u\n", (double)w_tests / n, (double)w_nodes / n, compact, W.leaves.size(), W.depth,
            w_max_stack);
+    printf("qnodes %d %.2f\n", g_grid.valid ? 1 : 0, (double)g_qnodes / n);
     return 0;
 }

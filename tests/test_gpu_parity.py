@@ -403,6 +403,26 @@ def test_gpu_last_launch_passes(gpu):
         assert r.last_launch_passes() == ["brute"]
 
 
+@pytest.mark.parametrize("qnodes,primary", [("1", "0"), ("0", "0"), ("1", "1")])
+def test_gpu_quantized_triangle_nodes(gpu, oracle_lib, monkeypatch, qnodes, primary):
+    """Walks of the binary triangle accelerator from global memory read its 16-B quantized
+    copy (tri_qnode.h: boxes rounded outward onto an exact f32 grid). Per-lane walk, and the
+    primary pre-pass beside it: the oracle's result either way."""
+    monkeypatch.setenv("RT_TRI_QNODES", qnodes)
+    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
+    scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
+    rays = scene.camera.recalculate_ray_directions()
+    acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
+    with Renderer(scene, camera_rays=rays) as r:
+        r.compute_frame(bounces)
+        assert r.launch_config()["scene_in_lds"] <= 1  # the accelerator in global memory
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((48, 64, 4), np.float32)
+    out_o = np.zeros((48, 64), np.uint32)
+    n_o = sum(o.render_frame(scene.params(accumulation_index=k), bounces, acc_o, out_o) for k in (1, 2))
+    assert_same(acc, out, n, acc_o, out_o, n_o)
+
+
 def test_gpu_update_scene_and_reset(gpu, oracle_lib):
     scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
     with Renderer(scene) as r:

@@ -55,6 +55,7 @@ def test_chess_scene_random_rays(harness, tmp_path):
     rays = random_rays(rng, 60000, [-12, -8, -12], [12, 8, 12], planes_y=[float(tris["a"][0][1])])
     out = run(harness, tmp_path, objs, subs, tris, rays)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
+    assert out.stdout.splitlines()[2].split()[1] == "1"  # quantized nodes walked and checked too
 
 
 def test_heightfield_and_grazing_rays(harness, tmp_path):
@@ -72,6 +73,10 @@ def test_heightfield_and_grazing_rays(harness, tmp_path):
     assert int(compact) == int(leaves)  # every heightfield strip is a compact leaf
     assert float(w_nodes) < 0.75 * float(nodes)  # 4-wide: fewer node loads than the binary walk's box tests
     assert int(max_stack) < int(depth) <= 32
+    # the 16-B quantized nodes (tri_qnode.h): every box contains its node's, the walk over them
+    # returns the sweep's result on every ray (checked above), and the coarser boxes cost few visits
+    _, q_valid, q_nodes = out.stdout.splitlines()[2].split()
+    assert int(q_valid) == 1 and float(q_nodes) < 1.1 * float(nodes)
 
 
 def test_shared_subobjects_duplicates_and_ties(harness, tmp_path):
