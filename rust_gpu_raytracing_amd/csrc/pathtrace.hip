@@ -335,16 +335,33 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
 
 // The triangle leaf: the reference's object and sub-object ray_in_bounds tests
 // and triangle tests for one (object, sub-object) pair (compute_shader.wgsl:431-500).
+// kLazySub (the accelerator in global memory): with the sub-object's triangle range in the
+// leaf record, the triangle loads start without the sub-object record, which is loaded and
+// its ray_in_bounds test run only for the first candidate that would change the lane's result
+// (a new best hit or a NaN distance); if that test fails, no triangle of the leaf counts --
+// exactly as the reference, which tests none of them then. Most leaves change nothing, so
+// their sub-object record is never read.
+template <bool kLazySub = false>
 __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
                                          uint32_t prim) {
-    const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base
+    const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base, range
     const RtObject& ob = sv.obj[pr.x];
-    const RtSubObject sub = sv.sub[pr.y];
-    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) ||
-        !ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds))
-        return;
-    for (uint32_t j = 0; j < sub.triangle_count; ++j) {
-        const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
+    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) return;
+    uint32_t first, count;
+    int sub_state;  // 1: passed, 0: not tested yet
+    if (kLazySub && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
+        first = pr.w & ((1u << 27) - 1u);
+        count = pr.w >> 27;
+        sub_state = 0;
+    } else {
+        const RtSubObject sub = sv.sub[pr.y];
+        if (!ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) return;
+        first = sub.first_triangle_index;
+        count = sub.triangle_count;
+        sub_state = 1;
+    }
+    for (uint32_t j = 0; j < count; ++j) {
+        const uint32_t ti = min(first + j, ka.triangle_count - 1u);
         const uint32_t seq = pr.z + j;
         const TriGeom g = load_tri(ka.triangles, ti);
         const float det = -dot(d, g.cn);
@@ -361,6 +378,11 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         if (u < 0.0f) continue;
         const float w = 1.0f - u - v;
         if (w < 0.0f) continue;
+        if (kLazySub && sub_state == 0) {
+            const RtSubObject sub = sv.sub[pr.y];
+            if (!ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) return;
+            sub_state = 1;
+        }
         if (nan_dist) {
             ts.nan_hit = true;
             continue;
@@ -582,7 +604,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     ts.node = (hit && !at_leaf) ? ts.node + 1u : __float_as_uint(lo.w);
 }
 
-template <bool kTris, bool kWide = false>
+template <bool kTris, bool kWide = false, bool kLazySub = false>
 __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     if (kWide && kTris && ts.phase == 0) {
         // one of the node's pending leaf records per batch
@@ -594,7 +616,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs&
         return;
     }
     if (kTris && ts.phase == 0)
-        tri_leaf(sv, ka, o, d, ts, ts.pending);
+        tri_leaf<kLazySub>(sv, ka, o, d, ts, ts.pending);
     else
     {
         test_sphere_group(sv, ts.pending, o, d, ts.a4, ts.a2, ts.sph);
@@ -1458,7 +1480,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             if (mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
                 if (kDeferLeaves<kTris> && leaves) {
                     RT_ISA_MARK("leaf_batch");
-                    leaf_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                    leaf_step<kTris, kWide, (kMode <= 1)>(sv, ka, p.o, p.d, ts);
                 } else {
                     RT_ISA_MARK("node_step");
                     node_step<kTris, kWide>(sv, ka, p.o, p.d, ts);

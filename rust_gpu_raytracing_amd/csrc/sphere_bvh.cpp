@@ -264,7 +264,7 @@ void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, 
             if (s.triangle_count == 0) continue;
             bool finite = true;
             for (int k = 0; k < 3; k++) finite = finite && std::isfinite(s.min_bounds[k]) && std::isfinite(s.max_bounds[k]);
-            prims.push_back(SubObjectPrim{o, si, base, 0});
+            prims.push_back(SubObjectPrim{o, si, base, prim_range(s.first_triangle_index, s.triangle_count)});
             for (int k = 0; k < 3; k++) {
                 // the reference's slab test is symmetric in min/max (:414-415); a
                 // non-finite box can still pass it on its other axes (NaN operands

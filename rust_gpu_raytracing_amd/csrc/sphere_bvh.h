@@ -87,8 +87,14 @@ struct SubObjectPrim {
     uint32_t object;    // object index (ray_in_bounds on its box, :431)
     uint32_t sub;       // sub-object index (ray_in_bounds on its box, :441)
     uint32_t seq_base;  // position of the sub-object's first triangle in the reference's sweep order
-    uint32_t _pad;
+    uint32_t range;     // first_triangle_index | triangle_count << 27 (kPrimRangeNone: read the sub-object)
 };
+constexpr uint32_t kPrimRangeNone = 0xffffffffu;
+// The sub-object's triangle range packed into its leaf record when it fits (first < 2^27, count < 32),
+// so a leaf test can start its triangle loads without the sub-object record (pathtrace.hip tri_leaf).
+inline uint32_t prim_range(uint32_t first, uint32_t count) {
+    return (first < (1u << 27) && count < 32u) ? (first | (count << 27)) : kPrimRangeNone;
+}
 static_assert(sizeof(SubObjectPrim) == 16, "prim layout");
 
 struct TriangleAccel {

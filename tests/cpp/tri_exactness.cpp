@@ -87,6 +87,7 @@ static Res sweep(const std::vector<rt_object_info>& ob, const std::vector<rt_sub
 }
 
 static long g_qnodes = 0;
+static bool g_lazy = false;  // the kernel's kLazySub leaf: the sub-object box tested at the first candidate
 static const std::vector<uint32_t>* g_q = nullptr;  // quantized records (4 words per node), or null
 static TriQGrid g_grid;
 
@@ -103,13 +104,13 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     while (node < n) {
         SphereBvhNode nd = A.nodes[node];
         if (g_q) {  // the kernel's quantized-node walk: the decoded box and the link word
-            g_qnodes++;
+            if (!g_lazy) g_qnodes++;
             const uint32_t* q = &(*g_q)[4 * (size_t)node];
             tri_qnode_box(q, g_grid, nd.bmin, nd.bmax);
             const bool is_leaf = (q[3] & 0x80000000u) != 0u;
             nd.leaf = is_leaf ? (q[3] & 0xffffffu) : kSphereBvhInternal;
             nd.skip = is_leaf ? node + 1 : q[3];
-        } else {
+        } else if (!g_lazy) {
             g_nodes++;
         }
         float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
@@ -119,10 +120,18 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
             const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
             const rt_object_info& OB = ob[p.object];
             const rt_sub_object_info& s = sb[p.sub];
-            if (rib(o, inv, OB.min_bounds, OB.max_bounds) && rib(o, inv, s.min_bounds, s.max_bounds)) {
-                for (uint32_t j = 0; j < s.triangle_count; j++) {
-                    if (!g_q) g_tests++;
-                    uint32_t ti = s.first_triangle_index + j, seq = p.seq_base + j;
+            const bool lazy = g_lazy && p.range != kPrimRangeNone;
+            int sub_state = lazy ? 0 : 1;
+            const uint32_t first = lazy ? (p.range & ((1u << 27) - 1u)) : s.first_triangle_index;
+            const uint32_t count = lazy ? (p.range >> 27) : s.triangle_count;
+            if (lazy && (first != s.first_triangle_index || count != s.triangle_count)) {
+                printf("PRIM RANGE mismatch\n");
+                exit(1);
+            }
+            if (rib(o, inv, OB.min_bounds, OB.max_bounds) && (lazy || rib(o, inv, s.min_bounds, s.max_bounds))) {
+                for (uint32_t j = 0; j < count; j++) {
+                    if (!g_q && !g_lazy) g_tests++;
+                    uint32_t ti = first + j, seq = p.seq_base + j;
                     const rt_scene_triangle& t = tr[ti];
                     V cn = ld(t.calc_normal);
                     float det = -dot(d, cn), inv_det = 1.0f / det;
@@ -138,6 +147,10 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
                     if (u < 0.0f) continue;
                     float w = 1.0f - u - v;
                     if (w < 0.0f) continue;
+                    if (sub_state == 0) {
+                        if (!rib(o, inv, s.min_bounds, s.max_bounds)) break;
+                        sub_state = 1;
+                    }
                     if (nan_dist) { nan_hit = true; continue; }
                     best = dist;
                     best_seq = seq;
@@ -300,13 +313,18 @@ int main(int argc, char** argv) {
             e = accel(A, ob, sb, tr, o, d, scale);
             g_q = nullptr;
         }
-        for (const Res* x : {&b, &c, &e}) {
+        g_lazy = true;  // the mode-1 kernel's walk: quantized nodes (when valid) and lazy sub-object tests
+        g_q = g_grid.valid ? &qn : nullptr;
+        Res f = accel(A, ob, sb, tr, o, d, scale);
+        g_q = nullptr;
+        g_lazy = false;
+        for (const Res* x : {&b, &c, &e, &f}) {
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
             memcpy(&tb, &x->t, 4);
             if (ta != tb || a.tri != x->tri || a.obj != x->obj || a.front != x->front) {
                 printf("MISMATCH (%s) ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n",
-                       x == &b ? "binary" : x == &c ? "wide" : "qnodes", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
+                       x == &b ? "binary" : x == &c ? "wide" : x == &e ? "qnodes" : "qnodes+lazy", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
                        x->t);
                 return 1;
             }
