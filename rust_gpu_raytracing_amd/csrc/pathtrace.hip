@@ -1875,7 +1875,7 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
                     const bool hit = valid && near_t <= far_t && far_t >= 0.0f;
                     const bool any = __ballot(hit) != 0;
                     const uint32_t leaf = __float_as_uint(hi.w);
-                    if (any && leaf != 0xffffffffu && hit) tri_leaf(sv, ka, o, d, ts, leaf & 0xffffffu);
+                    if (any && leaf != 0xffffffffu && hit) tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);
                     node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
                 }
                 if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
