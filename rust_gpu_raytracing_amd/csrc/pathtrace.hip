@@ -2126,10 +2126,16 @@ extern "C" __global__ void __launch_bounds__(256) rt_resolve_frames_kernel(
     float4* __restrict__ accum, uint32_t* __restrict__ output, const float4* __restrict__ light, uint32_t width,
     uint32_t height, uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
     uint32_t samples, uint32_t frames, unsigned long long* __restrict__ clock) {
-    // clock (rt_set_timing): {~earliest workgroup start, latest workgroup end}
-    if (clock && threadIdx.x == 0) atomicMax(clock, ~(unsigned long long)wall_clock64());
+    // clock (rt_set_timing): {~earliest workgroup start, latest workgroup end}, stamped by the
+    // first and the last kResolveStampBlocks workgroups only (workgroups start in index order
+    // and take the same time): thousands of workgroups each adding two atomics on the same two
+    // words cost tens of microseconds at the end of the pass
+    constexpr uint32_t kResolveStampBlocks = 64;
+    const bool first = blockIdx.x < kResolveStampBlocks;
+    const bool last = blockIdx.x + kResolveStampBlocks >= gridDim.x;
+    if (clock && first && threadIdx.x == 0) atomicMax(clock, ~(unsigned long long)wall_clock64());
     resolve_pixel(accum, output, light, width, height, tiles_x, owned_tiles, rank, world, k0, samples, frames);
-    if (clock) {
+    if (clock && last) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(clock + 1, (unsigned long long)wall_clock64());
     }
