@@ -148,3 +148,15 @@ def test_wide_large_sub_objects_and_inconsistent_records(harness, tmp_path):
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
     _, w_tests, w_nodes, compact, leaves, depth, max_stack = out.stdout.splitlines()[1].split()
     assert 0 < int(compact) < int(leaves)  # both kinds of leaves exercised
+
+
+def test_quantized_node_properties(tmp_path):
+    """tri_qnode.h on random roots and boxes (1e-30 .. 1e6, denormals, signed zeros, flat
+    boxes): the exact decode contains every stored box, and links round-trip."""
+    exe = tmp_path / "qnode_props"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", f"-I{ROOT / 'include'}",
+                    f"-I{ROOT / 'rust_gpu_raytracing_amd' / 'csrc'}", str(ROOT / "tests" / "cpp" / "qnode_props.cpp"),
+                    "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "3000"], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
+    assert int(out.stdout.split()[2]) > 100000
