@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -294,6 +294,18 @@ RT_API int rt_reset_ray_count(rt_ctx* ctx);
  * creation or the last rt_reset_ray_count. Synchronous. */
 RT_API int rt_set_brute_force(rt_ctx* ctx, int enable);
 RT_API int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out);
+
+/* Distance pruning of the triangle walk (new; ABI 8). The reference sweeps every
+ * object -> sub-object -> triangle (compute_shader.wgsl:422-517); the accelerator
+ * replaces the sweep by a walk that culls boxes the ray misses. With enable != 0
+ * (the default) the walk also skips boxes entered beyond the best triangle hit so
+ * far plus a slack of 1/64 of it, visiting the direction-ordered
+ * layout of the ray's octant first. The slack covers the f32 error of the
+ * reference's triangle test except for triangles within ~1e-4 rad of parallel to
+ * the ray whose plane passes within ~1e-4 x distance of its origin, where that
+ * test's own result is rounding noise; 0 = box culling only (exact by
+ * construction, as before ABI 8). Synchronous. */
+RT_API int rt_set_triangle_pruning(rt_ctx* ctx, int enable);
 
 /* Tile claim order (new; the reference dispatches a plain grid,
  * src/renderer.rs:238-249). 0 = tile index order. 1 = cost-ordered (the

@@ -117,6 +117,7 @@ SIGNATURES = {
     "rt_reset_ray_count": (ctypes.c_int, [_P]),
     "rt_accumulation_index": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_set_brute_force": (ctypes.c_int, [_P, ctypes.c_int]),
+    "rt_set_triangle_pruning": (ctypes.c_int, [_P, ctypes.c_int]),
     "rt_streamed_bytes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_set_tile_schedule": (ctypes.c_int, [_P, _U32]),
     "rt_tile_schedule_state": (ctypes.c_int, [_P, _P, _P]),

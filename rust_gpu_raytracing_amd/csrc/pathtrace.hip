@@ -28,6 +28,7 @@
 #include "rt_bvh_slab.h"
 #include "rt_device_math.h"
 #include "rt_kernel_args.h"
+#include "tri_qnode.h"
 
 // Analysis builds (tools/isa_loops.py, -DRT_ISA_MARKS) tag kernel regions with an
 // assembly comment so the tool can find the loop around each; product builds emit nothing.
@@ -259,8 +260,21 @@ __device__ __forceinline__ float prune_limit(const TraceState& ts) {
     return fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f + ts.slack;
 }
 
+// Distance pruning of the triangle walk (ka.tri_prune = rho, 0 = off): once a
+// triangle is hit at t, a box whose inflated entry lies beyond t * (1 + rho) + 2^-10 (|o| +
+// extent) / |d| is skipped. The slack covers the f32 error of the reference's distance and
+// barycentrics for every triangle not within ~1e-4 rad of parallel to the ray (where that
+// error grows as 1/cos), so such a box holds no triangle the reference would accept closer.
+constexpr float kTriPruneAbs = 0x1p-10f;
+__device__ __forceinline__ float tri_limit(const SceneView& sv, const KernelArgs& ka, f3 o, const TraceState& ts) {
+    if (ka.tri_prune == 0.0f || ts.tri.t == kF32Max) return __builtin_inff();
+    const float r = sqrt_up(dot(o, o));
+    const float sig = kTriPruneAbs * (r + sv.tri_extent) * (__builtin_amdgcn_rsqf(ts.a2 * 0.5f) * 1.001f);
+    return ts.tri.t * (1.0f + ka.tri_prune) + sig;
+}
+
 // Slab constants and depth bounds of a BVH walk. The triangle walk culls by
-// box only: no slack, no distance limit.
+// box, and by distance when pruning is on (tri_limit), with no slack.
 template <bool kTris>
 __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArgs& ka, f3 o, float a, uint32_t phase,
                                             TraceState& ts) {
@@ -275,6 +289,11 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
     }
     ts.slab = slab_ray(o.x, o.y, o.z, ts.inv.x, ts.inv.y, ts.inv.z, m);
     ts.limit = phase == 0 ? __builtin_inff() : prune_limit(ts);
+    if (kTris && phase == 0) {  // the accelerator layout ordered for this ray's direction octant (global walks)
+        const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
+                             ((__float_as_uint(ts.inv.z) >> 31) << 2);
+        ts.node = oct * ka.tri_octant_stride;
+    }
     if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
                              ((__float_as_uint(ts.inv.z) >> 31) << 2);
@@ -575,7 +594,8 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
         hi = make_float4(fmaf((float)(q.y >> 16), sv.qsx, sv.qox), fmaf((float)(q.z & 0xffffu), sv.qsy, sv.qoy),
                          fmaf((float)(q.z >> 16), sv.qsz, sv.qoz), 0.0f);
         const bool is_leaf = (q.w & 0x80000000u) != 0u;
-        lo.w = __uint_as_float(is_leaf ? ts.node + 1u : q.w);  // a leaf's skip link is node + 1 (pre-order)
+        // a leaf's skip link is node + 1 (pre-order), or the end for a layout's last leaf
+        lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : ts.node + 1u) : q.w);
         hi.w = __uint_as_float(is_leaf ? (q.w & 0xffffffu) : 0xffffffffu);
     } else {
         const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
@@ -615,9 +635,10 @@ __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs&
         tri_leaf_wide(sv, ka, o, d, ts, leaf);
         return;
     }
-    if (kTris && ts.phase == 0)
+    if (kTris && ts.phase == 0) {
         tri_leaf<kLazySub>(sv, ka, o, d, ts, ts.pending);
-    else
+        ts.limit = tri_limit(sv, ka, o, ts);
+    } else
     {
         test_sphere_group(sv, ts.pending, o, d, ts.a4, ts.a2, ts.sph);
         ts.limit = prune_limit(ts);
@@ -1866,16 +1887,20 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
         trace_begin<kTris>(sv, ka, o, d, ts);  // brute-force spheres, slab constants, phase
         if constexpr (kTris) {
             if (ts.phase == 0) {
-                // the triangle accelerator as a packet: wave-uniform node, per-lane culling
-                uint32_t node = 0;
+                // the triangle accelerator as a packet: wave-uniform node (the layout of the
+                // first lane's direction octant), per-lane culling and pruning
+                uint32_t node = __builtin_amdgcn_readfirstlane(ts.node);
                 while (node < ka.tri_nodes) {
                     const float4 lo = sv.tri_nodes[2u * node], hi = sv.tri_nodes[2u * node + 1u];
                     float near_t, far_t;
                     slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
-                    const bool hit = valid && near_t <= far_t && far_t >= 0.0f;
+                    const bool hit = valid && near_t <= far_t && far_t >= 0.0f && near_t <= ts.limit;
                     const bool any = __ballot(hit) != 0;
                     const uint32_t leaf = __float_as_uint(hi.w);
-                    if (any && leaf != 0xffffffffu && hit) tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);
+                    if (any && leaf != 0xffffffffu && hit) {
+                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);
+                        ts.limit = tri_limit(sv, ka, o, ts);
+                    }
                     node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
                 }
                 if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides

@@ -22,6 +22,7 @@
 #include "rt_kernel_args.h"
 #include "rt_scene_math.h"
 #include "sphere_bvh.h"
+#include "tri_qnode.h"
 #include "tri_wide.h"
 
 hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
@@ -40,8 +41,9 @@ hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const 
                           const uint2* object_tris, const rt_scene::Placement* place, uint32_t object_count,
                           uint32_t n_tri, uint32_t n_sub, RtTriangleHot* tris, float4* bounds, RtSubObject* subs,
                           RtObject* objects, hipStream_t stream);
-hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, uint4* q, float4* grid,
-                                        hipStream_t stream);
+hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, const uint32_t* src,
+                                        const uint32_t* skip, uint32_t n_out, SphereBvhNode* out32, uint4* q,
+                                        float4* grid, hipStream_t stream);
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
@@ -90,6 +92,9 @@ constexpr size_t kCounterWords = 1 + kDiagCounters + kDiagWaveRecords;
 // kQueueStripes = 4 per XCD by default (measured: C2 0.599 ms at 8, 0.595 at 32; C1
 // 0.076 -> 0.058 ms), up to kQueueStripesMax (RT_QUEUE_STRIPES).
 constexpr uint32_t kQueueStripes = 32;
+// Triangle-walk distance pruning: a node is skipped once its (inflated) box
+// is entered beyond best * (1 + kTriPruneRho) + kTriPruneAbs * (|o| + extent) / |d|.
+constexpr float kTriPruneRho = 1.0f / 64.0f;
 constexpr uint32_t kQueueStripesMax = 64;
 constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
@@ -169,6 +174,7 @@ struct rt_ctx {
     // 16-B quantized triangle nodes for walks from global memory (RT_TRI_QNODES=0: the 32-B nodes)
     bool use_qnodes = true;
     bool qnodes_dirty = true;          // the binary accelerator changed since the copy was made
+    bool derived_octants = false, derived_qnodes = false;  // what the last derivation produced
     uint4* d_tri_qnodes = nullptr;
     float4* d_tri_qgrid = nullptr;
     size_t qnodes_cap = 0;
@@ -236,6 +242,20 @@ struct rt_ctx {
     bool tri_dirty = true;
     uint32_t tri_count_built = 0xffffffffu;
     bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
+    // Direction-ordered layouts of the binary accelerator for walks from global memory (LDS
+    // modes 0/1; order_bvh_by_octant): per position of the 8 layouts the base node and the
+    // layout's skip link (host-built with the tree), and the 32-B copy derived from the base
+    // nodes on the device after every upload or refit (with the quantized copy).
+    // RT_TRI_OCTANTS=0: one layout (A/B switch).
+    bool use_tri_octants = true;
+    uint32_t* d_tri_src8 = nullptr;
+    uint32_t* d_tri_skip8 = nullptr;
+    SphereBvhNode* d_tri_bvh8 = nullptr;
+    size_t tri_src8_cap = 0, tri_skip8_cap = 0, tri_bvh8_cap = 0;
+    bool tri_octants_built = false;  // d_tri_src8 / d_tri_skip8 describe the current tree
+    // rt_set_triangle_pruning / RT_TRI_PRUNE: distance pruning of the triangle walk (DESIGN.md
+    // §5.3c): relative slack rho of the limit best * (1 + rho) + sigma, 0 = box culling only
+    float tri_prune = kTriPruneRho;
     // the 4-wide accelerator (tri_wide.h), RT_TRI_WIDE=1 (A/B switch): measured slower than the
     // binary one on C3-C5, so off by default
     bool use_tri_wide = false;
@@ -505,6 +525,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
             for (const TriLeaf& L : w.leaves) ctx->wide_compact_leaves += (L.count_flags & kWideLeafCompact) ? 1u : 0u;
             ctx->tri_levels = (uint32_t)w.level_off.size() - 1u;
             ctx->wide_built = true;
+            ctx->tri_octants_built = false;
             ctx->wide_refresh = false;
             ctx->tri_dirty = false;
             ctx->tri_count_built = object_count;
@@ -524,6 +545,22 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
     ctx->qnodes_dirty = true;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
     ctx->tri_prim_count = (uint32_t)acc.prims.size();
+    ctx->tri_octants_built = false;
+    if (ctx->use_tri_octants && acc.nodes.size() > 1 && acc.nodes.size() * 8 < (size_t)kTriWalkEnd) {
+        std::vector<SphereBvhNode> oct;
+        std::vector<uint32_t> src;
+        order_bvh_by_octant(acc.nodes, &oct, false, &src);
+        std::vector<uint32_t> skip(oct.size());
+        for (size_t i = 0; i < oct.size(); i++) skip[i] = oct[i].skip;
+        const size_t b8 = oct.size() * 4;
+        if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_src8), &ctx->tri_src8_cap, b8)) ||
+            (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_skip8), &ctx->tri_skip8_cap, b8)) ||
+            (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_bvh8), &ctx->tri_bvh8_cap, oct.size() * sizeof(SphereBvhNode))) ||
+            (rc = upload_raw(ctx, ctx->d_tri_src8, src.data(), b8)) ||
+            (rc = upload_raw(ctx, ctx->d_tri_skip8, skip.data(), b8)))
+            return rc;
+        ctx->tri_octants_built = true;
+    }
     // depth levels for the device refit (preorder: a node precedes its children)
     std::vector<uint32_t> depth(acc.nodes.size(), 0);
     uint32_t max_depth = 0;
@@ -749,6 +786,10 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
         env = std::getenv("RT_FRAME_PARALLEL");
         if (env) ctx->frame_parallel = env[0] != '0';
+        env = std::getenv("RT_TRI_OCTANTS");
+        if (env) ctx->use_tri_octants = env[0] != '0';
+        env = std::getenv("RT_TRI_PRUNE");
+        if (env) ctx->tri_prune = env[0] == '0' ? 0.0f : kTriPruneRho;
         env = std::getenv("RT_TRI_QNODES");
         if (env) ctx->use_qnodes = env[0] != '0';
         env = std::getenv("RT_STAGE_SUBS");
@@ -830,7 +871,8 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
-                    ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid};
+                    ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
+                    ctx->d_tri_skip8, ctx->d_tri_bvh8};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1271,30 +1313,51 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.sphere_boxes_ordered = (layouts == 8 && ctx->sphere_boxes_ordered && !tris) ? 1u : 0u;
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
     ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);
-    // walks of the binary triangle accelerator from global memory read its 16-B quantized copy
+    // walks of the binary triangle accelerator from global memory read its direction-ordered
+    // layouts (8 x tri_nodes positions, 32-B and 16-B quantized copies), else the single one
     ka.tri_qnodes = nullptr;
     ka.tri_qgrid = nullptr;
-    if (tris && !wide && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0 && ctx->use_qnodes) {
-        if (ctx->qnodes_cap < ka.tri_nodes) {
+    ka.tri_octant_stride = 0;
+    const bool global_walk = tris && !wide && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0;
+    const bool octants = global_walk && ctx->tri_octants_built;
+    const bool qnodes = global_walk && ctx->use_qnodes;
+    if (octants || qnodes) {
+        const uint32_t n_out = octants ? 8u * ka.tri_nodes : ka.tri_nodes;
+        if (qnodes && ctx->qnodes_cap < n_out) {
             RT_HIP(ctx, join_aux(ctx));
             RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
             if (ctx->d_tri_qnodes) RT_HIP(ctx, hipFree(ctx->d_tri_qnodes));
             ctx->d_tri_qnodes = nullptr;
             ctx->qnodes_cap = 0;
-            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qnodes), (size_t)ka.tri_nodes * sizeof(uint4)));
-            if (!ctx->d_tri_qgrid) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qgrid), 2 * sizeof(float4)));
-            ctx->qnodes_cap = ka.tri_nodes;
+            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qnodes), (size_t)n_out * sizeof(uint4)));
+            ctx->qnodes_cap = n_out;
             ctx->qnodes_dirty = true;
         }
-        if (ctx->qnodes_dirty) {  // after the accelerator's upload or refit (primary stream)
+        if (!ctx->d_tri_qgrid) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qgrid), 2 * sizeof(float4)));
+        if (ctx->qnodes_dirty || ctx->derived_octants != octants || ctx->derived_qnodes != qnodes) {
+            // after the accelerator's upload or refit (primary stream)
             RT_HIP(ctx, rt_launch_quantize_tri_nodes(reinterpret_cast<const SphereBvhNode*>(ctx->d_tri_bvh),
-                                                     ka.tri_nodes, ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->stream));
+                                                     ka.tri_nodes, octants ? ctx->d_tri_src8 : nullptr,
+                                                     octants ? ctx->d_tri_skip8 : nullptr, n_out,
+                                                     octants ? ctx->d_tri_bvh8 : nullptr,
+                                                     qnodes ? ctx->d_tri_qnodes : nullptr, ctx->d_tri_qgrid,
+                                                     ctx->stream));
             ctx->qnodes_dirty = false;
+            ctx->derived_octants = octants;
+            ctx->derived_qnodes = qnodes;
             ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
         }
-        ka.tri_qnodes = ctx->d_tri_qnodes;
-        ka.tri_qgrid = ctx->d_tri_qgrid;
+        if (qnodes) {
+            ka.tri_qnodes = ctx->d_tri_qnodes;
+            ka.tri_qgrid = ctx->d_tri_qgrid;
+        }
+        if (octants) {
+            ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh8);
+            ka.tri_octant_stride = ka.tri_nodes;
+            ka.tri_nodes = n_out;
+        }
     }
+    ka.tri_prune = (tris && !wide && ka.tri_accel) ? ctx->tri_prune : 0.0f;
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
@@ -1686,6 +1749,12 @@ int rt_ray_count(rt_ctx* ctx, uint64_t* out) {
 int rt_set_brute_force(rt_ctx* ctx, int enable) {
     RT_ENTER(ctx);
     ctx->brute = enable != 0;
+    return RT_OK;
+}
+
+int rt_set_triangle_pruning(rt_ctx* ctx, int enable) {
+    RT_ENTER(ctx);
+    ctx->tri_prune = enable ? kTriPruneRho : 0.0f;
     return RT_OK;
 }
 

@@ -161,6 +161,13 @@ struct KernelArgs {
     uint32_t tri_prim_count;  // triangle BVH leaves
     uint32_t tri_accel;       // 1: use the triangle BVH, 0: the reference's sweep
     const float* __restrict__ tri_extent;  // max |coordinate| over sub-object boxes (margin scale), device memory
+    // Walks from global memory (LDS modes 0/1): tri_bvh / tri_qnodes hold 8 direction-ordered
+    // layouts of tri_octant_stride nodes each (order_bvh_by_octant; tri_nodes = 8 x stride), a
+    // ray starts at layout octant(d) x stride; 0: one layout.
+    uint32_t tri_octant_stride;
+    // distance pruning of the triangle walk: once a triangle is hit at t, boxes
+    // entered beyond t * (1 + tri_prune) + 2^-10 (|o| + extent) / |d| are skipped; 0 = off
+    float tri_prune;
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     // Frame-parallel batch (frames > 1, accumulating): the queue holds one unit per

@@ -375,25 +375,40 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
 // ---- 16-B quantized copy of the binary triangle accelerator (tri_qnode.h) ----
 // grid[0] = {origin.xyz, valid}, grid[1] = {scale.xyz, 0}; with valid = 0 the walk reads the
 // 32-B nodes.
-extern "C" __global__ void __launch_bounds__(256) rt_quantize_tri_nodes_kernel(const SphereBvhNode* __restrict__ nodes,
-                                                                              uint32_t n, uint4* __restrict__ q,
-                                                                              float4* __restrict__ grid) {
+// With src / skip (the direction-ordered layouts of order_bvh_by_octant: n_out = 8 x n
+// positions, each the node src[i] of the base accelerator with the layout's skip link
+// skip[i]), position i of both copies is derived from the base node after every upload or
+// refit: out32 (32-B nodes, the layout's links) and q (quantized; a leaf whose skip leaves
+// its layout carries kTriQLastLeaf, so the walk ends there instead of at node + 1).
+extern "C" __global__ void __launch_bounds__(256) rt_quantize_tri_nodes_kernel(
+    const SphereBvhNode* __restrict__ nodes, uint32_t n, const uint32_t* __restrict__ src,
+    const uint32_t* __restrict__ skip, uint32_t n_out, SphereBvhNode* __restrict__ out32, uint4* __restrict__ q,
+    float4* __restrict__ grid) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     TriQGrid g{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, false};
     if (n != 0) g = tri_qgrid(nodes[0]);
-    if (i == 0) {
+    if (i == 0 && grid) {
         grid[0] = make_float4(g.origin[0], g.origin[1], g.origin[2], g.valid ? 1.f : 0.f);
         grid[1] = make_float4(g.scale[0], g.scale[1], g.scale[2], 0.f);
     }
-    if (!g.valid || i >= n) return;
+    if (i >= n_out) return;
+    SphereBvhNode nd = nodes[src ? src[i] : i];
+    if (src) {
+        nd.skip = skip[i];
+        if (out32) out32[i] = nd;
+    }
+    if (!g.valid || !q) return;
     uint32_t w[4];
-    tri_qnode(nodes[i], g, w);
+    tri_qnode(nd, g, w);
+    if (src && nd.leaf != kSphereBvhInternal && nd.skip >= n_out) w[3] |= kTriQLastLeaf;
     q[i] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, uint4* q, float4* grid,
-                                        hipStream_t stream) {
-    const uint32_t blocks = n ? (n + 255u) / 256u : 1u;
-    hipLaunchKernelGGL(rt_quantize_tri_nodes_kernel, dim3(blocks), dim3(256), 0, stream, nodes, n, q, grid);
+hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, const uint32_t* src,
+                                        const uint32_t* skip, uint32_t n_out, SphereBvhNode* out32, uint4* q,
+                                        float4* grid, hipStream_t stream) {
+    const uint32_t blocks = n_out ? (n_out + 255u) / 256u : 1u;
+    hipLaunchKernelGGL(rt_quantize_tri_nodes_kernel, dim3(blocks), dim3(256), 0, stream, nodes, n, src, skip, n_out,
+                       out32, q, grid);
     return hipGetLastError();
 }

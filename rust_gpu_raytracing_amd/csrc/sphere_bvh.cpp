@@ -205,8 +205,10 @@ bool box_layout_orderable(const std::vector<SphereBvhNode>& nodes) {
     return true;
 }
 
-void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out, bool swap_boxes) {
+void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out, bool swap_boxes,
+                         std::vector<uint32_t>* src_index) {
     out->clear();
+    if (src_index) src_index->clear();
     const uint32_t n = (uint32_t)in.size();
     if (n == 0) return;
     out->reserve(8 * (size_t)n);
@@ -217,6 +219,7 @@ void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<Spher
         std::function<void(uint32_t)> emit = [&](uint32_t src) {
             const uint32_t at = (uint32_t)out->size();
             out->push_back(in[src]);
+            if (src_index) src_index->push_back(src);
             if (swap_boxes)  // (near corner, far corner) for this octant
                 for (int k = 0; k < 3; k++)
                     if ((oct >> k) & 1u) std::swap(out->back().bmin[k], out->back().bmax[k]);

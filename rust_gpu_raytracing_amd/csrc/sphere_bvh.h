@@ -63,8 +63,10 @@ void build_sphere_slots(const rt_scene_sphere* spheres, uint32_t count, bool use
 // for its octant (bmin/bmax swapped on the axes of k's set bits), for the
 // min/max-free slab test (rt_bvh_slab.h: slab_hit_ordered); layout 0 is
 // unchanged either way. Only valid when box_layout_orderable(in).
+// src (optional) receives, per output node, the index of its node in `in` (the
+// device re-derives the layouts from `in` after a refit: rt_derive_tri_octants).
 void order_bvh_by_octant(const std::vector<SphereBvhNode>& in, std::vector<SphereBvhNode>* out,
-                         bool swap_boxes = false);
+                         bool swap_boxes = false, std::vector<uint32_t>* src = nullptr);
 
 // Every box is valid (bmin <= bmax) with finite coordinates of magnitude
 // <= 1e8, so that no plane * (1/d, capped at 1e30) overflows: the premise of

@@ -8,7 +8,8 @@
 // (fma(q, scale, origin), exact) contains the stored box, so the kernel's slab test on it
 // passes whenever the test on the stored box passes (f32 rounding is monotone): culling stays
 // exact. Link word: bit 31 set = leaf, bits 0-23 its record (the next node is always
-// node + 1 in pre-order); clear = internal node, the word is its skip link.
+// node + 1 in pre-order, except for the last leaf of a direction-ordered layout, which also
+// carries kTriQLastLeaf: its walk ends there); clear = internal node, the word is its skip link.
 // Shared by rt_quantize_tri_nodes_kernel (scene_edit.hip) and the CPU exactness harness.
 #pragma once
 
@@ -22,6 +23,9 @@
 #else
 #define RT_QN_FN inline
 #endif
+
+constexpr uint32_t kTriQLastLeaf = 0x40000000u;  // leaf link word: the walk ends after this leaf
+constexpr uint32_t kTriWalkEnd = 0x7fffffffu;     // a node index past every layout
 
 struct TriQGrid {
     float origin[3];

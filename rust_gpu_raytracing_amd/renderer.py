@@ -302,6 +302,11 @@ class Renderer:
         (BASELINE config 5's stress mode), instead of the acceleration structures."""
         self._call("rt_set_brute_force", int(enable))
 
+    def set_triangle_pruning(self, enable: bool) -> None:
+        """rt_set_triangle_pruning: distance pruning of the triangle walk (on by default;
+        False = box culling only, exact by construction)."""
+        self._call("rt_set_triangle_pruning", int(enable))
+
     def streamed_bytes(self) -> int:
         """Sub-object bytes the brute-force launches streamed through LDS."""
         v = ctypes.c_uint64()

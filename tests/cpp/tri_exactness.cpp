@@ -90,6 +90,13 @@ static long g_qnodes = 0;
 static bool g_lazy = false;  // the kernel's kLazySub leaf: the sub-object box tested at the first candidate
 static const std::vector<uint32_t>* g_q = nullptr;  // quantized records (4 words per node), or null
 static TriQGrid g_grid;
+// the kernel's global-memory walk (round 3): the direction-ordered layouts (order_bvh_by_octant,
+// quantized with the last-leaf flag as rt_quantize_tri_nodes_kernel derives them) and distance
+// pruning with the kernel's limit (pathtrace.hip tri_limit)
+static const std::vector<SphereBvhNode>* g_oct = nullptr;
+static const std::vector<uint32_t>* g_qoct = nullptr;
+static float g_prune = 0.0f;
+static long g_prune_nodes = 0, g_prune_tests = 0;
 
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
@@ -100,22 +107,33 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     Res r{F32_MAX_, -1, -1, 0};
     bool nan_hit = false;
     const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
-    uint32_t node = 0, n = (uint32_t)A.nodes.size();
+    const std::vector<SphereBvhNode>& NS = g_oct ? *g_oct : A.nodes;
+    const std::vector<uint32_t>* QS = g_oct ? g_qoct : g_q;
+    uint32_t n = (uint32_t)NS.size();
+    uint32_t node = 0;
+    if (g_oct) {
+        uint32_t ib[3];
+        memcpy(ib, &inv, 12);
+        node = ((ib[0] >> 31) | ((ib[1] >> 31) << 1) | ((ib[2] >> 31) << 2)) * (uint32_t)A.nodes.size();
+    }
+    float limit = INFINITY;
+    const float sig = 0x1p-10f * (std::sqrt(dot(o, o)) + A.extent) * (1.0f / std::sqrt(dot(d, d)) * 1.001f);
     while (node < n) {
-        SphereBvhNode nd = A.nodes[node];
-        if (g_q) {  // the kernel's quantized-node walk: the decoded box and the link word
+        SphereBvhNode nd = NS[node];
+        if (g_prune != 0.0f) g_prune_nodes++;
+        if (QS) {  // the kernel's quantized-node walk: the decoded box and the link word
             if (!g_lazy) g_qnodes++;
-            const uint32_t* q = &(*g_q)[4 * (size_t)node];
+            const uint32_t* q = &(*QS)[4 * (size_t)node];
             tri_qnode_box(q, g_grid, nd.bmin, nd.bmax);
             const bool is_leaf = (q[3] & 0x80000000u) != 0u;
             nd.leaf = is_leaf ? (q[3] & 0xffffffu) : kSphereBvhInternal;
-            nd.skip = is_leaf ? node + 1 : q[3];
+            nd.skip = is_leaf ? ((q[3] & kTriQLastLeaf) ? kTriWalkEnd : node + 1) : q[3];
         } else if (!g_lazy) {
             g_nodes++;
         }
         float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
         slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
-        bool hit = nt <= ft && ft >= 0.0f;
+        bool hit = nt <= ft && ft >= 0.0f && nt <= limit;
         if (hit && nd.leaf != kSphereBvhInternal) {
             const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
             const rt_object_info& OB = ob[p.object];
@@ -131,6 +149,7 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
             if (rib(o, inv, OB.min_bounds, OB.max_bounds) && (lazy || rib(o, inv, s.min_bounds, s.max_bounds))) {
                 for (uint32_t j = 0; j < count; j++) {
                     if (!g_q && !g_lazy) g_tests++;
+                    if (g_prune != 0.0f) g_prune_tests++;
                     uint32_t ti = first + j, seq = p.seq_base + j;
                     const rt_scene_triangle& t = tr[ti];
                     V cn = ld(t.calc_normal);
@@ -155,6 +174,7 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
                     best = dist;
                     best_seq = seq;
                     r = {dist, (int)ti, (int)p.object, det > 0.0f};
+                    if (g_prune != 0.0f) limit = best * (1.0f + g_prune) + sig;
                 }
             }
         }
@@ -301,6 +321,16 @@ int main(int argc, char** argv) {
                 }
         }
     }
+    std::vector<SphereBvhNode> oct;
+    std::vector<uint32_t> qoct;
+    order_bvh_by_octant(A.nodes, &oct, false);
+    if (g_grid.valid) {
+        qoct.resize(4 * oct.size());
+        for (size_t i = 0; i < oct.size(); i++) {
+            tri_qnode(oct[i], g_grid, &qoct[4 * i]);
+            if (oct[i].leaf != kSphereBvhInternal && oct[i].skip >= oct.size()) qoct[4 * i + 3] |= kTriQLastLeaf;
+        }
+    }
     long n = (long)rays.size() / 6, hits = 0;
     for (long i = 0; i < n; i++) {
         V o = ld(&rays[6 * i]), d = ld(&rays[6 * i + 3]);
@@ -316,15 +346,23 @@ int main(int argc, char** argv) {
         g_lazy = true;  // the mode-1 kernel's walk: quantized nodes (when valid) and lazy sub-object tests
         g_q = g_grid.valid ? &qn : nullptr;
         Res f = accel(A, ob, sb, tr, o, d, scale);
+        // the default global-memory walk: octant layouts (quantized when valid), lazy sub-objects, pruning
+        g_oct = oct.empty() ? nullptr : &oct;
+        g_qoct = g_grid.valid ? &qoct : nullptr;
+        g_prune = 1.0f / 64.0f;
+        Res h = accel(A, ob, sb, tr, o, d, scale);
+        g_prune = 0.0f;
+        g_oct = nullptr;
+        g_qoct = nullptr;
         g_q = nullptr;
         g_lazy = false;
-        for (const Res* x : {&b, &c, &e, &f}) {
+        for (const Res* x : {&b, &c, &e, &f, &h}) {
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
             memcpy(&tb, &x->t, 4);
             if (ta != tb || a.tri != x->tri || a.obj != x->obj || a.front != x->front) {
                 printf("MISMATCH (%s) ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n",
-                       x == &b ? "binary" : x == &c ? "wide" : x == &e ? "qnodes" : "qnodes+lazy", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
+                       x == &b ? "binary" : x == &c ? "wide" : x == &e ? "qnodes" : x == &f ? "qnodes+lazy" : "octants+prune", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
                        x->t);
                 return 1;
             }
@@ -337,5 +375,6 @@ int main(int argc, char** argv) {
     printf("wide %.2f %.2f %ld %zu %u %u\n", (double)w_tests / n, (double)w_nodes / n, compact, W.leaves.size(), W.depth,
            w_max_stack);
     printf("qnodes %d %.2f\n", g_grid.valid ? 1 : 0, (double)g_qnodes / n);
+    printf("prune %.2f %.2f\n", (double)g_prune_nodes / n, (double)g_prune_tests / n);
     return 0;
 }

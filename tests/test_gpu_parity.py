@@ -423,6 +423,46 @@ def test_gpu_quantized_triangle_nodes(gpu, oracle_lib, monkeypatch, qnodes, prim
     assert_same(acc, out, n, acc_o, out_o, n_o)
 
 
+@pytest.mark.parametrize("prune,octants,primary", [("1", "1", "0"), ("1", "0", "0"), ("1", "1", "1"),
+                                                   ("0", "1", "0")])
+def test_gpu_triangle_pruning(gpu, oracle_lib, monkeypatch, prune, octants, primary):
+    """Distance pruning of the triangle walk over the direction-ordered layouts (DESIGN.md
+    §5.3c), per-lane walk and primary pre-pass, and each switch alone: the oracle's result."""
+    monkeypatch.setenv("RT_TRI_PRUNE", prune)
+    monkeypatch.setenv("RT_TRI_OCTANTS", octants)
+    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
+    scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
+    rays = scene.camera.recalculate_ray_directions()
+    acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((48, 64, 4), np.float32)
+    out_o = np.zeros((48, 64), np.uint32)
+    n_o = sum(o.render_frame(scene.params(accumulation_index=k), bounces, acc_o, out_o) for k in (1, 2))
+    assert_same(acc, out, n, acc_o, out_o, n_o)
+
+
+@pytest.mark.parametrize("config,kw,frames", [
+    ("c5_heightfield", {}, 6),
+    ("c3_chess", {}, 20),
+    ("c4_mixed", dict(width=1920, height=1080), 10),
+])
+def test_gpu_triangle_pruning_full_frames(gpu, config, kw, frames):
+    """At BASELINE size the pruned walk (default) and box culling alone (rt_set_triangle_pruning
+    0, exact by construction) give the same accumulation bit for bit, frame after frame."""
+    scene, bounces = build_config(config, **kw)
+    res = []
+    for prune in (True, False):
+        with Renderer(scene, frame_batch=frames) as r:
+            r.set_triangle_pruning(prune)
+            for _ in range(frames):
+                r.compute_frame(bounces)
+            res.append((r.read_accumulation(), r.read_output(), r.ray_count()))
+    (a1, o1, n1), (a0, o0, n0) = res
+    assert n1 == n0
+    assert np.array_equal(o1, o0)
+    assert np.array_equal(a1.view(np.uint32), a0.view(np.uint32))
+
+
 def test_gpu_update_scene_and_reset(gpu, oracle_lib):
     scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
     with Renderer(scene) as r:
