@@ -101,10 +101,11 @@ constexpr uint32_t kQueueStride = 64;
 // traversing (pathtrace.hip, step 4 of the kernel loop). The longer a trace is
 // against a shading pass, the earlier it pays to shade the finished lanes
 // (measured: sphere scenes 8, C2 slower at 12+; triangle accelerator in LDS
-// 24, C3/C4 -2%; in global memory 32, C5 -10%).
+// 24, C3/C4 -2%; in global memory 32, C5 -10%; with the pruned octant walk of round 3,
+// 48: C5 5.95 -> 5.72 ms, profiles/r03_ah/knobs_c5b.jsonl; C3 unchanged at 24-32).
 uint32_t trav_threshold_for(int lds_mode, bool tris) {
     if (!tris) return 8;
-    return lds_mode == 2 ? 24 : 32;
+    return lds_mode == 2 ? 24 : 48;
 }
 // Triangle scenes test deferred leaves once this many eighths of the
 // traversing lanes hold one (pathtrace.hip, leaf_step): later for an LDS
