@@ -77,6 +77,10 @@ def test_heightfield_and_grazing_rays(harness, tmp_path):
     # returns the sweep's result on every ray (checked above), and the coarser boxes cost few visits
     _, q_valid, q_nodes = out.stdout.splitlines()[2].split()
     assert int(q_valid) == 1 and float(q_nodes) < 1.1 * float(nodes)
+    # the default global-memory walk: octant layouts + distance pruning, the
+    # sweep's result on every ray (checked above) with fewer visits and triangle tests
+    _, p_nodes, p_tests = out.stdout.splitlines()[3].split()
+    assert float(p_nodes) < float(nodes) and float(p_tests) < float(tests)
 
 
 def test_shared_subobjects_duplicates_and_ties(harness, tmp_path):
