@@ -922,7 +922,7 @@ __device__ __forceinline__ void primary_state(const PrimaryRecord& r, TraceState
     }
 }
 
-constexpr uint32_t kPrimaryThreads = 1024;  // 16 units per workgroup, sharing one LDS image of the scene
+constexpr uint32_t kPrimaryThreads = 1024;  // default: 16 units per workgroup, sharing one LDS image of the scene
 
 // The tile queue, striped over the XCDs. One device-scope atomic counter on a
 // single address serialises at the memory side (~15 ns per claim measured:
@@ -1817,8 +1817,8 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
 // sphere or triangle, distance, index, object, facing) as one 16-B record; the
 // path kernel starts those paths from the record instead of tracing their first
 // segment. Everything after the first segment is unchanged.
-template <int kMode, bool kTris>
-__global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs ka) {
+template <int kMode, bool kTris, uint32_t kThreads, uint32_t kMinWaves>
+__global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t tid = threadIdx.x;
     // rt_set_timing: the pre-pass opens the launch's device span (the path kernel closes it)
@@ -1833,13 +1833,13 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
         RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
         uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
         float4* l_nodes = reinterpret_cast<float4*>(lds + ka.lds_nodes_offset);
-        for (uint32_t i = tid; i < ka.sphere_slot_count; i += kPrimaryThreads) {
+        for (uint32_t i = tid; i < ka.sphere_slot_count; i += kThreads) {
             l_sph[i] = ka.sphere_slots[i];
             l_orig[i] = ka.sphere_orig[i];
         }
-        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kPrimaryThreads) l_nodes[i] = ka.sphere_bvh[i];
+        for (uint32_t i = tid; i < 2u * ka.sphere_nodes; i += kThreads) l_nodes[i] = ka.sphere_bvh[i];
         if constexpr (kTris)
-            for (uint32_t i = tid; i < ka.object_count; i += kPrimaryThreads) l_obj[i] = ka.objects[i];
+            for (uint32_t i = tid; i < ka.object_count; i += kThreads) l_obj[i] = ka.objects[i];
         sv.sph = l_sph;
         sv.orig = l_orig;
         sv.nodes = l_nodes;
@@ -1848,13 +1848,13 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
     if constexpr (kMode == 2) {
         float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
         uint4* l_tp = reinterpret_cast<uint4*>(lds + ka.lds_tri_prims_offset);
-        for (uint32_t i = tid; i < 2u * ka.tri_nodes; i += kPrimaryThreads) l_tn[i] = ka.tri_bvh[i];
-        for (uint32_t i = tid; i < ka.tri_prim_count; i += kPrimaryThreads) l_tp[i] = ka.tri_prims[i];
+        for (uint32_t i = tid; i < 2u * ka.tri_nodes; i += kThreads) l_tn[i] = ka.tri_bvh[i];
+        for (uint32_t i = tid; i < ka.tri_prim_count; i += kThreads) l_tp[i] = ka.tri_prims[i];
         sv.tri_nodes = l_tn;
         sv.tri_prims = l_tp;
         if (ka.lds_sub_offset) {
             RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_sub_offset);
-            for (uint32_t i = tid; i < ka.sub_object_count; i += kPrimaryThreads) l_sub[i] = ka.sub_objects[i];
+            for (uint32_t i = tid; i < ka.sub_object_count; i += kThreads) l_sub[i] = ka.sub_objects[i];
             sv.sub = l_sub;
         }
     }
@@ -1866,7 +1866,7 @@ __global__ void __launch_bounds__(kPrimaryThreads) rt_primary_kernel(KernelArgs 
     __syncthreads();
 
     // one wave per (frame, local tile) unit, frame-major
-    const uint32_t unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (kPrimaryThreads / 64u) + (tid >> 6));
+    const uint32_t unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64u) + (tid >> 6));
     if (unit >= ka.queue_units) return;  // the whole wave
     const uint32_t frame = unit / ka.owned_tiles, local_tile = unit - frame * ka.owned_tiles;
     const uint32_t slot = tid & 63u;
@@ -1990,20 +1990,24 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 
 size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
 
-hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, hipStream_t stream) {
-    const uint32_t per = kPrimaryThreads / 64u;
+hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
+                             uint32_t min_waves, hipStream_t stream) {
+    if (threads == 0) threads = kPrimaryThreads;
+    const uint32_t per = threads / 64u;
     const uint32_t blocks = (ka.queue_units + per - 1u) / per;
     if (blocks == 0) return hipSuccess;
-#define RT_PRIMARY(M, TR)                                                                                      \
-    if (mode == M && tris == TR) {                                                                             \
+#define RT_PRIMARY(M, TR, T, W)                                                                                \
+    if (mode == M && tris == TR && threads == T && min_waves == W) {                                           \
         if (lds_bytes > 64u * 1024u) {                                                                         \
-            hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_primary_kernel<M, TR>));           \
+            hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_primary_kernel<M, TR, T, W>));     \
             if (e != hipSuccess) return e;                                                                     \
         }                                                                                                      \
-        hipLaunchKernelGGL((rt_primary_kernel<M, TR>), dim3(blocks), dim3(kPrimaryThreads), lds_bytes, stream, ka); \
+        hipLaunchKernelGGL((rt_primary_kernel<M, TR, T, W>), dim3(blocks), dim3(T), lds_bytes, stream, ka);   \
         return hipGetLastError();                                                                              \
     }
-    RT_PRIMARY(1, true) RT_PRIMARY(2, true)
+    // (mode, triangles, workgroup size, minimum waves per SIMD: 0 = the compiler's choice)
+    RT_PRIMARY(1, true, 64, 0) RT_PRIMARY(1, true, 128, 0) RT_PRIMARY(1, true, 256, 0) RT_PRIMARY(1, true, 256, 8)
+    RT_PRIMARY(1, true, 512, 0) RT_PRIMARY(1, true, 1024, 0) RT_PRIMARY(2, true, 1024, 0)
 #undef RT_PRIMARY
     return hipErrorInvalidValue;
 }

@@ -48,7 +48,8 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
-hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, hipStream_t stream);
+hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
+                             uint32_t min_waves, hipStream_t stream);
 size_t rt_brute_tile_bytes();
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
@@ -273,6 +274,13 @@ struct rt_ctx {
     bool brute = false;
     // coherent primary rays (rt_primary_kernel): RT_PRIMARY_PASS 1 / 0 force on / off, -1 by scene
     int primary_pass = -1;
+    // Workgroup size of the pre-pass where the accelerator is walked from global memory (modes
+    // 0/1): its packet walks are chains of dependent node loads, so resident waves are what
+    // count; at 1024 threads and ~69 VGPRs only one workgroup (16 waves) fits a CU, at 256 seven
+    // (28 waves): C5 5.69 -> 5.24 ms per frame (profiles/r03_ai/ab_c5_pthreads.jsonl).
+    // RT_PRIMARY_THREADS 64 / 128 / 256 / 512 / 1024, RT_PRIMARY_WAVES 8: at most 64 VGPRs (A/B).
+    uint32_t primary_threads = 256;
+    uint32_t primary_min_waves = 0;
     uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
     size_t primary_cap = 0;
     unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
@@ -761,6 +769,13 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->use_tri_wide = env[0] == '1';
         env = std::getenv("RT_PRIMARY_PASS");
         if (env) ctx->primary_pass = env[0] == '0' ? 0 : 1;
+        env = std::getenv("RT_PRIMARY_THREADS");
+        if (env) {
+            const uint32_t t = (uint32_t)std::strtoul(env, nullptr, 10);
+            if (t == 64u || t == 128u || t == 256u || t == 512u || t == 1024u) ctx->primary_threads = t;
+        }
+        env = std::getenv("RT_PRIMARY_WAVES");
+        if (env && env[0] == '8') ctx->primary_min_waves = 8;
         env = std::getenv("RT_BRUTE_FORCE");
         ctx->brute = env && env[0] == '1';
         env = std::getenv("RT_TRI_COMPACT");
@@ -1489,7 +1504,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         pka.primary = ctx->d_primary[pi];
         pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile), frame-major
         const size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
-        RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, S));
+        RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, mode == 2 ? 1024u : ctx->primary_threads,
+                                      mode == 2 ? 0u : ctx->primary_min_waves, S));
         ka.primary = pka.primary;
     }
     hipError_t e = rt_launch_pathtrace(ka, mode, tris, wide, ctx->occ_threads, lds_bytes, blocks, S);
