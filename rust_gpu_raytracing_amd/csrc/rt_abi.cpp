@@ -277,10 +277,11 @@ struct rt_ctx {
     // Workgroup size of the pre-pass where the accelerator is walked from global memory (modes
     // 0/1): its packet walks are chains of dependent node loads, so resident waves are what
     // count; at 1024 threads and ~69 VGPRs only one workgroup (16 waves) fits a CU, at 256 seven
-    // (28 waves): C5 5.69 -> 5.24 ms per frame (profiles/r03_ai/ab_c5_pthreads.jsonl).
-    // RT_PRIMARY_THREADS 64 / 128 / 256 / 512 / 1024, RT_PRIMARY_WAVES 8: at most 64 VGPRs (A/B).
+    // (28 waves): C5 5.69 -> 5.24 ms per frame (profiles/r03_ai/ab_c5_pthreads.jsonl); held to
+    // 64 VGPRs, eight waves per SIMD (32 per CU): 5.04 ms (profiles/r03_aj/ab_c5_pthreads.jsonl).
+    // RT_PRIMARY_THREADS 64 / 128 / 256 / 512 / 1024 and RT_PRIMARY_WAVES 0 / 8 (A/B switches).
     uint32_t primary_threads = 256;
-    uint32_t primary_min_waves = 0;
+    uint32_t primary_min_waves = 8;
     uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
     size_t primary_cap = 0;
     unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
@@ -775,7 +776,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
             if (t == 64u || t == 128u || t == 256u || t == 512u || t == 1024u) ctx->primary_threads = t;
         }
         env = std::getenv("RT_PRIMARY_WAVES");
-        if (env && env[0] == '8') ctx->primary_min_waves = 8;
+        if (env) ctx->primary_min_waves = env[0] == '8' ? 8u : 0u;
+        if (ctx->primary_threads != 256u) ctx->primary_min_waves = 0;  // the 64-VGPR variant is built at 256
         env = std::getenv("RT_BRUTE_FORCE");
         ctx->brute = env && env[0] == '1';
         env = std::getenv("RT_TRI_COMPACT");
