@@ -1868,7 +1868,12 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
     // one wave per (frame, local tile) unit, frame-major
     const uint32_t unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64u) + (tid >> 6));
     if (unit >= ka.queue_units) return;  // the whole wave
-    const uint32_t frame = unit / ka.owned_tiles, local_tile = unit - frame * ka.owned_tiles;
+    // unit -> (frame, tile): frame-major, or tile-major (a tile's frames on consecutive waves of
+    // a workgroup: their packets walk nearly the same nodes, so the later ones find them in the
+    // CU's caches)
+    const uint32_t n_frames = ka.queue_units / ka.owned_tiles;
+    const uint32_t frame = ka.primary_tile_major ? unit % n_frames : unit / ka.owned_tiles;
+    const uint32_t local_tile = ka.primary_tile_major ? unit / n_frames : unit - frame * ka.owned_tiles;
     const uint32_t slot = tid & 63u;
     const uint32_t gt = local_tile * ka.world_size + ka.rank;
     const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);

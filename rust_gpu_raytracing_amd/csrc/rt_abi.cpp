@@ -282,6 +282,7 @@ struct rt_ctx {
     // RT_PRIMARY_THREADS 64 / 128 / 256 / 512 / 1024 and RT_PRIMARY_WAVES 0 / 8 (A/B switches).
     uint32_t primary_threads = 256;
     uint32_t primary_min_waves = 8;
+    bool primary_tile_major = false;  // RT_PRIMARY_TILE_MAJOR=1: a tile's frames on consecutive pre-pass waves (A/B)
     uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
     size_t primary_cap = 0;
     unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
@@ -775,6 +776,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
             const uint32_t t = (uint32_t)std::strtoul(env, nullptr, 10);
             if (t == 64u || t == 128u || t == 256u || t == 512u || t == 1024u) ctx->primary_threads = t;
         }
+        env = std::getenv("RT_PRIMARY_TILE_MAJOR");
+        if (env) ctx->primary_tile_major = env[0] == '1';
         env = std::getenv("RT_PRIMARY_WAVES");
         if (env) ctx->primary_min_waves = env[0] == '8' ? 8u : 0u;
         if (ctx->primary_threads != 256u) ctx->primary_min_waves = 0;  // the 64-VGPR variant is built at 256
@@ -1504,7 +1507,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         KernelArgs pka = ka;
         pka.primary = ctx->d_primary[pi];
-        pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile), frame-major
+        pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile)
+        pka.primary_tile_major = ctx->primary_tile_major ? 1u : 0u;
         const size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
         RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, mode == 2 ? 1024u : ctx->primary_threads,
                                       mode == 2 ? 0u : ctx->primary_min_waves, S));

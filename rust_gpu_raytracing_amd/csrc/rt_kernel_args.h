@@ -184,6 +184,7 @@ struct KernelArgs {
     // coherent primary rays (rt_primary_kernel): one 16-B trace result per (frame, sample, owned
     // pixel), indexed like frame_light; the path kernel starts its paths from them. Null: off.
     uint4* __restrict__ primary;
+    uint32_t primary_tile_major;  // the pre-pass takes its (frame, tile) units tile-major (1) or frame-major
     // brute-force launches (rt_brute_kernel): bytes of sub-object records streamed through LDS
     unsigned long long* __restrict__ stream_bytes;
     uint32_t texture_width;

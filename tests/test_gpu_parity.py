@@ -769,6 +769,10 @@ def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
     ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 2, 1, {"RT_FRAME_PARALLEL": "0", "RT_PRIMARY_PASS": "1"}),
     ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 1, 1, {"RT_PRIMARY_PASS": "1", "RT_LDS_MODE": "1"}),
     ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 2, 1, {}),       # default: on (accelerator in global memory)
+    # pre-pass workgroup sizes and unit orders (the default is 256 threads held to 64 VGPRs)
+    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 3, 1, {"RT_PRIMARY_THREADS": "64", "RT_PRIMARY_TILE_MAJOR": "1"}),
+    ("c5_heightfield", dict(nx=200, nz=100), 2, 1, 3, 2, {"RT_PRIMARY_THREADS": "1024", "RT_PRIMARY_TILE_MAJOR": "1"}),
+    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 3, 1, {"RT_PRIMARY_WAVES": "0"}),
 ])
 def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumulate, batch, world, env):
     """rt_primary_kernel traces every path's first segment as 8x8 packets (wave-uniform
