@@ -282,7 +282,9 @@ struct rt_ctx {
     // RT_PRIMARY_THREADS 64 / 128 / 256 / 512 / 1024 and RT_PRIMARY_WAVES 0 / 8 (A/B switches).
     uint32_t primary_threads = 256;
     uint32_t primary_min_waves = 8;
-    bool primary_tile_major = false;  // RT_PRIMARY_TILE_MAJOR=1: a tile's frames on consecutive pre-pass waves (A/B)
+    // a tile's frames on consecutive pre-pass waves, whose packets walk nearly the same nodes:
+    // C5 5.02 -> 4.93 ms (profiles/r03_al/ab_c5_ptm.jsonl); RT_PRIMARY_TILE_MAJOR=0: frame-major (A/B)
+    bool primary_tile_major = true;
     uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
     size_t primary_cap = 0;
     unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
