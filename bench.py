@@ -293,12 +293,31 @@ def main() -> int:
             r.compute_frame(bounces)
             if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
                 log(f"step {i + 1}/{args.steps}")
+        t_gather_in_region = 0.0
         if gathered:
             # the frame assembled on rank 0 (pack -> RCCL gather -> unpack), stream-ordered
-            # after the last frame; the closing barrier + sync waits for it
-            gather_frame(r, 0, args.gather, sync=False)
+            # after the last frame; the closing barrier + sync waits for it. The gather's
+            # share of the timed region is measured in place (events on the renderer's
+            # stream around it; gloo: the host-side span after the frames are done), so
+            # render time = timed region - that share is positive by construction.
+            r.flush()
+            if backend == "nccl":
+                stream = torch.cuda.ExternalStream(r.stream_handle, device=torch.device("cuda", device))
+                ev_frames = torch.cuda.Event(enable_timing=True)
+                ev_gather = torch.cuda.Event(enable_timing=True)
+                ev_frames.record(stream)
+                gather_frame(r, 0, args.gather, sync=False)
+                ev_gather.record(stream)
+            else:
+                r.synchronize()
+                t_frames = time.perf_counter()
+                gather_frame(r, 0, args.gather, sync=False)
+                r.synchronize()
+                t_gather_in_region = time.perf_counter() - t_frames
         barrier_sync()
         t_total = time.perf_counter() - t0
+        if gathered and backend == "nccl":
+            t_gather_in_region = ev_frames.elapsed_time(ev_gather) / 1e3
         r.set_timing(False)  # (reads the launch events back: outside the timed region)
         t_gather = t_gather_accum = t_gather_image = 0.0
         if gathered:
@@ -316,7 +335,10 @@ def main() -> int:
             t_gather_accum = timed_gather("accumulation")
             t_gather_image = timed_gather("image")
             t_gather = t_gather_image if args.gather == "image" else t_gather_accum
-        t_render = t_total - t_gather
+        # render time: the timed region minus the gather it contains, measured in that
+        # region (not the separately timed gathers above, which can take longer)
+        t_render = t_total - t_gather_in_region
+        assert 0.0 < t_render <= t_total, (t_render, t_total, t_gather_in_region)
         res = dict(r=r, scene=scene, bounces=bounces, width=width, height=height, rays=r.ray_count(),
                    streamed=r.streamed_bytes(),
                    settle_frames=settle_frames,
@@ -324,6 +346,7 @@ def main() -> int:
                    passes=r.last_launch_passes(),
                    timing=r.dispatch_time_total(), resolve_timing=r.resolve_time_total(),
                    owned_px=r.owned_pixel_count())
+        res["t_gather_in_region"] = t_gather_in_region
         stats = torch.tensor([t_total, t_render, t_gather, t_gather_accum, t_gather_image, float(res["rays"])],
                              dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         if dist_run:
@@ -370,6 +393,8 @@ def main() -> int:
         t0 = time.perf_counter()
         for _ in range(args.steps):
             g.compute_frame(bounces)
+        g.synchronize()  # the frames done on every device: the render share of the timed region
+        t_frames = time.perf_counter() - t0
         g.gather(0, args.gather)
         g.synchronize()
         t_total = time.perf_counter() - t0
@@ -382,11 +407,11 @@ def main() -> int:
         v0 = views[0]
         rays_total = g.ray_count()
         return dict(r=g, scene=scene, bounces=bounces, width=args.width, height=args.height,
-                    rays=rays_total / n, settle_frames=settle_frames, t_render=t_total - t_gather,
+                    rays=rays_total / n, settle_frames=settle_frames, t_render=t_frames,
                     t_gather=t_gather, gathered=True, launch=v0.launch_config(), passes=v0.last_launch_passes(),
                     timing=v0.dispatch_time_total(),
                     resolve_timing=v0.resolve_time_total(), owned_px=v0.owned_pixel_count(),
-                    t_total_max=t_total, t_render_max=t_total - t_gather, t_gather_max=t_gather,
+                    t_total_max=t_total, t_render_max=t_frames, t_gather_max=t_gather,
                     t_gather_accum_max=t_gather if args.gather == "accumulation" else 0.0,
                     t_gather_image_max=t_gather if args.gather == "image" else 0.0, rays_total=float(rays_total))
 

@@ -108,23 +108,61 @@ def test_gpu_full_frame_baseline_size(gpu, oracle_lib, config):
     assert_same(acc, out, n, *oracle_frames(oracle_lib, scene, bounces, 2, rays))
 
 
+_C5_SAMPLE = {}
+
+
+def _c5_full_size_oracle_sample(oracle_lib):
+    """C5 at its BASELINE size with the oracle's result on 20,000 random pixels of 2 frames
+    (the oracle sweeps all 142,858 sub-objects per ray, ~10^4 rays/s per thread); built once
+    and shared by the accelerator and brute-force tests."""
+    if not _C5_SAMPLE:
+        scene, bounces = build_config("c5_heightfield")
+        rays = scene.camera.recalculate_ray_directions()
+        o = oracle_lib.Oracle(scene, camera_rays=rays)
+        rng = np.random.default_rng(11)
+        pix = rng.choice(1920 * 1080, 20000, replace=False).astype(np.uint32)
+        a = None
+        for k in (1, 2):
+            a, o_out, _ = o.render_pixels(scene.params(accumulation_index=k), bounces, pix, accum_in=a)
+        _C5_SAMPLE.update(scene=scene, bounces=bounces, rays=rays, pix=pix, acc=a, out=o_out)
+    return _C5_SAMPLE
+
+
+def _check_c5_sample(smp, acc, out):
+    g_acc = acc.reshape(-1, 4)[smp["pix"]]
+    g_out = out.reshape(-1)[smp["pix"]]
+    assert rms_per_channel(g_acc, smp["acc"]).max() <= RMS_TOL
+    assert np.array_equal(g_out, smp["out"])
+    assert np.array_equal(g_acc.view(np.uint32), smp["acc"].view(np.uint32))
+
+
 def test_gpu_full_size_sampled_c5(gpu, oracle_lib):
-    """C5 (1M triangles, 1920x1080x8): the oracle sweeps all 142,858 sub-objects per ray
-    (~10^4 rays/s per thread), so 20,000 random pixels of 2 frames are checked."""
-    scene, bounces = build_config("c5_heightfield")
-    rays = scene.camera.recalculate_ray_directions()
-    acc, out, _ = gpu_render(scene, bounces, 2, rays=rays)
-    o = oracle_lib.Oracle(scene, camera_rays=rays)
-    rng = np.random.default_rng(11)
-    pix = rng.choice(1920 * 1080, 20000, replace=False).astype(np.uint32)
-    a = None
-    for k in (1, 2):
-        a, o_out, _ = o.render_pixels(scene.params(accumulation_index=k), bounces, pix, accum_in=a)
-    g_acc = acc.reshape(-1, 4)[pix]
-    g_out = out.reshape(-1)[pix]
-    assert rms_per_channel(g_acc, a).max() <= RMS_TOL
-    assert np.array_equal(g_out, o_out)
-    assert np.array_equal(g_acc.view(np.uint32), a.view(np.uint32))
+    """C5 (1M triangles, 1920x1080x8) on the default path: 20,000 random pixels of 2
+    frames against the oracle."""
+    smp = _c5_full_size_oracle_sample(oracle_lib)
+    acc, out, _ = gpu_render(smp["scene"], smp["bounces"], 2, rays=smp["rays"])
+    _check_c5_sample(smp, acc, out)
+
+
+def test_gpu_full_size_brute_force_c5(gpu, oracle_lib):
+    """BASELINE config 5 as named -- the 1,000,000-triangle mesh at 1920x1080x8 in the
+    brute-force LDS-tiled mode (rt_brute_kernel: the reference's own object -> sub-object
+    -> triangle sweep for every ray): the oracle's 20,000 sampled pixels, and every pixel
+    of both frames bit-identical to the accelerated default path."""
+    smp = _c5_full_size_oracle_sample(oracle_lib)
+    scene, bounces, rays = smp["scene"], smp["bounces"], smp["rays"]
+    with Renderer(scene, camera_rays=rays, frame_batch=2) as r:
+        r.set_brute_force(True)
+        for _ in range(2):
+            r.compute_frame(bounces)
+        acc, out, n = r.read_accumulation(), r.read_output(), r.ray_count()
+        assert r.streamed_bytes() > 0
+        assert "brute" in r.last_launch_passes()
+    _check_c5_sample(smp, acc, out)
+    acc_d, out_d, n_d = gpu_render(scene, bounces, 2, rays=rays)
+    assert n == n_d
+    assert np.array_equal(out, out_d)
+    assert np.array_equal(acc.view(np.uint32), acc_d.view(np.uint32))
 
 
 def test_gpu_reference_bounce_default(gpu, oracle_lib):
