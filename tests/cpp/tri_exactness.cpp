@@ -20,6 +20,7 @@
 
 #include "rt_bvh_slab.h"
 #include "sphere_bvh.h"
+#include "tri_cone.h"
 #include "tri_qnode.h"
 #include "tri_wide.h"
 
@@ -97,6 +98,13 @@ static const std::vector<SphereBvhNode>* g_oct = nullptr;
 static const std::vector<uint32_t>* g_qoct = nullptr;
 static float g_prune = 0.0f;
 static long g_prune_nodes = 0, g_prune_tests = 0;
+// certified pruning (tri_cone.h): cone records in base-node order, and per layout position
+// its base node (order_bvh_by_octant's src)
+static const std::vector<TriCone>* g_cones = nullptr;
+static const std::vector<uint32_t>* g_src = nullptr;
+static bool g_heur_count = false;
+static long g_heur_miss = 0;
+static long g_exact_nodes = 0, g_exact_tests = 0, g_exact_checks = 0, g_exact_pruned = 0;
 
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
@@ -117,6 +125,7 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
         node = ((ib[0] >> 31) | ((ib[1] >> 31) << 1) | ((ib[2] >> 31) << 2)) * (uint32_t)A.nodes.size();
     }
     float limit = INFINITY;
+    const TriConeRay tcr = tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z);
     const float sig = 0x1p-10f * (std::sqrt(dot(o, o)) + A.extent) * (1.0f / std::sqrt(dot(d, d)) * 1.001f);
     while (node < n) {
         SphereBvhNode nd = NS[node];
@@ -131,9 +140,22 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
         } else if (!g_lazy) {
             g_nodes++;
         }
+        if (g_cones) g_exact_nodes++;
         float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
         slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
         bool hit = nt <= ft && ft >= 0.0f && nt <= limit;
+        if (g_cones && hit && best != F32_MAX_ && nt > best) {
+            // certified pruning: the node's per-axis entries (the slab test's), then tri_cone_prunes
+            g_exact_checks++;
+            const float t1x = fminf(fmaf(nd.bmin[0], sr.ix, sr.lx), fmaf(nd.bmax[0], sr.ix, sr.hx));
+            const float t1y = fminf(fmaf(nd.bmin[1], sr.iy, sr.ly), fmaf(nd.bmax[1], sr.iy, sr.hy));
+            const float t1z = fminf(fmaf(nd.bmin[2], sr.iz, sr.lz), fmaf(nd.bmax[2], sr.iz, sr.hz));
+            const TriCone& cone = (*g_cones)[g_src ? (*g_src)[node] : node];
+            if (tri_cone_prunes(cone, tcr, best, t1x, t1y, t1z, fabsf(sr.ix), fabsf(sr.iy), fabsf(sr.iz))) {
+                hit = false;
+                g_exact_pruned++;
+            }
+        }
         if (hit && nd.leaf != kSphereBvhInternal) {
             const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
             const rt_object_info& OB = ob[p.object];
@@ -150,6 +172,7 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
                 for (uint32_t j = 0; j < count; j++) {
                     if (!g_q && !g_lazy) g_tests++;
                     if (g_prune != 0.0f) g_prune_tests++;
+                    if (g_cones) g_exact_tests++;
                     uint32_t ti = first + j, seq = p.seq_base + j;
                     const rt_scene_triangle& t = tr[ti];
                     V cn = ld(t.calc_normal);
@@ -291,6 +314,7 @@ int main(int argc, char** argv) {
     auto tr = load<rt_scene_triangle>(argv[3]);
     auto rays = load<float>(argv[4]);
     float scale = argc > 5 ? (float)atof(argv[5]) : 1.0e-5f;
+    g_heur_count = getenv("TRI_HEUR_COUNT") != nullptr;
     TriangleAccel A;
     build_triangle_accel(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), &A);
     // the wide accelerator, with compact leaves from the records in the kernel's 64-B layout
@@ -321,9 +345,38 @@ int main(int argc, char** argv) {
                 }
         }
     }
+    // cone records (tri_cone.h), children before parents (reverse pre-order)
+    std::vector<TriCone> cones(A.nodes.size());
+    {
+        std::vector<tricone::Acc> acc(A.nodes.size());
+        for (size_t ii = A.nodes.size(); ii-- > 0;) {
+            const SphereBvhNode& nd = A.nodes[ii];
+            tricone::Acc c = tricone::acc_empty();
+            if (nd.leaf != kSphereBvhInternal) {
+                const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
+                const rt_sub_object_info& sbi = sb[p.sub];
+                float lo[3], hi[3];
+                for (int k = 0; k < 3; k++) {
+                    lo[k] = fminf(sbi.min_bounds[k], sbi.max_bounds[k]);
+                    hi[k] = fmaxf(sbi.min_bounds[k], sbi.max_bounds[k]);
+                }
+                for (uint32_t j = 0; j < sbi.triangle_count; j++) {
+                    const rt_scene_triangle& t = tr[sbi.first_triangle_index + j];
+                    tricone::acc_add_triangle(c, t.a, t.edge_ab, t.edge_ac, t.calc_normal, lo, hi);
+                }
+                if (c.n == 0u) c.valid = false;
+            } else {
+                c = tricone::acc_from_record(cones[ii + 1]);
+                tricone::acc_add_acc(c, tricone::acc_from_record(cones[A.nodes[ii + 1].skip]));
+            }
+            cones[ii] = tricone::acc_record(c);
+        }
+    }
+    long narrow = 0;
+    for (const TriCone& c : cones) narrow += (c.flags & kTriConePrunable) == kTriConePrunable;
     std::vector<SphereBvhNode> oct;
-    std::vector<uint32_t> qoct;
-    order_bvh_by_octant(A.nodes, &oct, false);
+    std::vector<uint32_t> qoct, src;
+    order_bvh_by_octant(A.nodes, &oct, false, &src);
     if (g_grid.valid) {
         qoct.resize(4 * oct.size());
         for (size_t i = 0; i < oct.size(); i++) {
@@ -351,18 +404,31 @@ int main(int argc, char** argv) {
         g_qoct = g_grid.valid ? &qoct : nullptr;
         g_prune = 1.0f / 64.0f;
         Res h = accel(A, ob, sb, tr, o, d, scale);
+        if (g_heur_count) {  // TRI_HEUR_COUNT: the heuristic slack's misses are counted, not fatal
+            uint32_t ta, th;
+            memcpy(&ta, &a.t, 4);
+            memcpy(&th, &h.t, 4);
+            if (ta != th || a.tri != h.tri || a.obj != h.obj || a.front != h.front) g_heur_miss++;
+            h = a;
+        }
         g_prune = 0.0f;
+        // the certified walk (tri_cone.h) over the same layouts
+        g_cones = &cones;
+        g_src = oct.empty() ? nullptr : &src;
+        Res x = accel(A, ob, sb, tr, o, d, scale);
+        g_cones = nullptr;
+        g_src = nullptr;
         g_oct = nullptr;
         g_qoct = nullptr;
         g_q = nullptr;
         g_lazy = false;
-        for (const Res* x : {&b, &c, &e, &f, &h}) {
+        for (const Res* x : {&b, &c, &e, &f, &h, &x}) {
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
             memcpy(&tb, &x->t, 4);
             if (ta != tb || a.tri != x->tri || a.obj != x->obj || a.front != x->front) {
                 printf("MISMATCH (%s) ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n",
-                       x == &b ? "binary" : x == &c ? "wide" : x == &e ? "qnodes" : x == &f ? "qnodes+lazy" : "octants+prune", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
+                       x == &b ? "binary" : x == &c ? "wide" : x == &e ? "qnodes" : x == &f ? "qnodes+lazy" : x == &h ? "octants+prune" : "certified", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
                        x->t);
                 return 1;
             }
@@ -376,5 +442,8 @@ int main(int argc, char** argv) {
            w_max_stack);
     printf("qnodes %d %.2f\n", g_grid.valid ? 1 : 0, (double)g_qnodes / n);
     printf("prune %.2f %.2f\n", (double)g_prune_nodes / n, (double)g_prune_tests / n);
+    printf("certified %.2f %.2f %.2f %.2f %ld %zu\n", (double)g_exact_nodes / n, (double)g_exact_tests / n,
+           (double)g_exact_checks / n, (double)g_exact_pruned / n, narrow, cones.size());
+    printf("heuristic_misses %ld\n", g_heur_miss);
     return 0;
 }
