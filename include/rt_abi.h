@@ -295,17 +295,21 @@ RT_API int rt_reset_ray_count(rt_ctx* ctx);
 RT_API int rt_set_brute_force(rt_ctx* ctx, int enable);
 RT_API int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out);
 
-/* Distance pruning of the triangle walk (new; ABI 8). The reference sweeps every
- * object -> sub-object -> triangle (compute_shader.wgsl:422-517); the accelerator
- * replaces the sweep by a walk that culls boxes the ray misses. With enable != 0
- * (the default) the walk also skips boxes entered beyond the best triangle hit so
- * far plus a slack of 1/64 of it, visiting the direction-ordered
- * layout of the ray's octant first. The slack covers the f32 error of the
- * reference's triangle test except for triangles within ~1e-4 rad of parallel to
- * the ray whose plane passes within ~1e-4 x distance of its origin, where that
- * test's own result is rounding noise; 0 = box culling only (exact by
- * construction, as before ABI 8). Synchronous. */
-RT_API int rt_set_triangle_pruning(rt_ctx* ctx, int enable);
+/* Distance pruning of the triangle walk (new; ABI 8, modes since ABI 9). The
+ * reference sweeps every object -> sub-object -> triangle
+ * (compute_shader.wgsl:422-517); the accelerator replaces the sweep by a walk that
+ * culls boxes the ray misses, which is exact by construction.
+ * mode 1 (the default): certified pruning -- once a triangle is hit at t, a node is
+ * also skipped when its box, inflated by a derived bound on the f32 error of the
+ * reference's triangle test over the node's triangles (a normal cone per node plus
+ * two per-record coefficients, rt_tri_cone.h), is entered beyond t; exact by
+ * construction. 0: box culling only. 2: the relative slack of
+ * ABI 8 (skip boxes entered beyond t * (1 + 1/64) + 2^-10 (|o| + extent) / |d|):
+ * faster on scenes without coherent normals, NOT exact -- rays nearly in a
+ * triangle's plane near their origin can get another triangle than the sweep's
+ * (tests/test_tri_accel_cpu.py builds such rays). Walks of the octant-ordered
+ * layouts visit near boxes first in every mode. Synchronous. */
+RT_API int rt_set_triangle_pruning(rt_ctx* ctx, int mode);
 
 /* Tile claim order (new; the reference dispatches a plain grid,
  * src/renderer.rs:238-249). 0 = tile index order. 1 = cost-ordered (the

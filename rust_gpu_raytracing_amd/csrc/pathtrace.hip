@@ -260,17 +260,35 @@ __device__ __forceinline__ float prune_limit(const TraceState& ts) {
     return fmin_nn(ts.sph.t, ts.tri.t) * 1.00001f + ts.slack;
 }
 
-// Distance pruning of the triangle walk (ka.tri_prune = rho, 0 = off): once a
-// triangle is hit at t, a box whose inflated entry lies beyond t * (1 + rho) + 2^-10 (|o| +
-// extent) / |d| is skipped. The slack covers the f32 error of the reference's distance and
-// barycentrics for every triangle not within ~1e-4 rad of parallel to the ray (where that
-// error grows as 1/cos), so such a box holds no triangle the reference would accept closer.
+// The round-3 relative-slack pruning (ka.tri_prune_mode 2, opt-in; ka.tri_prune = rho, else 0):
+// once a triangle is hit at t, a box whose inflated entry lies beyond t * (1 + rho) + 2^-10
+// (|o| + extent) / |d| is skipped. The slack covers the f32 error of the reference's distance
+// and barycentrics only for triangles well away from parallel to the ray (that error grows
+// as 1/cos): NOT exact -- rays nearly in a triangle's plane close to their origin can lose the
+// sweep's winner (tests/test_tri_accel_cpu.py). The default is the certified test below.
 constexpr float kTriPruneAbs = 0x1p-10f;
 __device__ __forceinline__ float tri_limit(const SceneView& sv, const KernelArgs& ka, f3 o, const TraceState& ts) {
     if (ka.tri_prune == 0.0f || ts.tri.t == kF32Max) return __builtin_inff();
     const float r = sqrt_up(dot(o, o));
     const float sig = kTriPruneAbs * (r + sv.tri_extent) * (__builtin_amdgcn_rsqf(ts.a2 * 0.5f) * 1.001f);
     return ts.tri.t * (1.0f + ka.tri_prune) + sig;
+}
+
+// Certified distance pruning (ka.tri_prune_mode 1; tri_cone.h): a triangle
+// node whose box the walk enters beyond the best hit tb is skipped only when the node's cone
+// record proves that no triangle below it can pass the reference's test (:449-481) at a
+// distance <= tb. The per-axis entries are the culling slab test's own (rt_bvh_slab.h) on
+// the box as the walk decoded it.
+__device__ __forceinline__ bool tri_node_beyond(const KernelArgs& ka, uint32_t node, const SlabRay& sr, f3 o, f3 d,
+                                                float tb, float4 lo, float4 hi) {
+    const float4* rec = reinterpret_cast<const float4*>(ka.tri_cones + node);
+    const float4 c0 = rec[0], c1 = rec[1];
+    const TriCone c{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, __float_as_uint(c1.w)};
+    const float t1x = fminf(fmaf(lo.x, sr.ix, sr.lx), fmaf(hi.x, sr.ix, sr.hx));
+    const float t1y = fminf(fmaf(lo.y, sr.iy, sr.ly), fmaf(hi.y, sr.iy, sr.hy));
+    const float t1z = fminf(fmaf(lo.z, sr.iz, sr.lz), fmaf(hi.z, sr.iz, sr.hz));
+    return tri_cone_prunes(c, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), tb, t1x, t1y, t1z, fabsf(sr.ix),
+                           fabsf(sr.iy), fabsf(sr.iz));
 }
 
 // Slab constants and depth bounds of a BVH walk. The triangle walk culls by
@@ -611,7 +629,12 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     // side also not beyond the best sphere or the triangle hit (a sphere wins
     // only when strictly closer, :347); ts.slack / ts.limit are 0 / inf on the
     // triangle side
-    const bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
+    bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
+    if constexpr (kTris) {
+        // certified pruning: only for a box entered beyond the best triangle hit
+        if (tri && hit && ka.tri_prune_mode == 1u && near_t > ts.tri.t && ts.tri.t != kF32Max)
+            hit = !tri_node_beyond(ka, ts.node, ts.slab, o, d, ts.tri.t, lo, hi);
+    }
     const uint32_t leaf = __float_as_uint(hi.w);
     const bool at_leaf = hit && leaf != 0xffffffffu;
     if (at_leaf && !kDeferLeaves<kTris>) {
@@ -1899,7 +1922,9 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
                     const float4 lo = sv.tri_nodes[2u * node], hi = sv.tri_nodes[2u * node + 1u];
                     float near_t, far_t;
                     slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
-                    const bool hit = valid && near_t <= far_t && far_t >= 0.0f && near_t <= ts.limit;
+                    bool hit = valid && near_t <= far_t && far_t >= 0.0f && near_t <= ts.limit;
+                    if (hit && ka.tri_prune_mode == 1u && near_t > ts.tri.t && ts.tri.t != kF32Max)
+                        hit = !tri_node_beyond(ka, node, ts.slab, o, d, ts.tri.t, lo, hi);  // certified pruning
                     const bool any = __ballot(hit) != 0;
                     const uint32_t leaf = __float_as_uint(hi.w);
                     if (any && leaf != 0xffffffffu && hit) {

@@ -22,6 +22,7 @@
 #include "rt_kernel_args.h"
 #include "rt_scene_math.h"
 #include "sphere_bvh.h"
+#include "tri_cone.h"
 #include "tri_qnode.h"
 #include "tri_wide.h"
 
@@ -47,6 +48,10 @@ hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, 
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
+hipError_t rt_launch_tri_cones(const SphereBvhNode* nodes, uint32_t n, const SubObjectPrim* prims,
+                               const RtSubObject* subs, const RtTriangleHot* tris, uint32_t n_tri,
+                               const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels,
+                               TriCone* cones, const uint32_t* src8, TriCone* cones8, hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
@@ -256,8 +261,17 @@ struct rt_ctx {
     size_t tri_src8_cap = 0, tri_skip8_cap = 0, tri_bvh8_cap = 0;
     bool tri_octants_built = false;  // d_tri_src8 / d_tri_skip8 describe the current tree
     // rt_set_triangle_pruning / RT_TRI_PRUNE: distance pruning of the triangle walk (DESIGN.md
-    // §5.3c): relative slack rho of the limit best * (1 + rho) + sigma, 0 = box culling only
-    float tri_prune = kTriPruneRho;
+    // §5.3c): 1 = certified by the cone records (default, exact), 0 = box culling only,
+    // 2 = the round-3 relative slack (not exact)
+    int tri_prune_mode = 1;
+    // certified pruning records (tri_cone.h): per node of the base accelerator, and per position
+    // of the direction-ordered layouts; rebuilt on the device after any change of the
+    // accelerator or the triangles
+    TriCone* d_tri_cones = nullptr;
+    TriCone* d_tri_cones8 = nullptr;
+    size_t tri_cones_cap = 0, tri_cones8_cap = 0;
+    bool cones_dirty = true;
+    bool derived_cone_octants = false;
     // the 4-wide accelerator (tri_wide.h), RT_TRI_WIDE=1 (A/B switch): measured slower than the
     // binary one on C3-C5, so off by default
     bool use_tri_wide = false;
@@ -556,6 +570,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         (rc = upload_raw(ctx, ctx->d_tri_prims, acc.prims.data(), pb)))
         return rc;
     ctx->qnodes_dirty = true;
+    ctx->cones_dirty = true;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
     ctx->tri_prim_count = (uint32_t)acc.prims.size();
     ctx->tri_octants_built = false;
@@ -603,6 +618,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
 
 int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     if (n == 0) return RT_OK;
+    ctx->cones_dirty = true;
     void* p;
     int rc = staging(ctx, (size_t)n * sizeof(RtTriangleHot), &p);
     if (rc) return rc;
@@ -816,7 +832,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         env = std::getenv("RT_TRI_OCTANTS");
         if (env) ctx->use_tri_octants = env[0] != '0';
         env = std::getenv("RT_TRI_PRUNE");
-        if (env) ctx->tri_prune = env[0] == '0' ? 0.0f : kTriPruneRho;
+        if (env) ctx->tri_prune_mode = env[0] == '0' ? 0 : env[0] == '2' ? 2 : 1;
         env = std::getenv("RT_TRI_QNODES");
         if (env) ctx->use_qnodes = env[0] != '0';
         env = std::getenv("RT_STAGE_SUBS");
@@ -899,7 +915,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
                     ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
-                    ctx->d_tri_skip8, ctx->d_tri_bvh8};
+                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_cones, ctx->d_tri_cones8};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1383,7 +1399,44 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ka.tri_nodes = n_out;
         }
     }
-    ka.tri_prune = (tris && !wide && ka.tri_accel) ? ctx->tri_prune : 0.0f;
+    // distance pruning of the binary walk: certified (the cone records,
+    // rebuilt on the device after any change), or the round-3 relative slack, or none
+    ka.tri_prune_mode = (tris && !wide && ka.tri_accel && ka.tri_nodes != 0) ? (uint32_t)ctx->tri_prune_mode : 0u;
+    ka.tri_prune = ka.tri_prune_mode == 2u ? kTriPruneRho : 0.0f;
+    ka.tri_cones = nullptr;
+    if (ka.tri_prune_mode == 1u) {
+        const uint32_t n_base = octants ? ka.tri_octant_stride : ka.tri_nodes;
+        const size_t b1 = (size_t)n_base * sizeof(TriCone), b8 = octants ? 8u * b1 : 0u;
+        if (ctx->tri_cones_cap < b1 || ctx->tri_cones8_cap < b8) {  // (re)allocate: nothing may still read them
+            RT_HIP(ctx, join_aux(ctx));
+            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->tri_cones_cap < b1) {
+                if (ctx->d_tri_cones) RT_HIP(ctx, hipFree(ctx->d_tri_cones));
+                ctx->d_tri_cones = nullptr;
+                ctx->tri_cones_cap = 0;
+                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_cones), b1));
+                ctx->tri_cones_cap = b1;
+            }
+            if (ctx->tri_cones8_cap < b8) {
+                if (ctx->d_tri_cones8) RT_HIP(ctx, hipFree(ctx->d_tri_cones8));
+                ctx->d_tri_cones8 = nullptr;
+                ctx->tri_cones8_cap = 0;
+                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_cones8), b8));
+                ctx->tri_cones8_cap = b8;
+            }
+            ctx->cones_dirty = true;
+        }
+        if (ctx->cones_dirty || ctx->derived_cone_octants != octants) {
+            RT_HIP(ctx, rt_launch_tri_cones(ctx->d_tri_bvh, n_base, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri,
+                                            ctx->n_tri_dev, ctx->d_tri_order, ctx->d_tri_level_off, ctx->tri_levels,
+                                            ctx->d_tri_cones, octants ? ctx->d_tri_src8 : nullptr,
+                                            ctx->d_tri_cones8, ctx->stream));
+            ctx->cones_dirty = false;
+            ctx->derived_cone_octants = octants;
+            ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
+        }
+        ka.tri_cones = octants ? ctx->d_tri_cones8 : ctx->d_tri_cones;
+    }
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
@@ -1707,6 +1760,7 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
                                     ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
         ctx->qnodes_dirty = true;
     }
+    ctx->cones_dirty = true;  // the triangles changed
     return RT_OK;
 }
 
@@ -1779,9 +1833,10 @@ int rt_set_brute_force(rt_ctx* ctx, int enable) {
     return RT_OK;
 }
 
-int rt_set_triangle_pruning(rt_ctx* ctx, int enable) {
+int rt_set_triangle_pruning(rt_ctx* ctx, int mode) {
     RT_ENTER(ctx);
-    ctx->tri_prune = enable ? kTriPruneRho : 0.0f;
+    if (mode < 0 || mode > 2) return fail(ctx, RT_E_INVALID, "triangle pruning mode must be 0, 1 or 2");
+    ctx->tri_prune_mode = mode;
     return RT_OK;
 }
 

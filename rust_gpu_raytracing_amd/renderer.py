@@ -302,10 +302,12 @@ class Renderer:
         (BASELINE config 5's stress mode), instead of the acceleration structures."""
         self._call("rt_set_brute_force", int(enable))
 
-    def set_triangle_pruning(self, enable: bool) -> None:
-        """rt_set_triangle_pruning: distance pruning of the triangle walk (on by default;
-        False = box culling only, exact by construction)."""
-        self._call("rt_set_triangle_pruning", int(enable))
+    def set_triangle_pruning(self, mode: int) -> None:
+        """rt_set_triangle_pruning: distance pruning of the triangle walk.
+        1 (default): certified by per-node normal cones and a derived f32 error bound, exact
+        by construction; 0: box culling only (exact); 2: the round-3 relative slack (faster
+        on incoherent meshes, not exact)."""
+        self._call("rt_set_triangle_pruning", int(mode))
 
     def streamed_bytes(self) -> int:
         """Sub-object bytes the brute-force launches streamed through LDS."""

@@ -462,10 +462,11 @@ def test_gpu_quantized_triangle_nodes(gpu, oracle_lib, monkeypatch, qnodes, prim
 
 
 @pytest.mark.parametrize("prune,octants,primary", [("1", "1", "0"), ("1", "0", "0"), ("1", "1", "1"),
-                                                   ("0", "1", "0")])
+                                                   ("0", "1", "0"), ("2", "1", "0"), ("2", "1", "1")])
 def test_gpu_triangle_pruning(gpu, oracle_lib, monkeypatch, prune, octants, primary):
     """Distance pruning of the triangle walk over the direction-ordered layouts (DESIGN.md
-    §5.3c), per-lane walk and primary pre-pass, and each switch alone: the oracle's result."""
+    §5.3c): certified (1, default), none (0), the round-3 relative slack (2); per-lane walk
+    and primary pre-pass, and each switch alone: the oracle's result on this scene."""
     monkeypatch.setenv("RT_TRI_PRUNE", prune)
     monkeypatch.setenv("RT_TRI_OCTANTS", octants)
     monkeypatch.setenv("RT_PRIMARY_PASS", primary)
@@ -485,20 +486,59 @@ def test_gpu_triangle_pruning(gpu, oracle_lib, monkeypatch, prune, octants, prim
     ("c4_mixed", dict(width=1920, height=1080), 10),
 ])
 def test_gpu_triangle_pruning_full_frames(gpu, config, kw, frames):
-    """At BASELINE size the pruned walk (default) and box culling alone (rt_set_triangle_pruning
-    0, exact by construction) give the same accumulation bit for bit, frame after frame."""
+    """At BASELINE size the certified pruned walk (default), box culling alone
+    (rt_set_triangle_pruning 0) and the round-3 relative slack (2) give the same
+    accumulation bit for bit, frame after frame, on these scenes."""
     scene, bounces = build_config(config, **kw)
     res = []
-    for prune in (True, False):
+    for prune in (0, 1, 2):
         with Renderer(scene, frame_batch=frames) as r:
             r.set_triangle_pruning(prune)
             for _ in range(frames):
                 r.compute_frame(bounces)
             res.append((r.read_accumulation(), r.read_output(), r.ray_count()))
-    (a1, o1, n1), (a0, o0, n0) = res
-    assert n1 == n0
-    assert np.array_equal(o1, o0)
-    assert np.array_equal(a1.view(np.uint32), a0.view(np.uint32))
+    a0, o0, n0 = res[0]
+    for a1, o1, n1 in res[1:]:
+        assert n1 == n0
+        assert np.array_equal(o1, o0)
+        assert np.array_equal(a1.view(np.uint32), a0.view(np.uint32))
+
+
+@pytest.mark.parametrize("prune,primary", [("1", "0"), ("1", "1"), ("0", "0")])
+def test_gpu_grazing_rays_certified_pruning(gpu, oracle_lib, monkeypatch, prune, primary):
+    """Adversarial primary rays (tests/adversarial.py): the camera 1e-4 from a tilted plane
+    of 12,800 triangles, every direction within 1e-6..1e-3 rad of that plane after the
+    kernel's own jitter (:217-219, cancelled per pixel), so the reference's f32 distances and
+    barycentrics are rounding-dominated; then the paths' bounces. The certified walk
+    (default) and box culling must give the oracle's result bit for bit, with and without
+    the primary pre-pass."""
+    monkeypatch.setenv("RT_TRI_PRUNE", prune)
+    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
+    from rust_gpu_raytracing_amd.camera import Camera
+    from tests.adversarial import grazing_directions, tilted_plane_grid
+
+    w, h = 64, 48
+    scene, bounces = build_config("c1_four_spheres", width=w, height=h)
+    _, _, _, obj, frame = tilted_plane_grid(3, n=80, size=0.1)
+    scene.objects = [obj]
+    p0, e1, e2, nrm = frame
+    origin = (p0 - 1e-4 * nrm).astype(np.float32)
+    scene.camera = Camera(w, h, position=origin)
+    rays = scene.camera.recalculate_ray_directions()
+    want = grazing_directions(frame, w * h, (1e-6, 1e-3), np.random.default_rng(4)).astype(np.float32)
+    for i in range(w * h):  # frame k = 1: seed = index * 1 * 326624; jitter x, y, z (:219)
+        s = (i * 326624) & 0xFFFFFFFF
+        jit = []
+        for _ in range(3):
+            s, r01 = _pcg_f32(s)
+            jit.append((r01 * np.float32(2.0) - np.float32(1.0)) * np.float32(0.0005))
+        rays["direction"][i] = want[i] - np.array(jit, np.float32)
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((h, w, 4), np.float32)
+    out_o = np.zeros((h, w), np.uint32)
+    rays_o = o.render_frame(scene.params(accumulation_index=1), bounces, acc_o, out_o)
+    acc, out, n = gpu_render(scene, bounces, 1, rays=rays)
+    assert_same(acc, out, n, acc_o, out_o, rays_o)
 
 
 def test_gpu_update_scene_and_reset(gpu, oracle_lib):
