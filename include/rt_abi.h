@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 8
+#define RT_ABI_VERSION 9
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
