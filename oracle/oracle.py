@@ -20,6 +20,27 @@ LIB = HERE / "build" / "liboracle.so"
 CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC", "-shared", "-std=c11", "-Wall"]
 
 
+# bench.py's cpu_baseline leg times a build tuned for the host it runs on (SURVEY §8d:
+# -O3 -march=native); same IEEE semantics (no FMA contraction, no fast-math), so the
+# same results bit for bit -- cpu_baseline checks that on a crop before timing.
+BASELINE_CFLAGS = ["-O3", "-march=native", *CFLAGS[1:]]
+
+
+def build_baseline() -> Path:
+    """Compile the -O3 -march=native variant on this host (not shipped: built where it runs)."""
+    out = HERE / "build" / f"liboracle_native.{os.getpid()}.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    subprocess.run(["gcc", *BASELINE_CFLAGS, "-o", str(out), str(SRC), "-lm"], check=True)
+    return out
+
+
+def use_library(path: Path) -> None:
+    """Make lib() (and every Oracle) use the oracle built at ``path`` from here on."""
+    global _lib
+    _lib = None
+    lib(path)
+
+
 def build(force: bool = False) -> Path:
     """Compile the oracle with gcc (strict IEEE: no FMA contraction, no fast-math)."""
     if LIB.exists() and not force and LIB.stat().st_mtime >= SRC.stat().st_mtime:
@@ -54,10 +75,10 @@ class OHitOut(ctypes.Structure):
 _lib = None
 
 
-def lib() -> ctypes.CDLL:
+def lib(path: Path | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        L = ctypes.CDLL(str(build()))
+        L = ctypes.CDLL(str(path or build()))
         for n in ("oracle_logf", "oracle_cosf", "oracle_asinf", "oracle_acosf", "oracle_atanf"):
             getattr(L, n).restype = ctypes.c_float
             getattr(L, n).argtypes = [ctypes.c_float]

@@ -1383,6 +1383,10 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #ifdef RT_DIAG
     unsigned long long iters = 0, trav_cyc = 0, steps = 0, step_lanes = 0, shade_cyc = 0, refill_cyc = 0,
                        setup_cyc = 0, leaf_cyc = 0, leaf_steps = 0;
+    // lane occupancy by phase (RT_DIAG only): shading passes and the lanes they shade, split by
+    // the branch each lane takes (sky miss, glass, specular, diffuse), setup passes and lanes
+    unsigned long long shade_passes = 0, shade_lanes = 0, miss_lanes = 0, glass_lanes = 0, spec_lanes = 0,
+                       setup_passes = 0, setup_lanes = 0;
     const unsigned long long t_start = stamp();
 #endif
     while (true) {
@@ -1400,8 +1404,26 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             primary_state(PrimaryRecord{__uint_as_float(r.x), r.y, r.z, r.w}, ts);
             mode = kDone;
         }
+#ifdef RT_DIAG
+        {
+            const uint64_t dm = __ballot(mode == kDone);
+            if (dm) {
+                ++shade_passes;
+                shade_lanes += (unsigned long long)__popcll(dm);
+            }
+        }
+#endif
         if (mode == kDone) {
             const Hit h = trace_end<kTris>(sv, ka, p.o, p.d, ts);
+#ifdef RT_DIAG
+            {
+                const bool miss = h.t == kF32Max;
+                const RtMaterial dmat = sv.mat[min(h.material_index, ka.material_count - 1u)];
+                miss_lanes += (unsigned long long)__popcll(__ballot(miss));
+                glass_lanes += (unsigned long long)__popcll(__ballot(!miss && dmat.glass > 0.0f));
+                spec_lanes += (unsigned long long)__popcll(__ballot(!miss && !(dmat.glass > 0.0f) && dmat.specular > 0.0f));
+            }
+#endif
             ++rays;
             RT_ISA_MARK("shade");
             if (shade<(kMode >= 1)>(sv, ka, p, h)) {
@@ -1460,6 +1482,15 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #endif
         // 3. Start the next ray of every lane that has one (the bounce loop's
         // bound, :226, ends a path without a trace only when bounces == 0).
+#ifdef RT_DIAG
+        {
+            const uint64_t sm = __ballot(mode == kSetup);
+            if (sm) {
+                ++setup_passes;
+                setup_lanes += (unsigned long long)__popcll(sm);
+            }
+        }
+#endif
         if (mode == kSetup) {
             while (mode == kSetup && p.bounce >= ka.bounces) finish_sample();
             if (mode == kSetup) {
@@ -1566,6 +1597,14 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         atomicAdd(ka.diag + 7, setup_cyc);
         atomicAdd(ka.diag + 8, leaf_cyc);
         atomicAdd(ka.diag + 9, leaf_steps);
+        // (RT_DIAG builds do not write the RT_DIAG_TAIL per-wave records: words 12.. are free)
+        atomicAdd(ka.diag + 12, shade_passes);
+        atomicAdd(ka.diag + 13, shade_lanes);
+        atomicAdd(ka.diag + 14, miss_lanes);
+        atomicAdd(ka.diag + 15, glass_lanes);
+        atomicAdd(ka.diag + 16, spec_lanes);
+        atomicAdd(ka.diag + 17, setup_passes);
+        atomicAdd(ka.diag + 18, setup_lanes);
     }
 #endif
 #ifdef RT_DIAG_TAIL

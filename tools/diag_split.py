@@ -3,7 +3,9 @@
 usage: RT_LIB=build/variants/lib_diag.so python tools/diag_split.py [--frame-batch F] [config ...]
 Reports, summed over waves, the share of wave-cycles spent in the traversal
 loop (step 4 of the kernel loop); the rest is shading, RNG, refill and
-framebuffer I/O. Also: traversal steps per ray and mean lanes per step.
+framebuffer I/O. Also: traversal steps per ray and mean lanes per step, the lane
+occupancy of each phase, the inactive-lane share of the wave cycles by phase, and
+which branch the shaded lanes took (sky miss / glass / specular / diffuse).
 Stamps serialise the wave around each trace: read shares, not absolute times.
 """
 import json
@@ -32,12 +34,25 @@ for name in argv or list(SIZES):
         r.reset_ray_count()
         for _ in range(3 * fb):
             r.compute_frame(bounces)
-        c = r.debug_counters(10)
+        c = r.debug_counters(20)
         rays = r.ray_count()
     total, trav, steps, it, step_lanes, shade, refill, setup, leaf_cyc, leaf_steps = c[:10]
+    sh_pass, sh_lanes, miss, glass, spec, su_pass, su_lanes = c[12:19]
+    trav_occ = step_lanes / max(steps, 1) / 64
+    shade_occ = sh_lanes / max(sh_pass, 1) / 64
+    setup_occ = su_lanes / max(su_pass, 1) / 64
+    # inactive-lane share of all wave cycles, by phase: the phase's cycles x (1 - its mean occupancy)
+    idle = {"traversal": trav / total * (1 - trav_occ), "shading": shade / total * (1 - shade_occ),
+            "setup": setup / total * (1 - setup_occ), "refill_and_rest": (total - trav - shade - setup) / total}
+    hits = max(sh_lanes - miss, 1)
     print(json.dumps({"config": name, "frame_batch": fb, "trav_share": trav / total, "shade_share": shade / total,
                       "refill_share": refill / total, "setup_share": setup / total,
                       "rest_share": 1 - (trav + shade + refill + setup) / total,
                       "cycles_per_ray": total / rays, "steps_per_ray": steps / rays,
                       "lanes_per_step": step_lanes / max(steps, 1), "outer_iters_per_ray": it / rays,
-                      "leaf_share": leaf_cyc / total, "leaf_steps_per_ray": leaf_steps / rays}))
+                      "leaf_share": leaf_cyc / total, "leaf_steps_per_ray": leaf_steps / rays,
+                      "occupancy": {"traversal": trav_occ, "shading": shade_occ, "setup": setup_occ},
+                      "inactive_lane_share_by_phase": idle,
+                      "shaded_lanes": {"sky_miss": miss / max(sh_lanes, 1), "hit_glass": glass / hits,
+                                       "hit_specular": spec / hits, "hit_diffuse": 1 - (glass + spec) / hits},
+                      "note": "shading of a hit runs Box-Muller (3 normal draws) for every hit lane"}))
