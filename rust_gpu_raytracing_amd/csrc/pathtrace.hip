@@ -73,6 +73,11 @@ struct SceneView {
     // the quantized triangle nodes (modes 0/1; null: the 32-B nodes) and their grid
     const uint4* tri_q;
     float qox, qoy, qoz, qsx, qsy, qsz;
+    // mode 2: the vertex-indexed triangles in LDS (null: the 64-B records), and whether the
+    // leaves then test their sub-object lazily (the records not staged)
+    const float4* cverts;
+    const uint16_t* cidx;
+    bool lazy_sub;
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -175,6 +180,19 @@ struct TriGeom {
 __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t, uint32_t i) {
     const float4 p0 = t[i].p0, p1 = t[i].p1, p2 = t[i].p2;
     return TriGeom{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w)};
+}
+
+// A triangle from the LDS vertex table (mode 2): edge_ab, edge_ac and calc_normal recomputed
+// with SceneTriangle::new's f32 operations (src/buffers.rs:66-95; tri_wide.h
+// wide_tri_from_vertices) -- the record's own bits, checked for every triangle when the table
+// was built (rt_abi.cpp build_compact_triangles), so the test sees exactly the stored values.
+__device__ __forceinline__ TriGeom compact_tri(const SceneView& sv, uint32_t ti) {
+    const uint16_t* ix = sv.cidx + 3u * ti;
+    const float4 va = sv.cverts[ix[0]], vb = sv.cverts[ix[1]], vc = sv.cverts[ix[2]];
+    const f3 ab = mk(vb.x - va.x, vb.y - va.y, vb.z - va.z);
+    const f3 ac = mk(vc.x - va.x, vc.y - va.y, vc.z - va.z);
+    const f3 cn = mk(ab.y * ac.z - ab.z * ac.y, ab.z * ac.x - ab.x * ac.z, ab.x * ac.y - ab.y * ac.x);
+    return TriGeom{mk(va.x, va.y, va.z), ab, ac, cn};
 }
 
 // check_triangles, compute_shader.wgsl:422-517: the reference's own sweep over
@@ -386,7 +404,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) return;
     uint32_t first, count;
     int sub_state;  // 1: passed, 0: not tested yet
-    if (kLazySub && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
+    if ((kLazySub || sv.lazy_sub) && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
         first = pr.w & ((1u << 27) - 1u);
         count = pr.w >> 27;
         sub_state = 0;
@@ -400,7 +418,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     for (uint32_t j = 0; j < count; ++j) {
         const uint32_t ti = min(first + j, ka.triangle_count - 1u);
         const uint32_t seq = pr.z + j;
-        const TriGeom g = load_tri(ka.triangles, ti);
+        const TriGeom g = sv.cidx ? compact_tri(sv, ti) : load_tri(ka.triangles, ti);
         const float det = -dot(d, g.cn);
         const float inv_det = 1.0f / det;
         const f3 ao = o - g.a;
@@ -415,7 +433,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         if (u < 0.0f) continue;
         const float w = 1.0f - u - v;
         if (w < 0.0f) continue;
-        if (kLazySub && sub_state == 0) {
+        if ((kLazySub || sv.lazy_sub) && sub_state == 0) {
             const RtSubObject sub = sv.sub[pr.y];
             if (!ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) return;
             sub_state = 1;
@@ -1254,6 +1272,16 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_sub_offset);
             for (uint32_t i = tid; i < ka.sub_object_count; i += kThreads) l_sub[i] = ka.sub_objects[i];
             sv.sub = l_sub;
+        }
+        if (ka.lds_cidx_offset) {  // the vertex-indexed triangles, when they fit
+            float4* l_cv = reinterpret_cast<float4*>(lds + ka.lds_cvert_offset);
+            uint32_t* l_ci = reinterpret_cast<uint32_t*>(lds + ka.lds_cidx_offset);
+            const uint32_t* g_ci = reinterpret_cast<const uint32_t*>(ka.tri_cidx);
+            for (uint32_t i = tid; i < ka.tri_cvert_count; i += kThreads) l_cv[i] = ka.tri_cverts[i];
+            for (uint32_t i = tid; i < (3u * ka.triangle_count + 1u) / 2u; i += kThreads) l_ci[i] = g_ci[i];
+            sv.cverts = l_cv;
+            sv.cidx = reinterpret_cast<const uint16_t*>(l_ci);
+            sv.lazy_sub = ka.lds_sub_offset == 0;  // records in global memory: test them lazily
         }
     }
     for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];

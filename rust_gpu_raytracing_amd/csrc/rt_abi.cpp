@@ -267,6 +267,14 @@ struct rt_ctx {
     // certified pruning records (tri_cone.h): per node of the base accelerator, and per position
     // of the direction-ordered layouts; rebuilt on the device after any change of the
     // accelerator or the triangles
+    // the triangles as a vertex table + 3 u16 indices each (build_compact_triangles), staged
+    // in LDS by mode-2 launches when it fits; valid only while it reproduces every record
+    float4* d_cverts = nullptr;
+    uint16_t* d_cidx = nullptr;
+    size_t cverts_cap = 0, cidx_cap = 0;
+    uint32_t cvert_count = 0;
+    bool compact_valid = false;
+    bool use_lds_compact = true;  // RT_TRI_LDS_COMPACT=0: mode 2 reads the 64-B records (A/B switch)
     TriCone* d_tri_cones = nullptr;
     TriCone* d_tri_cones8 = nullptr;
     size_t tri_cones_cap = 0, tri_cones8_cap = 0;
@@ -616,9 +624,83 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
     return RT_OK;
 }
 
+// The triangles as a vertex table: vertices a, fl(a + edge_ab), fl(a + edge_ac) deduplicated
+// by bit pattern, and 3 u16 indices per triangle, when SceneTriangle::new's arithmetic
+// (src/buffers.rs:66-95, wide_tri_from_vertices) reproduces every record's edge_ab, edge_ac and
+// calc_normal bit for bit from them (the kernel recomputes those from the vertices), the
+// vertices number at most 65,536, and the table could fit the mode-2 LDS budget at all.
+bool build_compact_triangles(const rt_scene_triangle* t, uint32_t n, std::vector<float4>* verts,
+                             std::vector<uint16_t>* idx) {
+    if (n == 0 || (size_t)n * 6 > kLdsAccelBudget) return false;
+    struct Key {
+        uint32_t b[3];
+        uint32_t id;
+    };
+    std::vector<Key> keys(3 * (size_t)n);
+    for (uint32_t i = 0; i < n; i++) {
+        const rt_scene_triangle& r = t[i];
+        TriVertex v[3];
+        v[0] = TriVertex{r.a[0], r.a[1], r.a[2]};
+        v[1] = TriVertex{r.a[0] + r.edge_ab[0], r.a[1] + r.edge_ab[1], r.a[2] + r.edge_ab[2]};
+        v[2] = TriVertex{r.a[0] + r.edge_ac[0], r.a[1] + r.edge_ac[1], r.a[2] + r.edge_ac[2]};
+        float ab[3], ac[3], cn[3];
+        wide_tri_from_vertices(v[0], v[1], v[2], ab, ac, cn);
+        if (std::memcmp(ab, r.edge_ab, 12) || std::memcmp(ac, r.edge_ac, 12) || std::memcmp(cn, r.calc_normal, 12))
+            return false;
+        for (int k = 0; k < 3; k++) {
+            Key& q = keys[3 * (size_t)i + k];
+            std::memcpy(q.b, &v[k], 12);
+            q.id = 3u * i + (uint32_t)k;
+        }
+    }
+    std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+        return std::memcmp(x.b, y.b, 12) < 0 || (std::memcmp(x.b, y.b, 12) == 0 && x.id < y.id);
+    });
+    verts->clear();
+    idx->assign(3 * (size_t)n + 1, 0);  // + 1: the kernel stages whole u32 words
+    for (size_t j = 0; j < keys.size(); j++) {
+        if (j == 0 || std::memcmp(keys[j].b, keys[j - 1].b, 12) != 0) {
+            if (verts->size() == 65536) return false;
+            float f[3];
+            std::memcpy(f, keys[j].b, 12);
+            verts->push_back(make_float4(f[0], f[1], f[2], 0.0f));
+        }
+        (*idx)[keys[j].id] = (uint16_t)(verts->size() - 1);
+    }
+    return true;
+}
+
 int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     if (n == 0) return RT_OK;
     ctx->cones_dirty = true;
+    // the vertex table describes the whole buffer only when this upload rewrites all of it
+    ctx->compact_valid = false;
+    if (n == ctx->cap_tri) {
+        std::vector<float4> verts;
+        std::vector<uint16_t> idx;
+        if (build_compact_triangles(t, n, &verts, &idx)) {
+            const size_t bv = verts.size() * sizeof(float4), bi = idx.size() * sizeof(uint16_t);
+            if (ctx->cverts_cap < bv || ctx->cidx_cap < bi) {
+                RT_HIP(ctx, join_aux(ctx));
+                RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+                if (ctx->d_cverts) RT_HIP(ctx, hipFree(ctx->d_cverts));
+                if (ctx->d_cidx) RT_HIP(ctx, hipFree(ctx->d_cidx));
+                ctx->d_cverts = nullptr;
+                ctx->d_cidx = nullptr;
+                ctx->cverts_cap = ctx->cidx_cap = 0;
+                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_cverts), bv));
+                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_cidx), bi));
+                ctx->cverts_cap = bv;
+                ctx->cidx_cap = bi;
+            }
+            int rc;
+            if ((rc = upload_raw(ctx, ctx->d_cverts, verts.data(), bv)) ||
+                (rc = upload_raw(ctx, ctx->d_cidx, idx.data(), bi)))
+                return rc;
+            ctx->cvert_count = (uint32_t)verts.size();
+            ctx->compact_valid = true;
+        }
+    }
     void* p;
     int rc = staging(ctx, (size_t)n * sizeof(RtTriangleHot), &p);
     if (rc) return rc;
@@ -835,6 +917,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->tri_prune_mode = env[0] == '0' ? 0 : env[0] == '2' ? 2 : 1;
         env = std::getenv("RT_TRI_QNODES");
         if (env) ctx->use_qnodes = env[0] != '0';
+        env = std::getenv("RT_TRI_LDS_COMPACT");
+        if (env) ctx->use_lds_compact = env[0] != '0';
         env = std::getenv("RT_STAGE_SUBS");
         if (env) ctx->stage_subs = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
@@ -915,7 +999,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
                     ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
-                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_cones, ctx->d_tri_cones8};
+                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_cones, ctx->d_tri_cones8, ctx->d_cverts, ctx->d_cidx};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1173,6 +1257,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tri_wide = reinterpret_cast<const float4*>(ctx->d_wide);
     ka.tri_leaves = reinterpret_cast<const uint4*>(ctx->d_leaves);
     ka.tri_verts = ctx->d_verts;
+    ka.tri_cverts = ctx->d_cverts;
+    ka.tri_cidx = ctx->d_cidx;
+    ka.tri_cvert_count = ctx->cvert_count;
     ka.materials = ctx->d_mat;
     ka.objects = ctx->d_obj;
     ka.sub_objects = ctx->d_sub;
@@ -1279,6 +1366,18 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
             ka.lds_tri_prims_offset = (uint32_t)off;
             off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
+        }
+        // the vertex-indexed triangles, when they fit the mode-2 budget (the leaves' triangle
+        // reads then stay in LDS; RT_TRI_LDS_COMPACT=0 switches it off)
+        ka.lds_cvert_offset = ka.lds_cidx_offset = 0;
+        if (!wide && ctx->compact_valid && ctx->use_lds_compact && ka.tri_accel && ka.triangle_count == ctx->cap_tri) {
+            const size_t cv = al16(off + (size_t)ctx->cvert_count * sizeof(float4));
+            const size_t ci = al16(cv + (3u * (size_t)ka.triangle_count + 1u) / 2u * 4u);
+            if (ci + kLdsTailBytes <= kLdsAccelBudget) {
+                ka.lds_cvert_offset = (uint32_t)off;
+                ka.lds_cidx_offset = (uint32_t)cv;
+                off = ci;
+            }
         }
         // the sub-object records the leaves read, when they fit the mode-2 budget too
         // (one dependent global load less per leaf test; RT_STAGE_SUBS=0 switches it off)
@@ -1747,6 +1846,7 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
                                count, ctx->model_tris, (uint32_t)ctx->h_sub.size(), ctx->d_tri, ctx->d_tri_bounds,
                                ctx->d_sub, ctx->d_obj, ctx->stream));
     ctx->geom_on_device = true;
+    ctx->compact_valid = false;  // the triangles changed on the device: mode 2 reads the records
     // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds,
     // and the wide one's compact leaves are rechecked against the new triangles
     if (ctx->wide_built && ctx->tri_nodes && !ctx->tri_dirty) {

@@ -135,6 +135,11 @@ struct KernelArgs {
     const float4* __restrict__ tri_wide;          // TriWideNode[tri_nodes] as 8 float4 each
     const uint4* __restrict__ tri_leaves;         // TriLeaf as 4 uint4 each
     const TriVertex* __restrict__ tri_verts;      // compact leaves' vertex blocks
+    // vertex-indexed copy of the triangle records (mode 2 stages it in LDS): vertices, and per
+    // triangle 3 u16 indices (a, fl(a + edge_ab), fl(a + edge_ac))
+    const float4* __restrict__ tri_cverts;
+    const uint16_t* __restrict__ tri_cidx;
+    uint32_t tri_cvert_count;
     // textures (bindings 9, 11), RGBA8 sRGB, + decode table
     const uint32_t* __restrict__ textures;
     const uint32_t* __restrict__ env;
@@ -228,6 +233,11 @@ struct KernelArgs {
     uint32_t lds_tri_nodes_offset;
     uint32_t lds_tri_prims_offset;
     uint32_t lds_sub_offset;  // mode 2: sub-object records staged in LDS at this offset; 0: read from global
+    // mode 2: the triangles as a vertex table (float4 per vertex) and 3 u16 vertex indices per
+    // triangle, staged in LDS at these offsets when every record is reproduced bit for bit by
+    // SceneTriangle::new's arithmetic from its vertices (tri_compact_*; 0: the 64-B records)
+    uint32_t lds_cvert_offset;
+    uint32_t lds_cidx_offset;
     uint32_t lds_stack_offset;    // kWide: the walk's per-lane stack, tri_stack_depth x threads u32
     uint32_t lds_srgb_offset;
 };

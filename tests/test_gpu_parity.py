@@ -541,6 +541,27 @@ def test_gpu_grazing_rays_certified_pruning(gpu, oracle_lib, monkeypatch, prune,
     assert_same(acc, out, n, acc_o, out_o, rays_o)
 
 
+@pytest.mark.parametrize("compact,perturb", [("1", False), ("0", False), ("1", True)])
+def test_gpu_lds_vertex_indexed_triangles(gpu, oracle_lib, monkeypatch, compact, perturb):
+    """Mode 2 stages the triangles as an LDS vertex table (3 u16 indices per triangle) when
+    SceneTriangle::new's arithmetic reproduces every record from its vertices; the leaves then
+    recompute edge_ab / edge_ac / calc_normal (src/buffers.rs:66-95). On (chess), off, and with
+    records that do not follow from their vertices (calc_normal a few ulp off on some
+    triangles: the table is refused and the 64-B records are read): the oracle's result."""
+    monkeypatch.setenv("RT_TRI_LDS_COMPACT", compact)
+    scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
+    if perturb:
+        obj = scene.objects[3]
+        obj.triangles = obj.triangles.copy()
+        obj.triangles["calc_normal"][::5] *= np.float32(1.0000002)
+    rays = scene.camera.recalculate_ray_directions()
+    acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
+    with Renderer(scene, camera_rays=rays) as r:
+        r.compute_frame(bounces)
+        assert r.launch_config()["scene_in_lds"] == 2
+    assert_same(acc, out, n, *oracle_frames(oracle_lib, scene, bounces, 2, rays))
+
+
 def test_gpu_update_scene_and_reset(gpu, oracle_lib):
     scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
     with Renderer(scene) as r:

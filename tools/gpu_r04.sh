@@ -17,6 +17,11 @@ for s in $STEPS; do
         timeout -k 10 300 python3 tools/ab_env.py "RT_TRI_PRUNE=1" "RT_TRI_PRUNE=0" "RT_TRI_PRUNE=2" \
           --config $c --frames 20 --frame-batch 20 --rounds 5 >> "$OUT/ab_prune.jsonl" 2>> "$OUT/ab_prune.err"
       done ;;
+    knobs5)  # C5 under the certified default: layouts, pre-pass, thresholds re-tuned for an unpruned walk
+      timeout -k 10 400 python3 tools/ab_env.py "RT_TRI_PRUNE=1" "RT_TRI_PRUNE=1 RT_TRI_OCTANTS=0" \
+        "RT_TRI_PRUNE=1 RT_PRIMARY_PASS=0" "RT_TRI_PRUNE=1 RT_TRAV_THRESHOLD=32" "RT_TRI_PRUNE=1 RT_TRAV_THRESHOLD=24" \
+        "RT_TRI_PRUNE=1 RT_LEAF_BATCH=4" "RT_TRI_PRUNE=1 RT_LEAF_BATCH=6" \
+        --config c5_heightfield --frames 20 --frame-batch 20 --rounds 3 >> "$OUT/ab_knobs5.jsonl" 2>> "$OUT/ab_knobs5.err" ;;
     tail)
       RT_LIB=abvar/lib_tail.so timeout -k 10 300 python3 tools/tail_probe.py --frame-batch 20 --split 0/8 c2_rtiow \
         > "$OUT/tail_8way.jsonl" 2> "$OUT/tail.err"
