@@ -22,6 +22,12 @@ for s in $STEPS; do
         "RT_TRI_PRUNE=1 RT_PRIMARY_PASS=0" "RT_TRI_PRUNE=1 RT_TRAV_THRESHOLD=32" "RT_TRI_PRUNE=1 RT_TRAV_THRESHOLD=24" \
         "RT_TRI_PRUNE=1 RT_LEAF_BATCH=4" "RT_TRI_PRUNE=1 RT_LEAF_BATCH=6" \
         --config c5_heightfield --frames 20 --frame-batch 20 --rounds 3 >> "$OUT/ab_knobs5.jsonl" 2>> "$OUT/ab_knobs5.err" ;;
+    c3)  # the LDS vertex table (mode 2) on C3 and C4 at 1080p, certified default
+      for c in c3_chess c4_mixed; do
+        timeout -k 10 300 python3 tools/ab_env.py "RT_TRI_LDS_COMPACT=1" "RT_TRI_LDS_COMPACT=0" \
+          "RT_TRI_LDS_COMPACT=0 RT_STAGE_SUBS=0" --config $c --frames 20 --frame-batch 20 --rounds 5 \
+          >> "$OUT/ab_compact.jsonl" 2>> "$OUT/ab_compact.err"
+      done ;;
     tail)
       RT_LIB=abvar/lib_tail.so timeout -k 10 300 python3 tools/tail_probe.py --frame-batch 20 --split 0/8 c2_rtiow \
         > "$OUT/tail_8way.jsonl" 2> "$OUT/tail.err"
