@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--frame-batch", type=int, default=1, help="frames per launch (rt_set_frame_batch)")
+    ap.add_argument("--split", default="0/1", help="R/N: rank R's share of an N-way tile split (the strong bench)")
     args = ap.parse_args()
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     dirs = scene.camera.recalculate_ray_directions()
@@ -38,7 +39,8 @@ def main():
         for kv in spec.split():
             k, v = kv.split("=", 1)
             os.environ[k] = v
-        rs.append(Renderer(scene, camera_rays=dirs, frame_batch=args.frame_batch))
+        rank, world = map(int, args.split.split("/"))
+        rs.append(Renderer(scene, camera_rays=dirs, frame_batch=args.frame_batch, rank=rank, world_size=world))
         os.environ.clear()
         os.environ.update(saved)
     for r in rs:
@@ -68,7 +70,7 @@ def main():
     ref = rs[0].read_accumulation().view(np.uint32)
     for (s, t), r in zip(times.items(), rs):
         med = statistics.median(t)
-        print(json.dumps({"config": args.config, "spec": s, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+        print(json.dumps({"config": args.config, "split": args.split, "spec": s, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
                           "path_kernel_ms": round(statistics.median(dev[s]), 4),
                           "mray_s": round(rays[s] / med / 1e3, 1),
                           "bit_identical_to_first": bool(np.array_equal(r.read_accumulation().view(np.uint32), ref)),

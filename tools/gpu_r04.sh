@@ -36,6 +36,10 @@ for s in $STEPS; do
     diag)
       RT_LIB=abvar/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow c3_chess \
         > "$OUT/diag.jsonl" 2> "$OUT/diag.err" ;;
+    share8)  # the 8-way share (N=8 strong bench per rank): LDS image and threshold knobs
+      timeout -k 10 300 python3 tools/ab_env.py "RT_TILE_SCHEDULE=1" "RT_SPHERE_OCTANTS=0" "RT_TRAV_THRESHOLD=4" \
+        "RT_TRAV_THRESHOLD=12" "RT_TILE_SCHEDULE=0" "RT_BLOCK_THREADS=512" --split 0/8 --config c2_rtiow \
+        --frames 20 --frame-batch 20 --rounds 7 >> "$OUT/ab_share8.jsonl" 2>> "$OUT/ab_share8.err" ;;
     strong) timeout -k 10 300 python3 tools/strong_probe.py --steps 20 > "$OUT/strong_probe.jsonl" 2> "$OUT/strong_probe.err" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
