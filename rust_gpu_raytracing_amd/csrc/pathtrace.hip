@@ -622,6 +622,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
     float4 lo, hi;
+    bool narrow = true;  // 32-B nodes carry no flag: the record decides
     if (kTris && !kWide && tri && sv.tri_q) {
         // 16-B quantized node: the box decoded exactly (a superset of the 32-B node's box)
         const uint4 q = sv.tri_q[ts.node];
@@ -631,8 +632,9 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
                          fmaf((float)(q.z >> 16), sv.qsz, sv.qoz), 0.0f);
         const bool is_leaf = (q.w & 0x80000000u) != 0u;
         // a leaf's skip link is node + 1 (pre-order), or the end for a layout's last leaf
-        lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : ts.node + 1u) : q.w);
+        lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : ts.node + 1u) : (q.w & ~kTriQNarrow));
         hi.w = __uint_as_float(is_leaf ? (q.w & 0xffffffu) : 0xffffffffu);
+        narrow = (q.w & kTriQNarrow) != 0u;
     } else {
         const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
         lo = nodes[2u * ts.node];
@@ -650,7 +652,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
     if constexpr (kTris) {
         // certified pruning: only for a box entered beyond the best triangle hit
-        if (tri && hit && ka.tri_prune_mode == 1u && near_t > ts.tri.t && ts.tri.t != kF32Max)
+        if (tri && hit && narrow && ka.tri_prune_mode == 1u && near_t > ts.tri.t && ts.tri.t != kF32Max)
             hit = !tri_node_beyond(ka, ts.node, ts.slab, o, d, ts.tri.t, lo, hi);
     }
     const uint32_t leaf = __float_as_uint(hi.w);

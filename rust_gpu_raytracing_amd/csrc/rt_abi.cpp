@@ -52,6 +52,7 @@ hipError_t rt_launch_tri_cones(const SphereBvhNode* nodes, uint32_t n, const Sub
                                const RtSubObject* subs, const RtTriangleHot* tris, uint32_t n_tri,
                                const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels,
                                TriCone* cones, const uint32_t* src8, TriCone* cones8, hipStream_t stream);
+hipError_t rt_launch_tri_cone_flags(const TriCone* cones, uint32_t n, uint4* q, hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
@@ -1486,6 +1487,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ctx->qnodes_dirty = false;
             ctx->derived_octants = octants;
             ctx->derived_qnodes = qnodes;
+            ctx->cones_dirty = true;  // the fresh quantized copy has no kTriQNarrow bits yet
             ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
         }
         if (qnodes) {
@@ -1530,6 +1532,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
                                             ctx->n_tri_dev, ctx->d_tri_order, ctx->d_tri_level_off, ctx->tri_levels,
                                             ctx->d_tri_cones, octants ? ctx->d_tri_src8 : nullptr,
                                             ctx->d_tri_cones8, ctx->stream));
+            if (ka.tri_qnodes)  // the narrow-cone bit in the link words the walk reads
+                RT_HIP(ctx, rt_launch_tri_cone_flags(octants ? ctx->d_tri_cones8 : ctx->d_tri_cones, ka.tri_nodes,
+                                                     ctx->d_tri_qnodes, ctx->stream));
             ctx->cones_dirty = false;
             ctx->derived_cone_octants = octants;
             ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it

@@ -468,6 +468,22 @@ extern "C" __global__ void __launch_bounds__(256) rt_tri_cone_layouts_kernel(con
     if (i < n_out) out[i] = cones[src[i]];
 }
 
+// The kTriQNarrow bit of every quantized link word (tri_qnode.h) from its position's record:
+// set for a narrow cone, cleared otherwise (the copy is re-derived from the base nodes without it).
+extern "C" __global__ void __launch_bounds__(256) rt_tri_cone_flags_kernel(const TriCone* __restrict__ cones,
+                                                                          uint32_t n, uint4* __restrict__ q) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool narrow = (cones[i].flags & kTriConePrunable) == kTriConePrunable;
+    q[i].w = (q[i].w & ~kTriQNarrow) | (narrow ? kTriQNarrow : 0u);
+}
+
+hipError_t rt_launch_tri_cone_flags(const TriCone* cones, uint32_t n, uint4* q, hipStream_t stream) {
+    if (n == 0 || !q) return hipSuccess;
+    hipLaunchKernelGGL(rt_tri_cone_flags_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, cones, n, q);
+    return hipGetLastError();
+}
+
 hipError_t rt_launch_tri_cones(const SphereBvhNode* nodes, uint32_t n, const SubObjectPrim* prims,
                                const RtSubObject* subs, const RtTriangleHot* tris, uint32_t n_tri,
                                const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels,
