@@ -53,6 +53,9 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mray/s (primary+bounce) at 1920x1080, 8 bounces; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# f32 VALU lane peak for this path's scalar (non-packed, non-FMA-counted) code: 256 CUs x 4 SIMDs x
+# 16 lanes x 2.4 GHz (a wave64 instruction issues over 4 cycles of a SIMD16)
+VALU_LANE_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 KERNEL_NAMES = {"path": "rt_pathtrace_kernel", "primary": "rt_primary_kernel", "resolve": "rt_resolve_frames_kernel",
                 "brute": "rt_brute_kernel"}
 # The reference computes a frame every >= 0.8 ms and displays every >= 5 ms
@@ -553,6 +556,13 @@ def main() -> int:
                          if args.brute_force else
                          "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction"),
                 "valu": pmc_issue(pmc),
+                # the roofline this path is actually bound by: VALU issue x lane utilisation of the
+                # same PMC run against the f32 lane peak
+                "valu_lane_roofline": ({"bound": "valu", "unit": "T lane-op/s",
+                                        "achieved": pmc["valu_issue_util"] * pmc["valu_lane_util"] * VALU_LANE_PEAK_TOPS,
+                                        "peak": VALU_LANE_PEAK_TOPS,
+                                        "frac": pmc["valu_issue_util"] * pmc["valu_lane_util"]}
+                                       if pmc and pmc.get("valu_issue_util") is not None else None),
                 "build_hash": build_hash,
             },
         }
