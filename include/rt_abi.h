@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 9
+#define RT_ABI_VERSION 10
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -399,6 +399,13 @@ RT_API int rt_last_launch_passes(const rt_ctx* ctx, uint32_t* passes);
  * (tools/diag_split.py, tools/tail_probe.py), then, for n > 8, per-wave
  * (start, end) real-time stamps of the last launch (-DRT_DIAG_TAIL). */
 RT_API int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
+
+/* Diagnostics (ABI 10): re-derives every leaf certificate of the certified triangle walk
+ * (tri_cone.h) on the host from the device's current leaf records,
+ * sub-objects and triangles, and compares them with the records the device built.
+ * *mismatches = differing records, *valid = records that carry a certificate, *total =
+ * leaf records (all 0 when the last launch read no certificates). */
+RT_API int rt_debug_check_leaf_certificates(rt_ctx* ctx, uint32_t* mismatches, uint32_t* valid, uint32_t* total);
 
 /* Device self-check of the kernel's fast exact-arithmetic helpers against the
  * IEEE operations they replace, over every f32 input (current device):

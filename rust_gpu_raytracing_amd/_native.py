@@ -136,6 +136,8 @@ SIGNATURES = {
     "rt_launch_config": (ctypes.c_int, [_P] + [ctypes.POINTER(ctypes.c_uint32)] * 4),
     "rt_last_launch_passes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_debug_counters": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), _U32]),
+    "rt_debug_check_leaf_certificates": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32),
+                                                        ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "rt_math_selftest": (ctypes.c_int, [_U32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     "rt_stream": (_P, [_P]),
     "rt_srgb_table": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),

@@ -182,6 +182,12 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
     return TriGeom{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w)};
 }
 
+// The LDS vertex table (mode 2, compact_tri): build switch, off by default --
+// compiled in, its code cost the LDS-resident instances more registers than its smaller
+// triangle reads saved (C3 0.304 -> 0.317 ms per frame with it off at run time, 0.349 on).
+#ifndef RT_LDS_COMPACT
+#define RT_LDS_COMPACT 0
+#endif
 // A triangle from the LDS vertex table (mode 2): edge_ab, edge_ac and calc_normal recomputed
 // with SceneTriangle::new's f32 operations (src/buffers.rs:66-95; tri_wide.h
 // wide_tri_from_vertices) -- the record's own bits, checked for every triangle when the table
@@ -292,21 +298,22 @@ __device__ __forceinline__ float tri_limit(const SceneView& sv, const KernelArgs
     return ts.tri.t * (1.0f + ka.tri_prune) + sig;
 }
 
-// Certified distance pruning (ka.tri_prune_mode 1; tri_cone.h): a triangle
-// node whose box the walk enters beyond the best hit tb is skipped only when the node's cone
-// record proves that no triangle below it can pass the reference's test (:449-481) at a
-// distance <= tb. The per-axis entries are the culling slab test's own (rt_bvh_slab.h) on
-// the box as the walk decoded it.
-__device__ __forceinline__ bool tri_node_beyond(const KernelArgs& ka, uint32_t node, const SlabRay& sr, f3 o, f3 d,
-                                                float tb, float4 lo, float4 hi) {
-    const float4* rec = reinterpret_cast<const float4*>(ka.tri_cones + node);
-    const float4 c0 = rec[0], c1 = rec[1];
-    const TriCone c{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, __float_as_uint(c1.w)};
+// Certified distance pruning (ka.tri_prune_mode 1; tri_cone.h): when the walk
+// reaches a leaf whose box it enters beyond the best hit tb, the leaf's certificate proves, per
+// triangle, that the reference's test (:449-481) cannot accept it at a distance <= tb; those
+// triangles are skipped without being loaded, and the whole leaf when all are. Returns the mask
+// of skipped triangles (kLeafCertAll: the leaf). The per-axis entries are the culling slab
+// test's own (rt_bvh_slab.h) on the box as the walk decoded it.
+__device__ __forceinline__ uint32_t tri_leaf_skips(const KernelArgs& ka, uint32_t prim, const SlabRay& sr, f3 o, f3 d,
+                                                   float tb, float4 lo, float4 hi) {
+    const uint4* rec = reinterpret_cast<const uint4*>(ka.tri_leafcert + prim);
+    const uint4 c0 = rec[0], c1 = rec[1];
+    const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     const float t1x = fminf(fmaf(lo.x, sr.ix, sr.lx), fmaf(hi.x, sr.ix, sr.hx));
     const float t1y = fminf(fmaf(lo.y, sr.iy, sr.ly), fmaf(hi.y, sr.iy, sr.hy));
     const float t1z = fminf(fmaf(lo.z, sr.iz, sr.lz), fmaf(hi.z, sr.iz, sr.hz));
-    return tri_cone_prunes(c, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), tb, t1x, t1y, t1z, fabsf(sr.ix),
-                           fabsf(sr.iy), fabsf(sr.iz));
+    return tri_leafcert_skips(w, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), tb, t1x, t1y, t1z, fabsf(sr.ix),
+                              fabsf(sr.iy), fabsf(sr.iz));
 }
 
 // Slab constants and depth bounds of a BVH walk. The triangle walk culls by
@@ -396,15 +403,18 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
 // (a new best hit or a NaN distance); if that test fails, no triangle of the leaf counts --
 // exactly as the reference, which tests none of them then. Most leaves change nothing, so
 // their sub-object record is never read.
+// `pending`: the leaf record's index, with the mask of triangles its certificate skips in
+// bits 24-30 (tri_leaf_skips; they are not loaded).
 template <bool kLazySub = false>
 __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
-                                         uint32_t prim) {
+                                         uint32_t pending) {
+    const uint32_t prim = pending & 0xffffffu, skip = pending >> 24;
     const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base, range
     const RtObject& ob = sv.obj[pr.x];
     if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) return;
     uint32_t first, count;
     int sub_state;  // 1: passed, 0: not tested yet
-    if ((kLazySub || sv.lazy_sub) && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
+    if ((kLazySub || (RT_LDS_COMPACT && sv.lazy_sub)) && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
         first = pr.w & ((1u << 27) - 1u);
         count = pr.w >> 27;
         sub_state = 0;
@@ -416,9 +426,10 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         sub_state = 1;
     }
     for (uint32_t j = 0; j < count; ++j) {
+        if ((skip >> j) & 1u) continue;
         const uint32_t ti = min(first + j, ka.triangle_count - 1u);
         const uint32_t seq = pr.z + j;
-        const TriGeom g = sv.cidx ? compact_tri(sv, ti) : load_tri(ka.triangles, ti);
+        const TriGeom g = (RT_LDS_COMPACT && sv.cidx) ? compact_tri(sv, ti) : load_tri(ka.triangles, ti);
         const float det = -dot(d, g.cn);
         const float inv_det = 1.0f / det;
         const f3 ao = o - g.a;
@@ -433,7 +444,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         if (u < 0.0f) continue;
         const float w = 1.0f - u - v;
         if (w < 0.0f) continue;
-        if ((kLazySub || sv.lazy_sub) && sub_state == 0) {
+        if ((kLazySub || (RT_LDS_COMPACT && sv.lazy_sub)) && sub_state == 0) {
             const RtSubObject sub = sv.sub[pr.y];
             if (!ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) return;
             sub_state = 1;
@@ -612,7 +623,21 @@ constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
 template <int kMode, bool kTris>
 constexpr bool kDrainDecouple = kTris && kMode < 2;
 
-template <bool kTris, bool kWide = false>
+// Leaf certificates in the walks (certified pruning, tri_leaf_skips): walks from global memory
+// always carry the test; walks of the LDS-resident accelerator (mode 2) only when built with
+// RT_LEAFCERT_LDS=1 (off by default: the certificate is a lane-distinct global load where the
+// triangles it saves are LDS reads, and the code costs registers -- C3 0.304 ms per frame
+// without it, 0.335 compiled in and off, 0.362 on). Mode 2 then walks with
+// box culling, exact without any bound.
+#ifndef RT_LEAFCERT_LDS
+#define RT_LEAFCERT_LDS 0
+#endif
+template <int kMode>
+constexpr bool kCertWalk = kMode <= 1 || RT_LEAFCERT_LDS;
+
+
+// kCert: the walk reads leaf certificates (tri_leaf_skips) when ka.tri_leafcert is set.
+template <bool kTris, bool kWide = false, bool kCert = true>
 __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     const bool tri = kTris && ts.phase == 0;
     if (kWide && tri) {
@@ -622,7 +647,6 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
     float4 lo, hi;
-    bool narrow = true;  // 32-B nodes carry no flag: the record decides
     if (kTris && !kWide && tri && sv.tri_q) {
         // 16-B quantized node: the box decoded exactly (a superset of the 32-B node's box)
         const uint4 q = sv.tri_q[ts.node];
@@ -632,9 +656,8 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
                          fmaf((float)(q.z >> 16), sv.qsz, sv.qoz), 0.0f);
         const bool is_leaf = (q.w & 0x80000000u) != 0u;
         // a leaf's skip link is node + 1 (pre-order), or the end for a layout's last leaf
-        lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : ts.node + 1u) : (q.w & ~kTriQNarrow));
+        lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : ts.node + 1u) : q.w);
         hi.w = __uint_as_float(is_leaf ? (q.w & 0xffffffu) : 0xffffffffu);
-        narrow = (q.w & kTriQNarrow) != 0u;
     } else {
         const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
         lo = nodes[2u * ts.node];
@@ -650,19 +673,27 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     // only when strictly closer, :347); ts.slack / ts.limit are 0 / inf on the
     // triangle side
     bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
-    if constexpr (kTris) {
-        // certified pruning: only for a box entered beyond the best triangle hit
-        if (tri && hit && narrow && ka.tri_prune_mode == 1u && near_t > ts.tri.t && ts.tri.t != kF32Max)
-            hit = !tri_node_beyond(ka, ts.node, ts.slab, o, d, ts.tri.t, lo, hi);
-    }
     const uint32_t leaf = __float_as_uint(hi.w);
+    uint32_t skip = 0u;
+    if constexpr (kTris && !kWide && kCert) {
+        // certified pruning: a leaf whose box is entered beyond the best triangle hit
+        if (tri && hit && leaf != 0xffffffffu && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max) {
+            skip = tri_leaf_skips(ka, leaf & 0xffffffu, ts.slab, o, d, ts.tri.t, lo, hi);
+            if (skip == kLeafCertAll) hit = false;
+#ifdef RT_DIAG
+            atomicAdd(ka.diag + 19, 1ull);  // certificate checks, leaves skipped, triangles skipped
+            if (skip == kLeafCertAll) atomicAdd(ka.diag + 20, 1ull);
+            atomicAdd(ka.diag + 21, (unsigned long long)__popc(skip));
+#endif
+        }
+    }
     const bool at_leaf = hit && leaf != 0xffffffffu;
     if (at_leaf && !kDeferLeaves<kTris>) {
         test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
         ts.limit = prune_limit(ts);
     } else if (at_leaf) {
         if (ts.pending != kNoLeaf) return;  // blocked until the batch tests the deferred leaf
-        ts.pending = leaf & 0xffffffu;
+        ts.pending = (leaf & 0xffffffu) | (skip << 24);
     }
     ts.node = (hit && !at_leaf) ? ts.node + 1u : __float_as_uint(lo.w);
 }
@@ -1588,7 +1619,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                     leaf_step<kTris, kWide, (kMode <= 1)>(sv, ka, p.o, p.d, ts);
                 } else {
                     RT_ISA_MARK("node_step");
-                    node_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                    node_step<kTris, kWide, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
                 }
                 phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
                 if (ts.phase == 2) mode = kDone;
@@ -1597,7 +1628,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #pragma unroll
                     for (int k = 1; k < (kTris ? RT_TRAV_UNROLL_TRI : RT_TRAV_UNROLL); ++k) {
                         if (mode == kTrav) {
-                            node_step<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                            node_step<kTris, kWide, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
                             phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
                             if (ts.phase == 2) mode = kDone;
                         }
@@ -1992,12 +2023,16 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
                     float near_t, far_t;
                     slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
                     bool hit = valid && near_t <= far_t && far_t >= 0.0f && near_t <= ts.limit;
-                    if (hit && ka.tri_prune_mode == 1u && near_t > ts.tri.t && ts.tri.t != kF32Max)
-                        hit = !tri_node_beyond(ka, node, ts.slab, o, d, ts.tri.t, lo, hi);  // certified pruning
-                    const bool any = __ballot(hit) != 0;
                     const uint32_t leaf = __float_as_uint(hi.w);
+                    uint32_t skip = 0u;  // certified pruning: the lane's own leaf certificate test
+                    if (kCertWalk<kMode> && hit && leaf != 0xffffffffu && ka.tri_leafcert && near_t > ts.tri.t &&
+                        ts.tri.t != kF32Max) {
+                        skip = tri_leaf_skips(ka, leaf & 0xffffffu, ts.slab, o, d, ts.tri.t, lo, hi);
+                        if (skip == kLeafCertAll) hit = false;
+                    }
+                    const bool any = __ballot(hit) != 0;
                     if (any && leaf != 0xffffffffu && hit) {
-                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);
+                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, (leaf & 0xffffffu) | (skip << 24));
                         ts.limit = tri_limit(sv, ka, o, ts);
                     }
                     node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);

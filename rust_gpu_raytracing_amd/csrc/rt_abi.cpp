@@ -48,11 +48,8 @@ hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, 
 hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, const RtSubObject* subs,
                            const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels, float* extent_out,
                            hipStream_t stream);
-hipError_t rt_launch_tri_cones(const SphereBvhNode* nodes, uint32_t n, const SubObjectPrim* prims,
-                               const RtSubObject* subs, const RtTriangleHot* tris, uint32_t n_tri,
-                               const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels,
-                               TriCone* cones, const uint32_t* src8, TriCone* cones8, hipStream_t stream);
-hipError_t rt_launch_tri_cone_flags(const TriCone* cones, uint32_t n, uint4* q, hipStream_t stream);
+hipError_t rt_launch_tri_leafcert(const SubObjectPrim* prims, uint32_t n_prims, const RtSubObject* subs,
+                                  const RtTriangleHot* tris, uint32_t n_tri, TriLeafCert* out, hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
@@ -262,12 +259,10 @@ struct rt_ctx {
     size_t tri_src8_cap = 0, tri_skip8_cap = 0, tri_bvh8_cap = 0;
     bool tri_octants_built = false;  // d_tri_src8 / d_tri_skip8 describe the current tree
     // rt_set_triangle_pruning / RT_TRI_PRUNE: distance pruning of the triangle walk (DESIGN.md
-    // §5.3c): 1 = certified by the cone records (default, exact), 0 = box culling only,
+    // §5.3c): 1 = certified by the leaf certificates (default, exact), 0 = box culling only,
     // 2 = the round-3 relative slack (not exact)
     int tri_prune_mode = 1;
-    // certified pruning records (tri_cone.h): per node of the base accelerator, and per position
-    // of the direction-ordered layouts; rebuilt on the device after any change of the
-    // accelerator or the triangles
+    bool use_leafcert_lds = false;  // RT_TRI_LEAFCERT_LDS=1 (with a -DRT_LEAFCERT_LDS=1 build): mode-2 walks read them
     // the triangles as a vertex table + 3 u16 indices each (build_compact_triangles), staged
     // in LDS by mode-2 launches when it fits; valid only while it reproduces every record
     float4* d_cverts = nullptr;
@@ -275,12 +270,12 @@ struct rt_ctx {
     size_t cverts_cap = 0, cidx_cap = 0;
     uint32_t cvert_count = 0;
     bool compact_valid = false;
-    bool use_lds_compact = true;  // RT_TRI_LDS_COMPACT=0: mode 2 reads the 64-B records (A/B switch)
-    TriCone* d_tri_cones = nullptr;
-    TriCone* d_tri_cones8 = nullptr;
-    size_t tri_cones_cap = 0, tri_cones8_cap = 0;
+    bool use_lds_compact = false;  // RT_TRI_LDS_COMPACT=1 (with a -DRT_LDS_COMPACT=1 build): stage the table
+    // certified pruning (tri_cone.h): one certificate per leaf record, rebuilt on the device
+    // after any change of the accelerator or the triangles
+    TriLeafCert* d_tri_lcert = nullptr;
+    size_t tri_lcert_cap = 0;
     bool cones_dirty = true;
-    bool derived_cone_octants = false;
     // the 4-wide accelerator (tri_wide.h), RT_TRI_WIDE=1 (A/B switch): measured slower than the
     // binary one on C3-C5, so off by default
     bool use_tri_wide = false;
@@ -918,8 +913,10 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->tri_prune_mode = env[0] == '0' ? 0 : env[0] == '2' ? 2 : 1;
         env = std::getenv("RT_TRI_QNODES");
         if (env) ctx->use_qnodes = env[0] != '0';
+        env = std::getenv("RT_TRI_LEAFCERT_LDS");
+        if (env) ctx->use_leafcert_lds = env[0] == '1';
         env = std::getenv("RT_TRI_LDS_COMPACT");
-        if (env) ctx->use_lds_compact = env[0] != '0';
+        if (env) ctx->use_lds_compact = env[0] == '1';
         env = std::getenv("RT_STAGE_SUBS");
         if (env) ctx->stage_subs = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
@@ -1000,7 +997,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
                     ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
-                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_cones, ctx->d_tri_cones8, ctx->d_cverts, ctx->d_cidx};
+                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1487,7 +1484,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ctx->qnodes_dirty = false;
             ctx->derived_octants = octants;
             ctx->derived_qnodes = qnodes;
-            ctx->cones_dirty = true;  // the fresh quantized copy has no kTriQNarrow bits yet
             ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
         }
         if (qnodes) {
@@ -1500,46 +1496,30 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ka.tri_nodes = n_out;
         }
     }
-    // distance pruning of the binary walk: certified (the cone records,
+    // distance pruning of the binary walk: certified (the leaf certificates,
     // rebuilt on the device after any change), or the round-3 relative slack, or none
     ka.tri_prune_mode = (tris && !wide && ka.tri_accel && ka.tri_nodes != 0) ? (uint32_t)ctx->tri_prune_mode : 0u;
     ka.tri_prune = ka.tri_prune_mode == 2u ? kTriPruneRho : 0.0f;
-    ka.tri_cones = nullptr;
-    if (ka.tri_prune_mode == 1u) {
-        const uint32_t n_base = octants ? ka.tri_octant_stride : ka.tri_nodes;
-        const size_t b1 = (size_t)n_base * sizeof(TriCone), b8 = octants ? 8u * b1 : 0u;
-        if (ctx->tri_cones_cap < b1 || ctx->tri_cones8_cap < b8) {  // (re)allocate: nothing may still read them
+    ka.tri_leafcert = nullptr;
+    if (ka.tri_prune_mode == 1u && ka.tri_prim_count != 0 && (mode <= 1 || ctx->use_leafcert_lds)) {
+        const size_t bytes = (size_t)ka.tri_prim_count * sizeof(TriLeafCert);
+        if (ctx->tri_lcert_cap < bytes) {  // (re)allocate: nothing may still read them
             RT_HIP(ctx, join_aux(ctx));
             RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            if (ctx->tri_cones_cap < b1) {
-                if (ctx->d_tri_cones) RT_HIP(ctx, hipFree(ctx->d_tri_cones));
-                ctx->d_tri_cones = nullptr;
-                ctx->tri_cones_cap = 0;
-                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_cones), b1));
-                ctx->tri_cones_cap = b1;
-            }
-            if (ctx->tri_cones8_cap < b8) {
-                if (ctx->d_tri_cones8) RT_HIP(ctx, hipFree(ctx->d_tri_cones8));
-                ctx->d_tri_cones8 = nullptr;
-                ctx->tri_cones8_cap = 0;
-                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_cones8), b8));
-                ctx->tri_cones8_cap = b8;
-            }
+            if (ctx->d_tri_lcert) RT_HIP(ctx, hipFree(ctx->d_tri_lcert));
+            ctx->d_tri_lcert = nullptr;
+            ctx->tri_lcert_cap = 0;
+            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_lcert), bytes));
+            ctx->tri_lcert_cap = bytes;
             ctx->cones_dirty = true;
         }
-        if (ctx->cones_dirty || ctx->derived_cone_octants != octants) {
-            RT_HIP(ctx, rt_launch_tri_cones(ctx->d_tri_bvh, n_base, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri,
-                                            ctx->n_tri_dev, ctx->d_tri_order, ctx->d_tri_level_off, ctx->tri_levels,
-                                            ctx->d_tri_cones, octants ? ctx->d_tri_src8 : nullptr,
-                                            ctx->d_tri_cones8, ctx->stream));
-            if (ka.tri_qnodes)  // the narrow-cone bit in the link words the walk reads
-                RT_HIP(ctx, rt_launch_tri_cone_flags(octants ? ctx->d_tri_cones8 : ctx->d_tri_cones, ka.tri_nodes,
-                                                     ctx->d_tri_qnodes, ctx->stream));
+        if (ctx->cones_dirty) {
+            RT_HIP(ctx, rt_launch_tri_leafcert(ctx->d_tri_prims, ka.tri_prim_count, ctx->d_sub, ctx->d_tri,
+                                               ctx->n_tri_dev, ctx->d_tri_lcert, ctx->stream));
             ctx->cones_dirty = false;
-            ctx->derived_cone_octants = octants;
             ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
         }
-        ka.tri_cones = octants ? ctx->d_tri_cones8 : ctx->d_tri_cones;
+        ka.tri_leafcert = ctx->d_tri_lcert;
     }
     size_t lds_bytes;
     if (mode == 2) {
@@ -1991,7 +1971,9 @@ int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
 
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters) * sizeof(unsigned long long), ctx->stream));
+    // (RT_DIAG builds keep 12 more counters in the first per-wave record words, which only
+    // RT_DIAG_TAIL builds fill: cleared too)
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters + 12) * sizeof(unsigned long long), ctx->stream));
     RT_HIP(ctx, hipMemsetAsync(ctx->d_stream, 0, sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }
@@ -2130,6 +2112,45 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n) {
     const size_t m = std::min<size_t>(n, kDiagCounters + kDiagWaveRecords);
     RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_counter + 1, m * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_debug_check_leaf_certificates(rt_ctx* ctx, uint32_t* mismatches, uint32_t* valid, uint32_t* total) {
+    RT_ENTER(ctx);
+    if (!mismatches || !valid || !total) return fail(ctx, RT_E_INVALID, "NULL output");
+    *mismatches = *valid = *total = 0;
+    RT_HIP(ctx, join_aux(ctx));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t n = ctx->tri_prim_count;
+    if (!ctx->d_tri_lcert || ctx->cones_dirty || n == 0 || ctx->tri_lcert_cap < (size_t)n * sizeof(TriLeafCert))
+        return RT_OK;
+    std::vector<TriLeafCert> dev(n);
+    std::vector<SubObjectPrim> prims(n);
+    std::vector<RtSubObject> subs(ctx->n_sub_dev);
+    std::vector<RtTriangleHot> tris(ctx->n_tri_dev);
+    RT_HIP(ctx, hipMemcpy(dev.data(), ctx->d_tri_lcert, n * sizeof(TriLeafCert), hipMemcpyDeviceToHost));
+    RT_HIP(ctx, hipMemcpy(prims.data(), ctx->d_tri_prims, n * sizeof(SubObjectPrim), hipMemcpyDeviceToHost));
+    RT_HIP(ctx, hipMemcpy(subs.data(), ctx->d_sub, subs.size() * sizeof(RtSubObject), hipMemcpyDeviceToHost));
+    RT_HIP(ctx, hipMemcpy(tris.data(), ctx->d_tri, tris.size() * sizeof(RtTriangleHot), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; i++) {
+        const RtSubObject& s = subs[std::min<uint32_t>(prims[i].sub, (uint32_t)subs.size() - 1u)];
+        float lo[3], hi[3];
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::fmin(s.min_bounds[k], s.max_bounds[k]);
+            hi[k] = std::fmax(s.min_bounds[k], s.max_bounds[k]);
+        }
+        const uint32_t n_tri = (uint32_t)tris.size();
+        const uint32_t cnt = (s.triangle_count <= kLeafCertSlots && n_tri != 0u) ? s.triangle_count : 0u;
+        float a[kLeafCertSlots][3], ab[kLeafCertSlots][3], ac[kLeafCertSlots][3], cn[kLeafCertSlots][3];
+        for (uint32_t j = 0; j < cnt; ++j) {
+            float fn[3];
+            unpack_triangle(tris[std::min(s.first_triangle_index + j, n_tri - 1u)], a[j], ab[j], ac[j], cn[j], fn);
+        }
+        const TriLeafCert h = tricone::leafcert_build(cnt, a, ab, ac, cn, lo, hi);
+        *mismatches += std::memcmp(&h, &dev[i], sizeof(h)) != 0;
+        *valid += dev[i].w[7] != kLeafCertNone;
+    }
+    *total = n;
     return RT_OK;
 }
 

@@ -172,13 +172,14 @@ struct KernelArgs {
     // ray starts at layout octant(d) x stride; 0: one layout.
     uint32_t tri_octant_stride;
     // distance pruning of the triangle walk, once a triangle is hit at t:
-    // tri_prune_mode 1 = certified (a node is skipped when tri_cone_prunes proves, from its
-    // record in tri_cones -- same indexing as tri_bvh -- that none of its triangles can be
-    // accepted at a distance <= t); 2 = the round-3 relative slack (boxes entered beyond
-    // t * (1 + tri_prune) + 2^-10 (|o| + extent) / |d|; not exact); 0 = box culling only
+    // tri_prune_mode 1 = certified (a leaf entered beyond t: the triangles its certificate in
+    // tri_leafcert -- one per leaf record, tri_prims' indexing -- proves cannot be accepted at a
+    // distance <= t are skipped; null: box culling); 2 = the round-3 relative slack (boxes
+    // entered beyond t * (1 + tri_prune) + 2^-10 (|o| + extent) / |d|; not exact); 0 = box
+    // culling only
     uint32_t tri_prune_mode;
     float tri_prune;
-    const TriCone* __restrict__ tri_cones;
+    const TriLeafCert* __restrict__ tri_leafcert;
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     // Frame-parallel batch (frames > 1, accumulating): the queue holds one unit per

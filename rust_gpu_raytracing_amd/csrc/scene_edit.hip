@@ -414,90 +414,35 @@ hipError_t rt_launch_quantize_tri_nodes(const SphereBvhNode* nodes, uint32_t n, 
     return hipGetLastError();
 }
 
-// ---- certified pruning records of the binary triangle accelerator (tri_cone.h) ----
-// After every upload of the accelerator, of the triangles, or a refit: each leaf's record
-// from its sub-object's box and triangle records (the 64-B records the walks read, with the
-// walks' index clamp), then the internal nodes level by level, deepest first (the refit's
-// order), each from its two children's records; with the direction-ordered layouts, each
-// layout position takes its base node's record. Double-precision arithmetic rounded the safe
-// way (tri_cone.h), so a record never claims more than its triangles allow.
-extern "C" __global__ void __launch_bounds__(256) rt_tri_cone_leaves_kernel(
-    const SphereBvhNode* __restrict__ nodes, uint32_t n, const SubObjectPrim* __restrict__ prims,
-    const RtSubObject* __restrict__ subs, const RtTriangleHot* __restrict__ tris, uint32_t n_tri,
-    TriCone* __restrict__ cones) {
+// Leaf certificates (tri_cone.h TriLeafCert), one per leaf record (prim), from its sub-object's
+// box and the triangle records the walk's leaf test reads (same index clamp); rebuilt with the
+// cones after every change of the accelerator or the triangles.
+extern "C" __global__ void __launch_bounds__(256) rt_tri_leafcert_kernel(const SubObjectPrim* __restrict__ prims,
+                                                                        uint32_t n_prims,
+                                                                        const RtSubObject* __restrict__ subs,
+                                                                        const RtTriangleHot* __restrict__ tris,
+                                                                        uint32_t n_tri, TriLeafCert* __restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const SphereBvhNode nd = nodes[i];
-    if (nd.leaf == kSphereBvhInternal) return;
-    const RtSubObject s = subs[prims[nd.leaf & 0xffffffu].sub];
+    if (i >= n_prims) return;
+    const RtSubObject s = subs[prims[i].sub];
     float lo[3], hi[3];
     for (int k = 0; k < 3; k++) {
         lo[k] = fminf(s.min_bounds[k], s.max_bounds[k]);
         hi[k] = fmaxf(s.min_bounds[k], s.max_bounds[k]);
     }
-    tricone::Acc acc = tricone::acc_empty();
-    for (uint32_t j = 0; j < s.triangle_count && n_tri != 0u; ++j) {
-        float a[3], ab[3], ac[3], cn[3], fn[3];
-        unpack_triangle(tris[min(s.first_triangle_index + j, n_tri - 1u)], a, ab, ac, cn, fn);
-        tricone::acc_add_triangle(acc, a, ab, ac, cn, lo, hi);
+    const uint32_t cnt = (s.triangle_count <= kLeafCertSlots && n_tri != 0u) ? s.triangle_count : 0u;
+    float a[kLeafCertSlots][3], ab[kLeafCertSlots][3], ac[kLeafCertSlots][3], cn[kLeafCertSlots][3];
+    for (uint32_t j = 0; j < cnt; ++j) {
+        float fn[3];
+        unpack_triangle(tris[min(s.first_triangle_index + j, n_tri - 1u)], a[j], ab[j], ac[j], cn[j], fn);
     }
-    if (acc.n == 0u) acc.valid = false;
-    cones[i] = tricone::acc_record(acc);
+    out[i] = tricone::leafcert_build(cnt, a, ab, ac, cn, lo, hi);
 }
 
-extern "C" __global__ void __launch_bounds__(kRefitThreads) rt_tri_cone_merge_kernel(
-    const SphereBvhNode* __restrict__ nodes, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ level_offsets, uint32_t n_levels, TriCone* __restrict__ cones) {
-    for (uint32_t l = 0; l < n_levels; l++) {
-        for (uint32_t i = level_offsets[l] + threadIdx.x; i < level_offsets[l + 1]; i += kRefitThreads) {
-            const uint32_t n = order[i];
-            if (nodes[n].leaf != kSphereBvhInternal) continue;
-            tricone::Acc a = tricone::acc_from_record(cones[n + 1u]);
-            tricone::acc_add_acc(a, tricone::acc_from_record(cones[nodes[n + 1u].skip]));
-            cones[n] = tricone::acc_record(a);
-        }
-        __syncthreads();
-    }
-}
-
-extern "C" __global__ void __launch_bounds__(256) rt_tri_cone_layouts_kernel(const TriCone* __restrict__ cones,
-                                                                            const uint32_t* __restrict__ src,
-                                                                            uint32_t n_out,
-                                                                            TriCone* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n_out) out[i] = cones[src[i]];
-}
-
-// The kTriQNarrow bit of every quantized link word (tri_qnode.h) from its position's record:
-// set for a narrow cone, cleared otherwise (the copy is re-derived from the base nodes without it).
-extern "C" __global__ void __launch_bounds__(256) rt_tri_cone_flags_kernel(const TriCone* __restrict__ cones,
-                                                                          uint32_t n, uint4* __restrict__ q) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const bool narrow = (cones[i].flags & kTriConePrunable) == kTriConePrunable;
-    q[i].w = (q[i].w & ~kTriQNarrow) | (narrow ? kTriQNarrow : 0u);
-}
-
-hipError_t rt_launch_tri_cone_flags(const TriCone* cones, uint32_t n, uint4* q, hipStream_t stream) {
-    if (n == 0 || !q) return hipSuccess;
-    hipLaunchKernelGGL(rt_tri_cone_flags_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, cones, n, q);
-    return hipGetLastError();
-}
-
-hipError_t rt_launch_tri_cones(const SphereBvhNode* nodes, uint32_t n, const SubObjectPrim* prims,
-                               const RtSubObject* subs, const RtTriangleHot* tris, uint32_t n_tri,
-                               const uint32_t* order, const uint32_t* level_offsets, uint32_t n_levels,
-                               TriCone* cones, const uint32_t* src8, TriCone* cones8, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(rt_tri_cone_leaves_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, nodes, n, prims,
-                       subs, tris, n_tri, cones);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rt_tri_cone_merge_kernel, dim3(1), dim3(kRefitThreads), 0, stream, nodes, order,
-                       level_offsets, n_levels, cones);
-    e = hipGetLastError();
-    if (e != hipSuccess || !src8) return e;
-    hipLaunchKernelGGL(rt_tri_cone_layouts_kernel, dim3((8u * n + 255u) / 256u), dim3(256), 0, stream, cones, src8,
-                       8u * n, cones8);
+hipError_t rt_launch_tri_leafcert(const SubObjectPrim* prims, uint32_t n_prims, const RtSubObject* subs,
+                                  const RtTriangleHot* tris, uint32_t n_tri, TriLeafCert* out, hipStream_t stream) {
+    if (n_prims == 0 || !out) return hipSuccess;
+    hipLaunchKernelGGL(rt_tri_leafcert_kernel, dim3((n_prims + 255u) / 256u), dim3(256), 0, stream, prims, n_prims,
+                       subs, tris, n_tri, out);
     return hipGetLastError();
 }

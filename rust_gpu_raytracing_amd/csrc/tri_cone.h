@@ -1,31 +1,29 @@
 // tri_cone.h -- certified distance pruning of the triangle walk.
 //
-// Once a walk holds a triangle hit at distance tb, a node may be skipped only if no
-// triangle below it can pass the reference's f32 test (compute_shader.wgsl:449-481)
-// with a distance <= tb. Per node this header keeps what proves it: a double cone
-// bounding the directions of every triangle normal N = ab x ac below the node (axis A,
-// half-angle phi; N and -N alike), and two coefficients b, k of the f32 error bound.
+// Once a walk holds a triangle hit at distance tb, a triangle may be skipped only if the
+// reference's f32 test (compute_shader.wgsl:449-481) cannot accept it with a distance <= tb.
 //
 // The bound (derived in DESIGN.md §5.3c). If the f32 test accepts triangle T with
 // distance t, the point o + t d lies within
 //     delta_T = (b_T (t |d| + |o|) + k_T) / c_T,     c_T = |d . N| / (|d| |N|),
 // of T, where b_T and k_T depend only on T's stored record (its f32 calc_normal n may
-// differ from the exact N: |N - n| enters both), the triangle's corners may lie outside
-// its sub-object box by at most what k_T adds, and u = 2^-24:
+// differ from the exact N = ab x ac: |N - n| enters both), the triangle's corners may lie
+// outside its sub-object box by at most what k_T adds, and u = 2^-24:
 //     b_T = (|N - n| + 8u |n| + 32u |ab| |ac|) / |N|
 //     k_T = b_T |a| + (|ab| + |ac|) (|N - n| + 8u |n|) / |N| + excess_T + 2u (|ab| + |ac|)
-// So the ray, which holds that point at parameter t <= tb, enters the node box
-// inflated by delta = max_T delta_T no later than t. Conversely, when the inflated
-// box's entry (a certified lower bound, tri_cone_prunes) lies beyond tb, every
-// triangle below the node that the reference could accept has distance > tb: the
-// node cannot change the walk's lexicographic (distance, sweep position) minimum,
-// ties included (strict). c_T is bounded below from the cone: with psi the angle
-// between d and the axis (folded to [0, pi/2]), c_T >= cos(psi + phi) whenever
-// psi + phi < pi/2. A node whose cone is wider than a hemisphere, or whose
-// triangles have a non-finite or degenerate record, is never pruned: it is walked
-// with box culling alone, which is exact without any bound.
+// So the ray, which holds that point at parameter t <= tb, enters T's leaf box inflated by
+// delta_T no later than t. Conversely, when the inflated box's entry (a certified lower
+// bound) lies beyond tb, the reference cannot accept T at a distance <= tb: T cannot change
+// the walk's lexicographic (distance, sweep position) minimum, ties included (strict).
 //
-// Shared by the device builder (rt_tri_cones_kernel, scene_edit.hip), the walks
+// What carries c_T: a leaf's certificate (TriLeafCert) holds each of its triangles' own
+// normal, so c_T is bounded per triangle. Round 4 first bounded c_T per BVH node with a
+// normal cone over every triangle below; on the BASELINE scenes no cone above the leaves
+// is narrow enough (C3 closed meshes and C5's spiky heightfield face every direction) and
+// the cones pruned 0.00 (C3) / 3.7 (C5) of ~7 / ~225 node visits per ray, so the walks use
+// the leaf certificates alone.
+//
+// Shared by the device builder (rt_tri_leafcert_kernel, scene_edit.hip), the walks
 // (pathtrace.hip) and the CPU exactness harness (tests/cpp/tri_exactness.cpp).
 #pragma once
 
@@ -38,20 +36,7 @@
 #define RT_TC_FN inline
 #endif
 
-struct TriCone {
-    float ax, ay, az;  // cone axis (unit up to f32 rounding)
-    float cos_lo;      // cos(phi + slack), rounded down
-    float sin_hi;      // sin(phi + slack), rounded up
-    float b, k;        // error coefficients (header comment), rounded up
-    uint32_t flags;    // kTriConeValid | kTriConeNarrow
-};
-static_assert(sizeof(TriCone) == 32, "cone record layout");
-
-constexpr uint32_t kTriConeValid = 1u;   // every triangle below has a finite, non-degenerate record
-constexpr uint32_t kTriConeNarrow = 2u;  // phi < pi/2: the cone can bound c_T away from 0
-constexpr uint32_t kTriConePrunable = kTriConeValid | kTriConeNarrow;
-
-// Smallest cone lower bound the walk accepts (below it delta is too large to prune anyway).
+// Smallest lower bound of c_T the walk accepts (below it delta is too large to prune anyway).
 constexpr float kTriConeCMin = 1.0e-4f;
 
 namespace tricone {
@@ -77,7 +62,7 @@ RT_TC_FN float f_up(double v) {
 }
 RT_TC_FN double len3(double x, double y, double z) { return sqrt(x * x + y * y + z * z); }
 
-// Running state of a cone/coefficient build over a node's triangles (double).
+// Running state of a coefficient build over a leaf's triangles (double).
 struct Acc {
     double ax, ay, az;  // axis (unit), valid when n > 0
     double phi;         // half-angle (radians), an upper bound
@@ -98,6 +83,7 @@ RT_TC_FN double angle_between(double x0, double y0, double z0, double x1, double
 // Adds a cone (unit axis x, half-angle p) to acc: the new axis is the sign-aligned
 // sum of the two axes, the new half-angle the larger of (angle to each old axis +
 // its half-angle). Conservative: every direction in either cone is in the result.
+// (A single triangle's Acc holds its unit normal as the axis.)
 RT_TC_FN void acc_add_cone(Acc& acc, double x, double y, double z, double p) {
     if (acc.n == 0u) {
         acc.ax = x;
@@ -171,57 +157,117 @@ RT_TC_FN void acc_add_triangle(Acc& acc, const float a[3], const float ab[3], co
     acc_add_cone(acc, Nx / NN, Ny / NN, Nz / NN, 1e-9);
 }
 
-// A merged node: both children's triangles.
-RT_TC_FN void acc_add_acc(Acc& acc, const Acc& c) {
-    acc.valid = acc.valid && c.valid;
-    acc.b = fmax(acc.b, c.b);
-    acc.k = fmax(acc.k, c.k);
-    if (c.n > 0u) {
-        const uint32_t n = acc.n;
-        acc_add_cone(acc, c.ax, c.ay, c.az, c.phi);
-        acc.n = n + c.n;
-    }
-}
+}  // namespace tricone
 
-// The f32 record. Slack on the angle covers the axis' f32 rounding (<= ~2^-23 rad) and
-// the kernel's evaluation of cos(psi) (tri_cone_prunes).
-RT_TC_FN TriCone acc_record(const Acc& acc) {
-    TriCone r{0.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0u};
-    if (!acc.valid || acc.n == 0u) return r;
-    r.flags = kTriConeValid;
-    r.b = f_up(acc.b * (1.0 + 1e-6));
-    r.k = f_up(acc.k * (1.0 + 1e-6) + 1e-30);
-    const double phi = acc.phi + 1e-6;
-    if (phi < 1.5707963267948966 - 1e-6) {
-        r.flags |= kTriConeNarrow;
-        r.ax = (float)acc.ax;
-        r.ay = (float)acc.ay;
-        r.az = (float)acc.az;
-        r.cos_lo = f_down(cos(phi) - 1e-12);
-        r.sin_hi = f_up(sin(phi) + 1e-12);
-    }
-    return r;
-}
+// ---- Per-triangle certificates of a leaf ("leaf certificates") ----
+//
+// A node's cone must hold every normal below it, and on meshes whose facets face every
+// direction (C5's spiky heightfield: 64% of the nodes a ray enters beyond its hit carry no
+// cone at all) it proves nothing. A leaf holds at most a few triangles, so its record keeps
+// each triangle's own normal instead: 7 octahedral-encoded unit normals (16 + 16 bits,
+// checked at build time to lie within kLeafCertNormalErr of +-N/|N|) and the leaf's error
+// coefficients b, k (bf16, rounded up). The walk bounds c_T from below per triangle and
+// skips every triangle whose own delta_T keeps it beyond tb -- without loading it -- and the
+// whole leaf when all are skipped. Leaves with more than 7 triangles, or an invalid
+// triangle (tri_cone.h's admitted magnitudes), carry no certificate (w[7] = kLeafCertNone).
+// Slots past the leaf's count repeat triangle 0's normal, so they are skipped exactly when
+// triangle 0 is, and "all 7 bits" means "every triangle of the leaf".
+struct TriLeafCert {
+    uint32_t w[8];  // w[j], j < 7: octahedral normal of the leaf's triangle j; w[7]: bf16 b | bf16 k << 16
+};
+static_assert(sizeof(TriLeafCert) == 32, "leaf certificate layout");
 
-// Back to the double state (for a parent's merge): phi from the stored, conservative
-// cos/sin; a record that is not narrow has no usable axis (phi = pi/2 stays pi/2 up).
-RT_TC_FN Acc acc_from_record(const TriCone& r) {
-    Acc a = acc_empty();
-    a.valid = (r.flags & kTriConeValid) != 0u;
-    a.b = r.b;
-    a.k = r.k;
-    a.n = 1u;
-    if (r.flags & kTriConeNarrow) {
-        const double l = len3(r.ax, r.ay, r.az);
-        a.ax = r.ax / l;
-        a.ay = r.ay / l;
-        a.az = r.az / l;
-        a.phi = atan2((double)r.sin_hi, (double)r.cos_lo) + 1e-9;
+constexpr uint32_t kLeafCertNone = 0xffffffffu;
+constexpr uint32_t kLeafCertSlots = 7u;
+constexpr uint32_t kLeafCertAll = (1u << kLeafCertSlots) - 1u;
+// Largest |n_T - (+-v)| allowed between the unit normal and the decoded (unit-scaled) direction;
+// 16-bit octahedral quantization stays under ~1e-4, the builder refuses a record above this.
+constexpr float kLeafCertNormalErr = 0x1p-12f;
+
+// Octahedral decode, exact in f32: every value is a multiple of 2^-15 in [-1, 1]. |v| lies in
+// [1/sqrt(3), 1]; v is not normalised (|d.v| / |d| <= |d.v| / (|d| |v|) is the bound used).
+RT_TC_FN void leafcert_decode(uint32_t q, float& x, float& y, float& z) {
+    const float px = (float)((int)(q & 0xffffu) - 32768) * 0x1p-15f;
+    const float py = (float)((int)(q >> 16) - 32768) * 0x1p-15f;
+    const float pz = (1.0f - fabsf(px)) - fabsf(py);
+    if (pz < 0.0f) {
+        x = copysignf(1.0f - fabsf(py), px);
+        y = copysignf(1.0f - fabsf(px), py);
     } else {
-        a.ax = 1.0;
-        a.phi = 3.2;  // wider than a hemisphere: every merge stays wide
+        x = px;
+        y = py;
     }
-    return a;
+    z = pz;
+}
+
+// bf16 of a non-negative value, rounded up (0xffff: not representable / invalid).
+RT_TC_FN uint32_t leafcert_bf16_up(double v) {
+    if (!(v >= 0.0) || !(v < 1.0e30)) return 0xffffu;
+    uint32_t bits;
+    const float f = tricone::f_up(v);
+    __builtin_memcpy(&bits, &f, 4);
+    if (bits & 0xffffu) bits += 0x10000u;  // positive finite: a larger magnitude
+    return bits >> 16;
+}
+RT_TC_FN float leafcert_bf16(uint32_t h) {
+    const uint32_t bits = h << 16;
+    float f;
+    __builtin_memcpy(&f, &bits, 4);
+    return f;
+}
+
+namespace tricone {
+
+// Encodes the unit direction (x, y, z) (double); returns false when the decoded direction
+// is not within kLeafCertNormalErr (minus a margin for the double evaluation) of it.
+RT_TC_FN bool leafcert_encode(double x, double y, double z, uint32_t& q) {
+    const double s = fabs(x) + fabs(y) + fabs(z);
+    if (!(s > 0.0)) return false;
+    double px = x / s, py = y / s;
+    if (z < 0.0) {
+        const double tx = (1.0 - fabs(py)) * (px >= 0.0 ? 1.0 : -1.0);
+        const double ty = (1.0 - fabs(px)) * (py >= 0.0 ? 1.0 : -1.0);
+        px = tx;
+        py = ty;
+    }
+    long qx = lround(px * 32768.0) + 32768, qy = lround(py * 32768.0) + 32768;
+    qx = qx < 0 ? 0 : qx > 65535 ? 65535 : qx;
+    qy = qy < 0 ? 0 : qy > 65535 ? 65535 : qy;
+    q = (uint32_t)qx | ((uint32_t)qy << 16);
+    float fx, fy, fz;
+    leafcert_decode(q, fx, fy, fz);
+    const double l = len3(fx, fy, fz);
+    if (!(l > 0.5)) return false;
+    const double ex = fx / l - x, ey = fy / l - y, ez = fz / l - z;
+    const double fxn = fx / l + x, fyn = fy / l + y, fzn = fz / l + z;
+    const double e = fmin(len3(ex, ey, ez), len3(fxn, fyn, fzn));
+    return e <= (double)kLeafCertNormalErr * 0.99;
+}
+
+// The certificate of one leaf: its sub-object box [lo, hi] and its n triangles' records.
+RT_TC_FN TriLeafCert leafcert_build(uint32_t n, const float (*a)[3], const float (*ab)[3], const float (*ac)[3],
+                                    const float (*cn)[3], const float lo[3], const float hi[3]) {
+    TriLeafCert c;
+    for (uint32_t j = 0; j < 8u; j++) c.w[j] = 0u;
+    c.w[7] = kLeafCertNone;
+    if (n == 0u || n > kLeafCertSlots) return c;
+    double b = 0.0, k = 0.0;
+    for (uint32_t j = 0; j < n; j++) {
+        Acc acc = acc_empty();
+        acc_add_triangle(acc, a[j], ab[j], ac[j], cn[j], lo, hi);
+        if (!acc.valid) return c;
+        b = fmax(b, acc.b);
+        k = fmax(k, acc.k);
+        if (!leafcert_encode(acc.ax, acc.ay, acc.az, c.w[j])) {
+            c.w[7] = kLeafCertNone;
+            return c;
+        }
+    }
+    for (uint32_t j = n; j < kLeafCertSlots; j++) c.w[j] = c.w[0];
+    const uint32_t hb = leafcert_bf16_up(b * (1.0 + 1e-6)), hk = leafcert_bf16_up(k * (1.0 + 1e-6) + 1e-30);
+    if (hb == 0xffffu || hk == 0xffffu) return c;
+    c.w[7] = hb | (hk << 16);
+    return c;
 }
 
 }  // namespace tricone
@@ -246,26 +292,38 @@ RT_TC_FN TriConeRay tri_cone_ray(float ox, float oy, float oz, float dx, float d
     return r;
 }
 
-// True when the node (cone record c) cannot hold a triangle the reference accepts at a
-// distance <= tb. t1x..z: the culling slab test's per-axis entry parameters of the node box
-// (inflated by the culling margin; rt_bvh_slab.h), aix..z: |1/d| as capped there.
-// Every step rounds toward "do not prune" (DESIGN.md §5.3c).
-RT_TC_FN bool tri_cone_prunes(const TriCone& c, const TriConeRay& r, float tb, float t1x, float t1y, float t1z,
-                              float aix, float aiy, float aiz) {
-    if ((c.flags & kTriConePrunable) != kTriConePrunable || !(r.dlen_hi <= 1.0e5f) || !(r.olen_hi <= 1.0e15f) ||
-        !(r.inv_dlen_lo <= 1.0e5f))
-        return false;
-    // cos(psi) = |d.A| / |d| to within 1e-6 (f32 dot, |A| = 1 +- 2^-23)
-    const float cp = fabsf((r.dx * c.ax + r.dy * c.ay) + r.dz * c.az) * r.inv_dlen_lo;
-    const float cl = fmaxf(cp - 1.0e-6f, 0.0f);
-    const float su = sqrtf(fmaxf(1.0f - cl * cl, 0.0f) + 4.0e-6f);
-    const float clb = (cl * c.cos_lo - su * c.sin_hi) - 1.0e-6f;
-    if (!(clb >= kTriConeCMin) || !(clb >= 4.0f * c.b)) return false;
-    const float num = (c.b * (tb * r.dlen_hi + r.olen_hi) + c.k) * 1.00001f;
-    const float delta = (num / clb) * 1.00001f;
+// The triangles of a leaf (certificate w, as stored) that cannot pass the reference's test
+// at a distance <= tb, as a mask over the 7 slots (kLeafCertAll: the whole leaf). t1x..z: the
+// culling slab test's per-axis entry parameters of the leaf box (inflated by the culling
+// margin; rt_bvh_slab.h), aix..z: |1/d| as capped there. c_T is bounded from the triangle's
+// own normal, with one division per leaf: a triangle is skipped when its delta_T = num / c_T keeps
+// the inflated box's entry beyond tb on some axis a, i.e. when
+//     c_T > num |1/d_a| s / (t1_a - tb s)   for an axis with t1_a > tb s,
+// evaluated with margins that round every step toward "do not skip".
+RT_TC_FN uint32_t tri_leafcert_skips(const uint32_t* w, const TriConeRay& r, float tb, float t1x, float t1y, float t1z,
+                                     float aix, float aiy, float aiz) {
+    if (w[7] == kLeafCertNone || !(r.dlen_hi <= 1.0e5f) || !(r.olen_hi <= 1.0e15f) || !(r.inv_dlen_lo <= 1.0e5f))
+        return 0u;
+    const float b = leafcert_bf16(w[7] & 0xffffu), k = leafcert_bf16(w[7] >> 16);
     const float s = 1.0f + 0x1p-20f;
-    const float nx = t1x - (delta * aix) * s;
-    const float ny = t1y - (delta * aiy) * s;
-    const float nz = t1z - (delta * aiz) * s;
-    return fmaxf(fmaxf(nx, ny), nz) > tb * s;
+    const float tbs = tb * s;
+    const float num = (b * (tb * r.dlen_hi + r.olen_hi) + k) * 1.00001f;
+    // smallest c_T that skips: min over axes entered beyond tb (others give +inf or NaN, ignored)
+    const float gx = t1x - tbs, gy = t1y - tbs, gz = t1z - tbs;
+    float need = INFINITY;
+    if (gx > 0.0f) need = fminf(need, (num * aix * s) / gx);
+    if (gy > 0.0f) need = fminf(need, (num * aiy * s) / gy);
+    if (gz > 0.0f) need = fminf(need, (num * aiz * s) / gz);
+    need = fmaxf(need * 1.0001f, fmaxf(kTriConeCMin, 4.0f * b));
+    if (!(need < 1.0f)) return 0u;
+    // c_T >= |d.v| / |d| - kLeafCertNormalErr (|v| <= 1), the dot's rounding in the 1e-6
+    const float thr = need + kLeafCertNormalErr + 1.0e-6f;
+    uint32_t m = 0u;
+    for (uint32_t j = 0; j < kLeafCertSlots; j++) {
+        float vx, vy, vz;
+        leafcert_decode(w[j], vx, vy, vz);
+        const float cp = fabsf((r.dx * vx + r.dy * vy) + r.dz * vz) * r.inv_dlen_lo;
+        if (cp * 0.999999f > thr) m |= 1u << j;
+    }
+    return m;
 }

@@ -25,10 +25,6 @@
 #endif
 
 constexpr uint32_t kTriQLastLeaf = 0x40000000u;  // leaf link word: the walk ends after this leaf
-// Either link word: the node's certified-pruning record (tri_cone.h) holds a narrow cone, so a
-// walk entering it beyond its best hit reads that record; clear = it cannot be pruned by
-// distance, and the record is not read. Set by rt_tri_cone_flags_kernel after the records.
-constexpr uint32_t kTriQNarrow = 0x20000000u;
 constexpr uint32_t kTriWalkEnd = 0x7fffffffu;     // a node index past every layout
 
 struct TriQGrid {

@@ -359,6 +359,13 @@ class Renderer:
         N.check(self._ctx, self._lib.rt_debug_counters(self._ctx, v, n), self._lib)
         return list(v)
 
+    def check_leaf_certificates(self) -> tuple:
+        """(mismatches, valid, total): the device's leaf certificates re-derived on the host from
+        the device's own leaf records, sub-objects and triangles (include/rt_abi.h)."""
+        m, v, t = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(self._ctx, self._lib.rt_debug_check_leaf_certificates(self._ctx, m, v, t), self._lib)
+        return m.value, v.value, t.value
+
     def set_tile_schedule(self, schedule: int) -> None:
         """0: claim tiles in index order; 1: cost-ordered (most rays of an earlier launch first)."""
         self._call("rt_set_tile_schedule", schedule)

@@ -98,13 +98,12 @@ static const std::vector<SphereBvhNode>* g_oct = nullptr;
 static const std::vector<uint32_t>* g_qoct = nullptr;
 static float g_prune = 0.0f;
 static long g_prune_nodes = 0, g_prune_tests = 0;
-// certified pruning (tri_cone.h): cone records in base-node order, and per layout position
-// its base node (order_bvh_by_octant's src)
-static const std::vector<TriCone>* g_cones = nullptr;
-static const std::vector<uint32_t>* g_src = nullptr;
 static bool g_heur_count = false;
 static long g_heur_miss = 0;
-static long g_exact_nodes = 0, g_exact_tests = 0, g_exact_checks = 0, g_exact_pruned = 0;
+static long g_exact_nodes = 0, g_exact_tests = 0;
+// certified pruning (tri_cone.h): the leaf certificates, per prim (the kernel's default walk)
+static const std::vector<TriLeafCert>* g_lcert = nullptr;
+static long g_lcert_leaves = 0, g_lcert_skipped = 0, g_lcert_tris = 0;
 
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
@@ -140,20 +139,21 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
         } else if (!g_lazy) {
             g_nodes++;
         }
-        if (g_cones) g_exact_nodes++;
+        if (g_lcert) g_exact_nodes++;
         float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
         slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
         bool hit = nt <= ft && ft >= 0.0f && nt <= limit;
-        if (g_cones && hit && best != F32_MAX_ && nt > best) {
-            // certified pruning: the node's per-axis entries (the slab test's), then tri_cone_prunes
-            g_exact_checks++;
+        uint32_t skip = 0u;  // leaf certificate: triangles proven beyond the best hit
+        if (g_lcert && hit && nd.leaf != kSphereBvhInternal && best != F32_MAX_ && nt > best) {
             const float t1x = fminf(fmaf(nd.bmin[0], sr.ix, sr.lx), fmaf(nd.bmax[0], sr.ix, sr.hx));
             const float t1y = fminf(fmaf(nd.bmin[1], sr.iy, sr.ly), fmaf(nd.bmax[1], sr.iy, sr.hy));
             const float t1z = fminf(fmaf(nd.bmin[2], sr.iz, sr.lz), fmaf(nd.bmax[2], sr.iz, sr.hz));
-            const TriCone& cone = (*g_cones)[g_src ? (*g_src)[node] : node];
-            if (tri_cone_prunes(cone, tcr, best, t1x, t1y, t1z, fabsf(sr.ix), fabsf(sr.iy), fabsf(sr.iz))) {
+            skip = tri_leafcert_skips((*g_lcert)[nd.leaf & 0xffffffu].w, tcr, best, t1x, t1y, t1z, fabsf(sr.ix),
+                                      fabsf(sr.iy), fabsf(sr.iz));
+            g_lcert_leaves++;
+            if (skip == kLeafCertAll) {
                 hit = false;
-                g_exact_pruned++;
+                g_lcert_skipped++;
             }
         }
         if (hit && nd.leaf != kSphereBvhInternal) {
@@ -170,9 +170,13 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
             }
             if (rib(o, inv, OB.min_bounds, OB.max_bounds) && (lazy || rib(o, inv, s.min_bounds, s.max_bounds))) {
                 for (uint32_t j = 0; j < count; j++) {
+                    if ((skip >> j) & 1u) {
+                        g_lcert_tris++;
+                        continue;
+                    }
                     if (!g_q && !g_lazy) g_tests++;
                     if (g_prune != 0.0f) g_prune_tests++;
-                    if (g_cones) g_exact_tests++;
+                    if (g_lcert) g_exact_tests++;
                     uint32_t ti = first + j, seq = p.seq_base + j;
                     const rt_scene_triangle& t = tr[ti];
                     V cn = ld(t.calc_normal);
@@ -345,38 +349,31 @@ int main(int argc, char** argv) {
                 }
         }
     }
-    // cone records (tri_cone.h), children before parents (reverse pre-order)
-    std::vector<TriCone> cones(A.nodes.size());
-    {
-        std::vector<tricone::Acc> acc(A.nodes.size());
-        for (size_t ii = A.nodes.size(); ii-- > 0;) {
-            const SphereBvhNode& nd = A.nodes[ii];
-            tricone::Acc c = tricone::acc_empty();
-            if (nd.leaf != kSphereBvhInternal) {
-                const SubObjectPrim& p = A.prims[nd.leaf & 0xffffffu];
-                const rt_sub_object_info& sbi = sb[p.sub];
-                float lo[3], hi[3];
-                for (int k = 0; k < 3; k++) {
-                    lo[k] = fminf(sbi.min_bounds[k], sbi.max_bounds[k]);
-                    hi[k] = fmaxf(sbi.min_bounds[k], sbi.max_bounds[k]);
-                }
-                for (uint32_t j = 0; j < sbi.triangle_count; j++) {
-                    const rt_scene_triangle& t = tr[sbi.first_triangle_index + j];
-                    tricone::acc_add_triangle(c, t.a, t.edge_ab, t.edge_ac, t.calc_normal, lo, hi);
-                }
-                if (c.n == 0u) c.valid = false;
-            } else {
-                c = tricone::acc_from_record(cones[ii + 1]);
-                tricone::acc_add_acc(c, tricone::acc_from_record(cones[A.nodes[ii + 1].skip]));
-            }
-            cones[ii] = tricone::acc_record(c);
+    // leaf certificates, per prim (rt_tri_leafcert_kernel derives them the same way)
+    std::vector<TriLeafCert> lcert(A.prims.size());
+    long lcert_valid = 0;
+    for (size_t pi = 0; pi < A.prims.size(); pi++) {
+        const rt_sub_object_info& sbi = sb[A.prims[pi].sub];
+        float lo[3], hi[3];
+        for (int k = 0; k < 3; k++) {
+            lo[k] = fminf(sbi.min_bounds[k], sbi.max_bounds[k]);
+            hi[k] = fmaxf(sbi.min_bounds[k], sbi.max_bounds[k]);
         }
+        const uint32_t cnt = sbi.triangle_count <= kLeafCertSlots ? sbi.triangle_count : 0u;
+        float ta[kLeafCertSlots][3], tab[kLeafCertSlots][3], tac[kLeafCertSlots][3], tcn[kLeafCertSlots][3];
+        for (uint32_t j = 0; j < cnt; j++) {
+            const rt_scene_triangle& t = tr[sbi.first_triangle_index + j];
+            memcpy(ta[j], t.a, 12);
+            memcpy(tab[j], t.edge_ab, 12);
+            memcpy(tac[j], t.edge_ac, 12);
+            memcpy(tcn[j], t.calc_normal, 12);
+        }
+        lcert[pi] = tricone::leafcert_build(cnt, ta, tab, tac, tcn, lo, hi);
+        lcert_valid += lcert[pi].w[7] != kLeafCertNone;
     }
-    long narrow = 0;
-    for (const TriCone& c : cones) narrow += (c.flags & kTriConePrunable) == kTriConePrunable;
     std::vector<SphereBvhNode> oct;
-    std::vector<uint32_t> qoct, src;
-    order_bvh_by_octant(A.nodes, &oct, false, &src);
+    std::vector<uint32_t> qoct;
+    order_bvh_by_octant(A.nodes, &oct, false, nullptr);
     if (g_grid.valid) {
         qoct.resize(4 * oct.size());
         for (size_t i = 0; i < oct.size(); i++) {
@@ -412,12 +409,10 @@ int main(int argc, char** argv) {
             h = a;
         }
         g_prune = 0.0f;
-        // the certified walk (tri_cone.h) over the same layouts
-        g_cones = &cones;
-        g_src = oct.empty() ? nullptr : &src;
+        // the certified walk (tri_cone.h leaf certificates) over the same layouts
+        g_lcert = &lcert;
         Res x = accel(A, ob, sb, tr, o, d, scale);
-        g_cones = nullptr;
-        g_src = nullptr;
+        g_lcert = nullptr;
         g_oct = nullptr;
         g_qoct = nullptr;
         g_q = nullptr;
@@ -442,8 +437,9 @@ int main(int argc, char** argv) {
            w_max_stack);
     printf("qnodes %d %.2f\n", g_grid.valid ? 1 : 0, (double)g_qnodes / n);
     printf("prune %.2f %.2f\n", (double)g_prune_nodes / n, (double)g_prune_tests / n);
-    printf("certified %.2f %.2f %.2f %.2f %ld %zu\n", (double)g_exact_nodes / n, (double)g_exact_tests / n,
-           (double)g_exact_checks / n, (double)g_exact_pruned / n, narrow, cones.size());
+    printf("certified %.2f %.2f %.2f %.2f %.2f %ld %zu\n", (double)g_exact_nodes / n, (double)g_exact_tests / n,
+           (double)g_lcert_leaves / n, (double)g_lcert_skipped / n, (double)g_lcert_tris / n, lcert_valid,
+           lcert.size());
     printf("heuristic_misses %ld\n", g_heur_miss);
     return 0;
 }

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.rt_abi_version() == 9
+    assert native_lib.rt_abi_version() == 10
 
 
 def test_library_built_from_these_sources(native_lib):

@@ -480,6 +480,18 @@ def test_gpu_triangle_pruning(gpu, oracle_lib, monkeypatch, prune, octants, prim
     assert_same(acc, out, n, acc_o, out_o, n_o)
 
 
+def test_gpu_leaf_certificates_match_host(gpu):
+    """The leaf certificates the device builds (rt_tri_leafcert_kernel) are bit for bit the
+    host's (tri_cone.h, the CPU harness's builder), and every C5 leaf carries one."""
+    scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
+    with Renderer(scene) as r:
+        r.set_triangle_pruning(1)
+        r.compute_frame(bounces)
+        r.synchronize()
+        mism, valid, total = r.check_leaf_certificates()
+        assert total == len(scene.flatten()[1]) and mism == 0 and valid == total, (mism, valid, total)
+
+
 @pytest.mark.parametrize("config,kw,frames", [
     ("c5_heightfield", {}, 6),
     ("c3_chess", {}, 20),

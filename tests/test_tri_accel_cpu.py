@@ -187,18 +187,21 @@ def test_adversarial_grazing_rays_certified_pruning(harness, tmp_path, seed, h_r
     misses = int(line(out, "heuristic_misses")[0])
     if c_range[1] <= 1e-5:
         assert misses > 0  # the heuristic slack is not exact: a ray it gets wrong
-    nodes, tests, checks, pruned, narrow, total = line(out, "certified")
-    assert int(narrow) == int(total)  # a flat grid: every cone is narrow
+    nodes, tests, checked, skipped, tris_skipped, valid, total = line(out, "certified")
+    assert int(valid) == int(total)  # every leaf of the grid carries a certificate
     if c_range[1] >= 1e-3:
-        assert float(pruned) > 0  # and where the bound allows, the certified walk does prune
+        assert float(skipped) > 0  # and where the bound allows, the certified walk does skip leaves
 
 
 def test_certified_pruning_real_scenes(harness, tmp_path):
-    """The certified walk on C3's chess scene with random rays: exact, and cone records for every node."""
+    """The certified walk on C3's chess scene with random rays: exact, a certificate for every
+    leaf, and fewer triangle tests than box culling."""
     scene, _ = build_config("c3_chess", width=16, height=16, env_size=(16, 8), texture_size=(8, 8))
     objs, subs, tris = scene.flatten()
     rays = random_rays(np.random.default_rng(7), 30000, [-12, -8, -12], [12, 8, 12])
     out = run(harness, tmp_path, objs, subs, tris, rays)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
-    nodes, tests, checks, pruned, narrow, total = line(out, "certified")
-    assert 0 < int(narrow) < int(total)
+    nodes, tests, checked, skipped, tris_skipped, valid, total = line(out, "certified")
+    assert int(valid) == int(total)
+    box_tests = float(out.stdout.splitlines()[0].split()[3])
+    assert float(skipped) > 0 and float(tests) < box_tests

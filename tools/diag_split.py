@@ -34,10 +34,11 @@ for name in argv or list(SIZES):
         r.reset_ray_count()
         for _ in range(3 * fb):
             r.compute_frame(bounces)
-        c = r.debug_counters(20)
+        c = r.debug_counters(24)
         rays = r.ray_count()
     total, trav, steps, it, step_lanes, shade, refill, setup, leaf_cyc, leaf_steps = c[:10]
     sh_pass, sh_lanes, miss, glass, spec, su_pass, su_lanes = c[12:19]
+    cert_checks, cert_leaves, cert_tris = c[19:22]  # leaf certificates (certified pruning)
     trav_occ = step_lanes / max(steps, 1) / 64
     shade_occ = sh_lanes / max(sh_pass, 1) / 64
     setup_occ = su_lanes / max(su_pass, 1) / 64
@@ -51,6 +52,8 @@ for name in argv or list(SIZES):
                       "cycles_per_ray": total / rays, "steps_per_ray": steps / rays,
                       "lanes_per_step": step_lanes / max(steps, 1), "outer_iters_per_ray": it / rays,
                       "leaf_share": leaf_cyc / total, "leaf_steps_per_ray": leaf_steps / rays,
+                      "leaf_certificates_per_ray": {"checked": cert_checks / rays, "leaves_skipped": cert_leaves / rays,
+                                                    "triangles_skipped": cert_tris / rays},
                       "occupancy": {"traversal": trav_occ, "shading": shade_occ, "setup": setup_occ},
                       "inactive_lane_share_by_phase": idle,
                       "shaded_lanes": {"sky_miss": miss / max(sh_lanes, 1), "hit_glass": glass / hits,
