@@ -107,17 +107,21 @@ constexpr uint32_t kQueueStride = 64;
 // (measured: sphere scenes 8, C2 slower at 12+; triangle accelerator in LDS
 // 24, C3/C4 -2%; in global memory 32, C5 -10%; with the pruned octant walk of round 3,
 // 48: C5 5.95 -> 5.72 ms, profiles/r03_ah/knobs_c5b.jsonl; C3 unchanged at 24-32).
-uint32_t trav_threshold_for(int lds_mode, bool tris) {
+// certified: walks from global memory with the certified pruning, whose
+// traces visit the box-culling node set (about twice the relative slack's): they return to
+// shading later and batch their leaves earlier (C5 13.0 -> 11.1 ms per frame at 56 / 3,
+// profiles/r04_f/ab.jsonl; the slack keeps round 3's 48 / 5).
+uint32_t trav_threshold_for(int lds_mode, bool tris, bool certified) {
     if (!tris) return 8;
-    return lds_mode == 2 ? 24 : 48;
+    return lds_mode == 2 ? 24 : certified ? 56 : 48;
 }
 // Triangle scenes test deferred leaves once this many eighths of the
 // traversing lanes hold one (pathtrace.hip, leaf_step): later for an LDS
 // accelerator, earlier when the leaf's loads go to global memory anyway.
 // Re-measured with 20-frame launches (profiles/archive/r02_s4/r02_s4k, r02_s4l):
 // mode 2 at 6 (C4 -2.3% against 7, C3 within 0.3%), modes 0/1 at 5 (C5 -2.9%
-// against 6; 4 and 3 within 0.4% of 5).
-uint32_t leaf_batch_for(int lds_mode) { return lds_mode == 2 ? 6 : 5; }
+// against 6; 4 and 3 within 0.4% of 5); certified walks at 3 (above).
+uint32_t leaf_batch_for(int lds_mode, bool certified) { return lds_mode == 2 ? 6 : certified ? 3 : 5; }
 // Instances with the triangle accelerator in global memory: the same once the
 // tile queue is empty, when the wave goes back to shading only if some lane
 // has finished and after at least kDefaultDrainMinSteps traversal steps
@@ -1450,8 +1454,9 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.sphere_nodes = layouts * ctx->n_nodes;
     ka.sphere_octant_stride = layouts == 8 ? ctx->n_nodes : 0u;
     ka.sphere_boxes_ordered = (layouts == 8 && ctx->sphere_boxes_ordered && !tris) ? 1u : 0u;
-    ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris);
-    ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode);
+    const bool certified = tris && !wide && mode <= 1 && ka.tri_accel && ctx->tri_prune_mode == 1;
+    ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris, certified);
+    ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode, certified);
     // walks of the binary triangle accelerator from global memory read its direction-ordered
     // layouts (8 x tri_nodes positions, 32-B and 16-B quantized copies), else the single one
     ka.tri_qnodes = nullptr;

@@ -104,6 +104,7 @@ static long g_exact_nodes = 0, g_exact_tests = 0;
 // certified pruning (tri_cone.h): the leaf certificates, per prim (the kernel's default walk)
 static const std::vector<TriLeafCert>* g_lcert = nullptr;
 static long g_lcert_leaves = 0, g_lcert_skipped = 0, g_lcert_tris = 0;
+static uint32_t g_subtree_max = 0;
 
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
@@ -144,6 +145,24 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
         slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
         bool hit = nt <= ft && ft >= 0.0f && nt <= limit;
         uint32_t skip = 0u;  // leaf certificate: triangles proven beyond the best hit
+        if (g_lcert && g_subtree_max && hit && nd.leaf == kSphereBvhInternal && best != F32_MAX_ && nt > best) {
+            // experiment (TRI_SUBTREE_MAX): an ideal certificate for small subtrees -- every leaf's
+            // own certificate evaluated on this node's box entry
+            uint32_t tri_count = 0;
+            for (uint32_t q = node; q < nd.skip && q < n; q++)
+                if (NS[q].leaf != kSphereBvhInternal) tri_count += sb[A.prims[NS[q].leaf & 0xffffffu].sub].triangle_count;
+            if (tri_count <= g_subtree_max) {
+                const float t1x = fminf(fmaf(nd.bmin[0], sr.ix, sr.lx), fmaf(nd.bmax[0], sr.ix, sr.hx));
+                const float t1y = fminf(fmaf(nd.bmin[1], sr.iy, sr.ly), fmaf(nd.bmax[1], sr.iy, sr.hy));
+                const float t1z = fminf(fmaf(nd.bmin[2], sr.iz, sr.lz), fmaf(nd.bmax[2], sr.iz, sr.hz));
+                bool all = true;
+                for (uint32_t q = node; q < nd.skip && q < n && all; q++)
+                    if (NS[q].leaf != kSphereBvhInternal)
+                        all = tri_leafcert_skips((*g_lcert)[NS[q].leaf & 0xffffffu].w, tcr, best, t1x, t1y, t1z,
+                                                 fabsf(sr.ix), fabsf(sr.iy), fabsf(sr.iz)) == kLeafCertAll;
+                if (all) hit = false;
+            }
+        }
         if (g_lcert && hit && nd.leaf != kSphereBvhInternal && best != F32_MAX_ && nt > best) {
             const float t1x = fminf(fmaf(nd.bmin[0], sr.ix, sr.lx), fmaf(nd.bmax[0], sr.ix, sr.hx));
             const float t1y = fminf(fmaf(nd.bmin[1], sr.iy, sr.ly), fmaf(nd.bmax[1], sr.iy, sr.hy));
@@ -319,6 +338,7 @@ int main(int argc, char** argv) {
     auto rays = load<float>(argv[4]);
     float scale = argc > 5 ? (float)atof(argv[5]) : 1.0e-5f;
     g_heur_count = getenv("TRI_HEUR_COUNT") != nullptr;
+    if (getenv("TRI_SUBTREE_MAX")) g_subtree_max = (uint32_t)atoi(getenv("TRI_SUBTREE_MAX"));
     TriangleAccel A;
     build_triangle_accel(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), &A);
     // the wide accelerator, with compact leaves from the records in the kernel's 64-B layout
