@@ -182,6 +182,16 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
     return TriGeom{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w)};
 }
 
+// Leaf certificates in the walks (certified pruning, tri_leaf_skips): walks from global memory
+// always carry the test; walks of the LDS-resident accelerator (mode 2) only when built with
+// RT_LEAFCERT_LDS=1. Off by default: the code costs the LDS-resident instances registers, more
+// than the triangle tests it skips save (C3 0.304 ms per frame without it, 0.335 compiled in
+// and off, 0.362 on; a variant testing at the leaf with the certificates staged in LDS measured
+// 0.297 compiled in and off, 0.312 on, against 0.269). Mode 2 then walks with
+// box culling, exact without any bound.
+#ifndef RT_LEAFCERT_LDS
+#define RT_LEAFCERT_LDS 0
+#endif
 // The LDS vertex table (mode 2, compact_tri): build switch, off by default --
 // compiled in, its code cost the LDS-resident instances more registers than its smaller
 // triangle reads saved (C3 0.304 -> 0.317 ms per frame with it off at run time, 0.349 on).
@@ -403,6 +413,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
 // (a new best hit or a NaN distance); if that test fails, no triangle of the leaf counts --
 // exactly as the reference, which tests none of them then. Most leaves change nothing, so
 // their sub-object record is never read.
+
 // `pending`: the leaf record's index, with the mask of triangles its certificate skips in
 // bits 24-30 (tri_leaf_skips; they are not loaded).
 template <bool kLazySub = false>
@@ -623,17 +634,8 @@ constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
 template <int kMode, bool kTris>
 constexpr bool kDrainDecouple = kTris && kMode < 2;
 
-// Leaf certificates in the walks (certified pruning, tri_leaf_skips): walks from global memory
-// always carry the test; walks of the LDS-resident accelerator (mode 2) only when built with
-// RT_LEAFCERT_LDS=1 (off by default: the certificate is a lane-distinct global load where the
-// triangles it saves are LDS reads, and the code costs registers -- C3 0.304 ms per frame
-// without it, 0.335 compiled in and off, 0.362 on). Mode 2 then walks with
-// box culling, exact without any bound.
-#ifndef RT_LEAFCERT_LDS
-#define RT_LEAFCERT_LDS 0
-#endif
 template <int kMode>
-constexpr bool kCertWalk = kMode <= 1 || RT_LEAFCERT_LDS;
+constexpr bool kCertWalk = kMode <= 1 || RT_LEAFCERT_LDS == 1;
 
 
 // kCert: the walk reads leaf certificates (tri_leaf_skips) when ka.tri_leafcert is set.
