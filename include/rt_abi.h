@@ -299,11 +299,12 @@ RT_API int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out);
  * reference sweeps every object -> sub-object -> triangle
  * (compute_shader.wgsl:422-517); the accelerator replaces the sweep by a walk that
  * culls boxes the ray misses, which is exact by construction.
- * mode 1 (the default): certified pruning -- once a triangle is hit at t, a node is
- * also skipped when its box, inflated by a derived bound on the f32 error of the
- * reference's triangle test over the node's triangles (a normal cone per node plus
- * two per-record coefficients, rt_tri_cone.h), is entered beyond t; exact by
- * construction. 0: box culling only. 2: the relative slack of
+ * mode 1 (the default): certified pruning -- once a triangle is hit at t, a triangle
+ * of a leaf entered beyond t is also skipped (not loaded) when the leaf box, inflated
+ * by a derived bound on the f32 error of the reference's triangle test for that
+ * triangle (its own normal and two coefficients, the leaf's certificate, tri_cone.h;
+ * ABI 10), is entered beyond t; exact by construction. Walks of an
+ * LDS-resident accelerator use box culling in this mode. 0: box culling only. 2: the relative slack of
  * ABI 8 (skip boxes entered beyond t * (1 + 1/64) + 2^-10 (|o| + extent) / |d|):
  * faster on scenes without coherent normals, NOT exact -- rays nearly in a
  * triangle's plane near their origin can get another triangle than the sweep's
