@@ -192,6 +192,11 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
 #ifndef RT_LEAFCERT_LDS
 #define RT_LEAFCERT_LDS 0
 #endif
+// Walks from global memory: the certificate test made in the leaf batch (node_step records the
+// leaf box's gap beyond the best hit) instead of in node_step (build switch for A/B).
+#ifndef RT_LEAFCERT_DEFER
+#define RT_LEAFCERT_DEFER 0
+#endif
 // The LDS vertex table (mode 2, compact_tri): build switch, off by default --
 // compiled in, its code cost the LDS-resident instances more registers than its smaller
 // triangle reads saved (C3 0.304 -> 0.317 ms per frame with it off at run time, 0.349 on).
@@ -281,6 +286,9 @@ struct TraceState {
     uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf;
                        // wide walk: leaf_base << 4 | mask of the node's leaves still to test
     uint32_t sp;       // wide walk: stack entries in use
+#if RT_LEAFCERT_DEFER
+    float cert_gap;    // deferred leaf certificate test (pending bit 24): the leaf box's gap beyond the best hit
+#endif
     bool nan_hit;
     SphereHit sph;
     TriHit tri;
@@ -419,7 +427,19 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
 template <bool kLazySub = false>
 __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
                                          uint32_t pending) {
-    const uint32_t prim = pending & 0xffffffu, skip = pending >> 24;
+    const uint32_t prim = pending & 0xffffffu;
+#if RT_LEAFCERT_DEFER
+    uint32_t skip = 0u;
+    if ((pending >> 24) & 1u) {  // the certificate test deferred by node_step
+        const uint4* rec = reinterpret_cast<const uint4*>(ka.tri_leafcert + prim);
+        const uint4 c0 = rec[0], c1 = rec[1];
+        const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        skip = tri_leafcert_skips_gap(w, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), ts.tri.t, ts.cert_gap);
+        if (skip == kLeafCertAll) return;
+    }
+#else
+    const uint32_t skip = pending >> 24;
+#endif
     const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base, range
     const RtObject& ob = sv.obj[pr.x];
     if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) return;
@@ -680,8 +700,21 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     if constexpr (kTris && !kWide && kCert) {
         // certified pruning: a leaf whose box is entered beyond the best triangle hit
         if (tri && hit && leaf != 0xffffffffu && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max) {
+#if RT_LEAFCERT_DEFER
+            // the gap of the leaf box beyond the best hit, for the leaf batch's certificate test
+            if (ts.pending == kNoLeaf) {
+                const float tbs = ts.tri.t * (1.0f + 0x1p-20f);
+                const SlabRay& sr = ts.slab;
+                const float gx = (fminf(fmaf(lo.x, sr.ix, sr.lx), fmaf(hi.x, sr.ix, sr.hx)) - tbs) * fabsf(d.x);
+                const float gy = (fminf(fmaf(lo.y, sr.iy, sr.ly), fmaf(hi.y, sr.iy, sr.hy)) - tbs) * fabsf(d.y);
+                const float gz = (fminf(fmaf(lo.z, sr.iz, sr.lz), fmaf(hi.z, sr.iz, sr.hz)) - tbs) * fabsf(d.z);
+                ts.cert_gap = fmaxf(fmaxf(gx, gy), gz) * (1.0f - 0x1p-20f);
+                skip = ts.cert_gap > 0.0f ? 1u : 0u;  // (bit 24 of pending: test deferred)
+            }
+#else
             skip = tri_leaf_skips(ka, leaf & 0xffffffu, ts.slab, o, d, ts.tri.t, lo, hi);
             if (skip == kLeafCertAll) hit = false;
+#endif
 #ifdef RT_DIAG
             atomicAdd(ka.diag + 19, 1ull);  // certificate checks, leaves skipped, triangles skipped
             if (skip == kLeafCertAll) atomicAdd(ka.diag + 20, 1ull);
@@ -2034,7 +2067,11 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
                     }
                     const bool any = __ballot(hit) != 0;
                     if (any && leaf != 0xffffffffu && hit) {
+#if RT_LEAFCERT_DEFER
+                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);  // (bit 24 means "deferred" there)
+#else
                         tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, (leaf & 0xffffffu) | (skip << 24));
+#endif
                         ts.limit = tri_limit(sv, ka, o, ts);
                     }
                     node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);

@@ -327,3 +327,27 @@ RT_TC_FN uint32_t tri_leafcert_skips(const uint32_t* w, const TriConeRay& r, flo
     }
     return m;
 }
+
+// The same test with the box entry condensed into one distance, for walks that defer it to
+// their leaf batches: gap = max over axes of (t1_a - tb0 s) |d_a| (1 - 2^-20), the distance
+// (lower bound) by which the leaf box's inflated-slab entry lies beyond tb0 >= tb along some
+// axis; with delta_T < gap that axis still enters beyond tb. (|d_a| <= 1 / |1/d_a| as capped,
+// up to the rounding the 2^-20 covers.)
+RT_TC_FN uint32_t tri_leafcert_skips_gap(const uint32_t* w, const TriConeRay& r, float tb, float gap) {
+    if (w[7] == kLeafCertNone || !(gap > 0.0f) || !(r.dlen_hi <= 1.0e5f) || !(r.olen_hi <= 1.0e15f) ||
+        !(r.inv_dlen_lo <= 1.0e5f))
+        return 0u;
+    const float b = leafcert_bf16(w[7] & 0xffffu), k = leafcert_bf16(w[7] >> 16);
+    const float num = (b * (tb * r.dlen_hi + r.olen_hi) + k) * 1.00001f;
+    const float need = fmaxf((num / gap) * 1.0001f, fmaxf(kTriConeCMin, 4.0f * b));
+    if (!(need < 1.0f)) return 0u;
+    const float thr = need + kLeafCertNormalErr + 1.0e-6f;
+    uint32_t m = 0u;
+    for (uint32_t j = 0; j < kLeafCertSlots; j++) {
+        float vx, vy, vz;
+        leafcert_decode(w[j], vx, vy, vz);
+        const float cp = fabsf((r.dx * vx + r.dy * vy) + r.dz * vz) * r.inv_dlen_lo;
+        if (cp * 0.999999f > thr) m |= 1u << j;
+    }
+    return m;
+}
