@@ -303,10 +303,15 @@ def main() -> int:
         r.set_timing(True)
         barrier_sync()
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            r.compute_frame(bounces)
-            if rank == 0 and args.steps >= 50 and (i + 1) % 50 == 0:
-                log(f"step {i + 1}/{args.steps}")
+        # the steps' compute_frame calls, a launch's worth per C call (rt_submit_frames: the
+        # host loop a native caller runs, without a Python round trip per frame)
+        done = 0
+        while done < args.steps:
+            n = min(frame_batch, args.steps - done)
+            r.submit_frames(bounces, n)
+            done += n
+            if rank == 0 and args.steps >= 50 and done % 50 < n:
+                log(f"step {done}/{args.steps}")
         t_gather_in_region = 0.0
         if gathered:
             # the frame assembled on rank 0 (pack -> RCCL gather -> unpack), stream-ordered

@@ -231,6 +231,13 @@ RT_API int rt_compute_frame(rt_ctx* ctx, uint32_t bounces);
  * per step. frames >= 1. Asynchronous. */
 RT_API int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
 
+/* `count` consecutive rt_compute_frame calls made in one call (new, ABI 10): the loop a
+ * native host runs around rt_compute_frame, for callers whose per-call overhead is not
+ * negligible (the Python mirror: ~2 us per ctypes call, 40 us per 20-frame bench step at
+ * N GPUs, where a rank's launch is 0.7 ms). Frame batching applies exactly as to the single
+ * calls; results are identical. Stops at the first failing call. Asynchronous. */
+RT_API int rt_submit_frames(rt_ctx* ctx, uint32_t bounces, uint32_t count);
+
 /* Frame batching (new; the reference submits one dispatch per compute_frame,
  * src/renderer.rs:238-249, and wgpu runs it later, asynchronously). With
  * max_frames > 1, rt_compute_frame queues its frame (Params and k advance as

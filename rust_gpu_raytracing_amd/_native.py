@@ -105,6 +105,7 @@ SIGNATURES = {
     "rt_dispatch": (ctypes.c_int, [_P, _U32]),
     "rt_compute_frame": (ctypes.c_int, [_P, _U32]),
     "rt_compute_frames": (ctypes.c_int, [_P, _U32, _U32]),
+    "rt_submit_frames": (ctypes.c_int, [_P, _U32, _U32]),
     "rt_set_frame_batch": (ctypes.c_int, [_P, _U32]),
     "rt_frame_batch": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "rt_flush": (ctypes.c_int, [_P]),

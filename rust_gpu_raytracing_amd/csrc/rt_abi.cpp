@@ -1709,6 +1709,15 @@ int rt_compute_frame(rt_ctx* ctx, uint32_t bounces) {
     return flush_frames(ctx);
 }
 
+int rt_submit_frames(rt_ctx* ctx, uint32_t bounces, uint32_t count) {
+    if (!ctx) return RT_E_INVALID;
+    for (uint32_t i = 0; i < count; i++) {
+        const int rc = rt_compute_frame(ctx, bounces);
+        if (rc) return rc;
+    }
+    return RT_OK;
+}
+
 int rt_set_frame_batch(rt_ctx* ctx, uint32_t max_frames) {
     RT_ENTER(ctx);
     if (max_frames == 0 || max_frames > kMaxFrameBatch)

@@ -229,6 +229,11 @@ class Renderer:
         rt_compute_frames in include/rt_abi.h). Asynchronous."""
         self._call("rt_compute_frames", bounces, frames)
 
+    def submit_frames(self, bounces: int = REFERENCE_BOUNCES, count: int = 1) -> None:
+        """``count`` compute_frame calls in one C call (rt_submit_frames: the host loop a native
+        caller runs, without a ctypes round trip per frame). Asynchronous."""
+        self._call("rt_submit_frames", bounces, count)
+
     def set_frame_batch(self, max_frames: int) -> None:
         """rt_set_frame_batch: up to ``max_frames`` queued compute_frame calls per launch."""
         self._call("rt_set_frame_batch", max_frames)

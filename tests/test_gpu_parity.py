@@ -367,7 +367,8 @@ def test_gpu_unpack_all_ranks_one_launch(gpu, accumulate, world, dst):
 def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, batch, parallel, kw):
     """rt_set_frame_batch: queued frames launched F at a time give, after every
     observable point, exactly the single-frame sequence (the oracle's): a readback
-    in the middle of a batch, a bounce change, and a tail shorter than F. Both batch
+    in the middle of a batch, a bounce change, and a tail shorter than F (frames queued
+    one call at a time and through rt_submit_frames). Both batch
     kernels: frame-parallel (a queue unit per (frame, tile), lights resolved in order,
     the default) and RT_FRAME_PARALLEL=0 (each pixel's frames back to back on a lane)."""
     monkeypatch.setenv("RT_FRAME_PARALLEL", parallel)
@@ -382,8 +383,7 @@ def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, 
         assert r.accumulation_index == (batch if accumulate else 1)
         mid = r.read_accumulation(), r.read_output(), r.ray_count()  # flushes the partial batch
         assert r.frame_batch() == (batch, 0)
-        for f in range(batch + 1):  # a full batch, then one queued frame
-            r.compute_frame(bounces)
+        r.submit_frames(bounces, batch + 1)  # a full batch, then one queued frame (rt_submit_frames)
         r.compute_frame(bounces + 1)  # bounce change: the queued frame is launched first
         end = r.read_accumulation(), r.read_output(), r.ray_count()
     o = oracle_lib.Oracle(scene, camera_rays=rays)

@@ -42,8 +42,11 @@ def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms, what="i
         r.reset_timing()
         r.set_timing(True)
         t0 = time.perf_counter()
-        for _ in range(steps):
-            r.compute_frame(bounces)
+        done = 0
+        while done < steps:  # as bench.py: a launch's worth of compute_frame calls per rt_submit_frames
+            n = min(fb, steps - done)
+            r.submit_frames(bounces, n)
+            done += n
         t_submit = time.perf_counter() - t0
         r.synchronize()
         t = time.perf_counter() - t0
