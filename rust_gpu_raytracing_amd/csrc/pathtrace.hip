@@ -193,9 +193,11 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
 #define RT_LEAFCERT_LDS 0
 #endif
 // Walks from global memory: the certificate test made in the leaf batch (node_step records the
-// leaf box's gap beyond the best hit) instead of in node_step (build switch for A/B).
+// leaf box's gap beyond the best hit, one more VGPR) instead of in node_step, where every wave
+// step paid for the seven normals of whichever lane met a certified leaf (C5 11.08 -> 10.81 ms
+// per frame, 10.71 with leaf batches at 4/8; profiles/r04_k). RT_LEAFCERT_DEFER=0: in node_step.
 #ifndef RT_LEAFCERT_DEFER
-#define RT_LEAFCERT_DEFER 0
+#define RT_LEAFCERT_DEFER 1
 #endif
 // The LDS vertex table (mode 2, compact_tri): build switch, off by default --
 // compiled in, its code cost the LDS-resident instances more registers than its smaller

@@ -109,7 +109,8 @@ constexpr uint32_t kQueueStride = 64;
 // 48: C5 5.95 -> 5.72 ms, profiles/r03_ah/knobs_c5b.jsonl; C3 unchanged at 24-32).
 // certified: walks from global memory with the certified pruning, whose
 // traces visit the box-culling node set (about twice the relative slack's): they return to
-// shading later and batch their leaves earlier (C5 13.0 -> 11.1 ms per frame at 56 / 3,
+// shading later and batch their leaves earlier (C5 13.0 -> 11.1 ms per frame at 56 / 3, 10.7 at 56 / 4
+// once the certificate test moved into the leaf batch;
 // profiles/r04_f/ab.jsonl; the slack keeps round 3's 48 / 5).
 uint32_t trav_threshold_for(int lds_mode, bool tris, bool certified) {
     if (!tris) return 8;
@@ -120,8 +121,9 @@ uint32_t trav_threshold_for(int lds_mode, bool tris, bool certified) {
 // accelerator, earlier when the leaf's loads go to global memory anyway.
 // Re-measured with 20-frame launches (profiles/archive/r02_s4/r02_s4k, r02_s4l):
 // mode 2 at 6 (C4 -2.3% against 7, C3 within 0.3%), modes 0/1 at 5 (C5 -2.9%
-// against 6; 4 and 3 within 0.4% of 5); certified walks at 3 (above).
-uint32_t leaf_batch_for(int lds_mode, bool certified) { return lds_mode == 2 ? 6 : certified ? 3 : 5; }
+// against 6; 4 and 3 within 0.4% of 5); certified walks at 4 (above; 3 before the certificate
+// test moved into the leaf batch, profiles/r04_k).
+uint32_t leaf_batch_for(int lds_mode, bool certified) { return lds_mode == 2 ? 6 : certified ? 4 : 5; }
 // Instances with the triangle accelerator in global memory: the same once the
 // tile queue is empty, when the wave goes back to shading only if some lane
 // has finished and after at least kDefaultDrainMinSteps traversal steps
