@@ -195,7 +195,7 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
 // Walks from global memory: the certificate test made in the leaf batch (node_step records the
 // leaf box's gap beyond the best hit, one more VGPR) instead of in node_step, where every wave
 // step paid for the seven normals of whichever lane met a certified leaf (C5 11.08 -> 10.81 ms
-// per frame, 10.71 with leaf batches at 4/8; profiles/r04_k). RT_LEAFCERT_DEFER=0: in node_step.
+// per frame, 10.71 with leaf batches at 4/8; profiles/r04/r04_k). RT_LEAFCERT_DEFER=0: in node_step.
 #ifndef RT_LEAFCERT_DEFER
 #define RT_LEAFCERT_DEFER 1
 #endif
