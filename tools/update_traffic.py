@@ -20,12 +20,14 @@ ROOT = Path(__file__).resolve().parents[1]
 def main(prof_dir, dest):
     prof_dir, dest = Path(prof_dir).resolve(), Path(dest).resolve()
     dest.mkdir(parents=True, exist_ok=True)
-    summ = summarize_prof.main(prof_dir)
+    bench_line = json.loads((prof_dir / "trace_bench.json").read_text().strip().splitlines()[-1])
+    # the launch's dominant kernel: the brute-force sweep kernel, or the path kernel
+    kernel = "rt_brute_kernel" if "rt_brute_kernel" in bench_line["roofline"].get("kernel", "") else "rt_pathtrace_kernel"
+    summ = summarize_prof.main(prof_dir, kernel)
     (dest / "summary.json").write_text(json.dumps(summ, indent=1) + "\n")
     ks = prof_dir / "trace" / "run_kernel_stats.csv"
     if ks.exists():
         shutil.copy(ks, dest / "kernel_stats.csv")
-    bench_line = json.loads((prof_dir / "trace_bench.json").read_text().strip().splitlines()[-1])
     shutil.copy(prof_dir / "trace_bench.json", dest / "trace_bench.json")
     key = f'{bench_line["config"]["workload"]} | frame_batch {bench_line["config"]["frame_batch"]}'
     f = ROOT / "profiles" / "pmc_traffic.json"
