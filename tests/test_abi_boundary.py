@@ -98,7 +98,10 @@ def test_invalid_create_is_rejected_without_device(native_lib):
 
 def test_null_context_calls_fail_cleanly(native_lib):
     assert native_lib.rt_compute_frame(None, 8) == N.RT_E_INVALID
+    assert native_lib.rt_submit_frames(None, 8, 3) == N.RT_E_INVALID
     assert native_lib.rt_synchronize(None) == N.RT_E_INVALID
+    z = ctypes.c_uint32()
+    assert native_lib.rt_debug_check_leaf_certificates(None, z, z, z) == N.RT_E_INVALID
     native_lib.rt_destroy(None)
 
 
