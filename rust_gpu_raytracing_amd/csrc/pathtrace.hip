@@ -670,12 +670,6 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     }
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
-    // RT_SPHERE_DEFER 2 (sphere-only kernels): a lane whose leaf is deferred waits for the batch
-    // instead of walking on, so it visits exactly the nodes the on-the-spot test would (its
-    // pruning distance is current when it resumes), while the group tests run for many lanes
-    // at once instead of on every node step for the few lanes at a leaf
-    if constexpr (!kTris && RT_SPHERE_DEFER == 2)
-        if (ts.pending != kNoLeaf) return;
     float4 lo, hi;
     if (kTris && !kWide && tri && sv.tri_q) {
         // 16-B quantized node: the box decoded exactly (a superset of the 32-B node's box)
