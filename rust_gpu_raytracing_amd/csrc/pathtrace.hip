@@ -725,6 +725,19 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
         }
     }
     const bool at_leaf = hit && leaf != 0xffffffffu;
+#ifdef RT_DIAG
+    if constexpr (!kDeferLeaves<kTris>) {  // node steps and the sphere-group tests inside them, with their lanes
+        const uint64_t act = __ballot(true), lf = __ballot(at_leaf);
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(act)) {
+            atomicAdd(ka.diag + 22, 1ull);
+            atomicAdd(ka.diag + 23, (unsigned long long)__popcll(act));
+            if (lf) {
+                atomicAdd(ka.diag + 24, 1ull);
+                atomicAdd(ka.diag + 25, (unsigned long long)__popcll(lf));
+            }
+        }
+    }
+#endif
     if (at_leaf && !kDeferLeaves<kTris>) {
         test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
         ts.limit = prune_limit(ts);

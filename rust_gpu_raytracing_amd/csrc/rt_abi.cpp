@@ -1987,9 +1987,9 @@ int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
 
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
-    // (RT_DIAG builds keep 12 more counters in the first per-wave record words, which only
+    // (RT_DIAG builds keep 16 more counters in the first per-wave record words, which only
     // RT_DIAG_TAIL builds fill: cleared too)
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters + 12) * sizeof(unsigned long long), ctx->stream));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters + 16) * sizeof(unsigned long long), ctx->stream));
     RT_HIP(ctx, hipMemsetAsync(ctx->d_stream, 0, sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }

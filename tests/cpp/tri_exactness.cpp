@@ -105,6 +105,9 @@ static long g_exact_nodes = 0, g_exact_tests = 0;
 static const std::vector<TriLeafCert>* g_lcert = nullptr;
 static long g_lcert_leaves = 0, g_lcert_skipped = 0, g_lcert_tris = 0;
 static uint32_t g_subtree_max = 0;
+// experiment (TRI_DEPTH_HIST): the certified walk's node visits by tree depth (octant layouts)
+static std::vector<uint8_t> g_depth;
+static long g_depth_visits[64] = {0};
 
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
@@ -141,6 +144,7 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
             g_nodes++;
         }
         if (g_lcert) g_exact_nodes++;
+        if (g_lcert && !g_depth.empty()) g_depth_visits[std::min<int>(g_depth[node], 63)]++;
         float nt, ft;  // the kernel's slab test (rt_bvh_slab.h)
         slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
         bool hit = nt <= ft && ft >= 0.0f && nt <= limit;
@@ -401,6 +405,14 @@ int main(int argc, char** argv) {
             if (oct[i].leaf != kSphereBvhInternal && oct[i].skip >= oct.size()) qoct[4 * i + 3] |= kTriQLastLeaf;
         }
     }
+    if (getenv("TRI_DEPTH_HIST") && !oct.empty()) {
+        g_depth.assign(oct.size(), 0);
+        for (size_t i = 0; i < oct.size(); i++)
+            if (oct[i].leaf == kSphereBvhInternal && i + 1 < oct.size()) {
+                g_depth[i + 1] = g_depth[i] + 1;
+                if (oct[i + 1].skip < oct.size()) g_depth[oct[i + 1].skip] = g_depth[i] + 1;
+            }
+    }
     long n = (long)rays.size() / 6, hits = 0;
     for (long i = 0; i < n; i++) {
         V o = ld(&rays[6 * i]), d = ld(&rays[6 * i + 3]);
@@ -461,5 +473,11 @@ int main(int argc, char** argv) {
            (double)g_lcert_leaves / n, (double)g_lcert_skipped / n, (double)g_lcert_tris / n, lcert_valid,
            lcert.size());
     printf("heuristic_misses %ld\n", g_heur_miss);
+    if (!g_depth.empty()) {  // depth, visits per ray at that depth, nodes of one layout at that depth
+        std::vector<long> per(64, 0);
+        for (size_t i = 0; i < A.nodes.size(); i++) per[std::min<int>(g_depth[i], 63)]++;
+        for (int k = 0; k < 64; k++)
+            if (per[k] || g_depth_visits[k]) printf("depth %d %.3f %ld\n", k, (double)g_depth_visits[k] / n, per[k]);
+    }
     return 0;
 }

@@ -34,11 +34,14 @@ for name in argv or list(SIZES):
         r.reset_ray_count()
         for _ in range(3 * fb):
             r.compute_frame(bounces)
-        c = r.debug_counters(24)
+        c = r.debug_counters(28)
         rays = r.ray_count()
     total, trav, steps, it, step_lanes, shade, refill, setup, leaf_cyc, leaf_steps = c[:10]
     sh_pass, sh_lanes, miss, glass, spec, su_pass, su_lanes = c[12:19]
     cert_checks, cert_leaves, cert_tris = c[19:22]  # leaf certificates (certified pruning)
+    # sphere-only kernels: wave-level node steps and their lanes, the sphere-group tests run inside
+    # them (a group runs for the whole wave when any lane is at a leaf) and the lanes at a leaf
+    n_steps, n_step_lanes, n_groups, n_group_lanes = c[22:26]
     trav_occ = step_lanes / max(steps, 1) / 64
     shade_occ = sh_lanes / max(sh_pass, 1) / 64
     setup_occ = su_lanes / max(su_pass, 1) / 64
@@ -52,6 +55,9 @@ for name in argv or list(SIZES):
                       "cycles_per_ray": total / rays, "steps_per_ray": steps / rays,
                       "lanes_per_step": step_lanes / max(steps, 1), "outer_iters_per_ray": it / rays,
                       "leaf_share": leaf_cyc / total, "leaf_steps_per_ray": leaf_steps / rays,
+                      "sphere_node_steps": {"per_ray": n_steps / rays, "lanes_per_step": n_step_lanes / max(n_steps, 1),
+                                            "steps_with_a_group_test": n_groups / max(n_steps, 1),
+                                            "lanes_per_group_test": n_group_lanes / max(n_groups, 1)},
                       "leaf_certificates_per_ray": {"checked": cert_checks / rays, "leaves_skipped": cert_leaves / rays,
                                                     "triangles_skipped": cert_tris / rays},
                       "occupancy": {"traversal": trav_occ, "shading": shade_occ, "setup": setup_occ},
