@@ -2003,6 +2003,14 @@ int rt_accumulation_index(const rt_ctx* ctx, uint32_t* out) {
 int rt_set_timing(rt_ctx* ctx, int enable) {
     RT_ENTER(ctx);
     ctx->timing = enable != 0;
+    // The launch-clock slots are allocated (and zeroed) here rather than by the first timed
+    // launch: callers switch timing on ahead of the region they time (bench.py), which then
+    // holds no hipMalloc on its launch path.
+    if (ctx->timing && !ctx->d_clock) {
+        const int rc = dev_alloc(ctx, &ctx->d_clock, kClockWords * (size_t)kClockSlots);
+        if (rc) return rc;
+        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     return RT_OK;
 }
 
