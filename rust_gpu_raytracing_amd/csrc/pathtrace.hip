@@ -643,13 +643,21 @@ constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
 // Node steps per wave-wide check of the traversal loop (the ballots of the
 // threshold and leaf-batch tests, exec-mask updates). Lanes that finish inside
 // the group idle for its remaining steps; the visit order is unchanged.
-// Measured (RT_TRAV_UNROLL / _TRI = 1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%.
+// Measured (RT_TRAV_UNROLL / _TRI = 1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%. Round 4, per
+// accelerator placement (profiles/r04/r04_z): global-memory walks 3 -> 4 / 5 / 6: C5 -4.0% /
+// -4.3% / -1.6%; LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%; sphere walks 2 or 4: C2
+// +1.5% / +0.8%.
 #ifndef RT_TRAV_UNROLL
 #define RT_TRAV_UNROLL 3
 #endif
-#ifndef RT_TRAV_UNROLL_TRI
-#define RT_TRAV_UNROLL_TRI 3
+#ifndef RT_TRAV_UNROLL_TRI  // triangle scenes, accelerator in global memory (modes 0, 1)
+#define RT_TRAV_UNROLL_TRI 5
 #endif
+#ifndef RT_TRAV_UNROLL_LDS  // triangle scenes, accelerator in LDS (mode 2)
+#define RT_TRAV_UNROLL_LDS 2
+#endif
+template <int kMode, bool kTris>
+constexpr int kTravUnroll = !kTris ? RT_TRAV_UNROLL : kMode <= 1 ? RT_TRAV_UNROLL_TRI : RT_TRAV_UNROLL_LDS;
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
@@ -1676,7 +1684,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                 if (!(kDeferLeaves<kTris> && leaves)) {
                     // further node steps before the next wave-wide check (RT_TRAV_UNROLL)
 #pragma unroll
-                    for (int k = 1; k < (kTris ? RT_TRAV_UNROLL_TRI : RT_TRAV_UNROLL); ++k) {
+                    for (int k = 1; k < kTravUnroll<kMode, kTris>; ++k) {
                         if (mode == kTrav) {
                             node_step<kTris, kWide, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
                             phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
