@@ -17,12 +17,13 @@ default "--scaling strong", the metric's config: the 1920x1080 frame is
 tile-split across ranks (8x8 tile t -> rank t % N), launches of up
 to 32N frames (a GPU's launch holds the units of an N=1 launch), and the timed region also
 assembles the frame on rank 0 once (device pack -> RCCL gather -> unpack), so `value`
-includes the gather (also reported as gather_ms). --gather image (default) moves the
-displayed RGBA8 frame (4 B/px; accumulations stay sharded on their owners, which keep
-accumulating their tiles), --gather accumulation the RGBA32F accumulation (16 B/px, the
-whole renderer state on rank 0). Both gathers are also timed alone after the timed
-region (gather_image_ms, gather_accum_ms), and value_with_accum_gather prices the
-accumulation gather instead. A secondary "weak" object measures the same view at N x the pixels
+includes the gather (also reported as gather_ms). --gather accumulation (default, the
+north star's "RCCL gather of the accumulated RGBA buffer") moves the RGBA32F accumulation
+(16 B/px, the whole renderer state on rank 0, which rebuilds the RGBA8 output from it);
+--gather image the displayed RGBA8 frame (4 B/px; accumulations stay sharded on their
+owners). Both gathers are also timed alone after the timed region (gather_image_ms,
+gather_accum_ms), and value_with_image_gather / value_with_accum_gather price the run
+with either payload. A secondary "weak" object measures the same view at N x the pixels
 ((1920*sqrt(N)) x (1080*sqrt(N)) in whole tiles, one 1920x1080 frame's worth
 of tiles per GPU). `value` = all ranks' rays / the slowest rank's time.
 
@@ -192,9 +193,10 @@ def main() -> int:
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the secondary weak-scaling measurement")
     ap.add_argument("--no-cadences", action="store_true",
                     help="N=1: skip the secondary single-frame and display-cadence timings")
-    ap.add_argument("--gather", choices=["image", "accumulation"], default="image",
-                    help="N>1: the payload of the gather in the timed region: the displayed RGBA8 frame "
-                         "(4 B/px) or the RGBA32F accumulation (16 B/px)")
+    ap.add_argument("--gather", choices=["image", "accumulation"], default="accumulation",
+                    help="N>1: the payload of the gather in the timed region: the RGBA32F accumulation "
+                         "(16 B/px, the north star's 'RCCL gather of the accumulated RGBA buffer'; default) or "
+                         "the displayed RGBA8 frame (4 B/px)")
     ap.add_argument("--driver", choices=["torch", "group"], default="torch",
                     help="N>1 route: torch = one process per GPU (torch.distributed.run, RCCL via ProcessGroupNCCL); "
                          "group = one process driving --gpus devices through the C ABI (rt_create_multi, "
@@ -249,14 +251,24 @@ def main() -> int:
             return int(round(args.width * scale / 8.0)) * 8, int(round(args.height * scale / 8.0)) * 8
         return args.width, args.height
 
-    def run(scaling, frame_batch):
+    def run(scaling, frame_batch, pattern="submit"):
         """Warmup, then exactly args.steps frames between barrier + sync; with N > 1 the
         timed region also assembles the image on rank 0 (pack -> RCCL gather -> unpack),
-        once per run (a readback after the last frame, amortised over the steps)."""
+        once per run (a readback after the last frame, amortised over the steps).
+        pattern "reference" (N=1 secondary): the reference's event loop through the default
+        ABI -- no rt_set_frame_batch (frame_batch None), one rt_compute_frame call per frame
+        and every DISPLAY_CADENCE_FRAMES frames the display copy (rt_copy_output_to_device,
+        update_texture's buffer-to-texture copy on the device) into a display buffer."""
         width, height = size_for(scaling)
         scene, default_bounces = build_config(args.config, width=width, height=height)
         bounces = args.bounces or default_bounces
         r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=frame_batch)
+        if frame_batch is None:
+            frame_batch = r.frame_batch()[0]
+        display = None
+        if pattern == "reference":
+            bpr = int(r._lib.rt_bytes_per_row(width, 256))
+            display = (torch.zeros(height * bpr, dtype=torch.uint8, device=torch.device("cuda", device)), bpr)
         if args.brute_force:
             r.set_brute_force(True)
 
@@ -306,6 +318,12 @@ def main() -> int:
         # the steps' compute_frame calls, a launch's worth per C call (rt_submit_frames: the
         # host loop a native caller runs, without a Python round trip per frame)
         done = 0
+        if pattern == "reference":
+            for i in range(args.steps):
+                r.compute_frame(bounces)
+                if (i + 1) % DISPLAY_CADENCE_FRAMES == 0:
+                    r.copy_output_to_device(display[0].data_ptr(), display[1])
+            done = args.steps
         while done < args.steps:
             n = min(frame_batch, args.steps - done)
             r.submit_frames(bounces, n)
@@ -455,15 +473,17 @@ def main() -> int:
         if not same:
             return 3
     r.close()
-    # Secondary cadences (N=1): the library's default single-frame launches (the
-    # reference's one dispatch per compute_frame, src/renderer.rs:201-252) and the
-    # reference's display pacing -- a frame computed every >= 0.8 ms, displayed every
-    # >= 5 ms (src/main.rs:88-92, 365-375), i.e. about 6 frames per displayed image,
-    # so launches of 6 frames, each materialising its last frame's RGBA8 output.
+    # Secondary cadences (N=1): the reference's call pattern through the default ABI (one
+    # rt_compute_frame per frame, no rt_set_frame_batch, the display copy every 6 frames:
+    # src/renderer.rs:201-283, src/main.rs:88-92, 365-375 -- a frame computed every >= 0.8 ms,
+    # displayed every >= 5 ms); one launch per frame (rt_set_frame_batch(1), the reference's
+    # one dispatch per compute_frame); launches of 6 frames (the display pacing, submitted).
     cadences = {}
     if world == 1 and not args.no_cadences and args.driver != "group":
-        for key, batch in (("ms_per_step_f1", 1), ("ms_per_step_display_cadence", DISPLAY_CADENCE_FRAMES)):
-            c_run = run(args.scaling, batch)
+        for key, batch, pattern in (("ms_per_step_reference_pattern", None, "reference"),
+                                    ("ms_per_step_f1", 1, "submit"),
+                                    ("ms_per_step_display_cadence", DISPLAY_CADENCE_FRAMES, "submit")):
+            c_run = run(args.scaling, batch, pattern)
             c_run["r"].close()
             cadences[key] = c_run["t_total_max"] / args.steps * 1e3
     weak = None
@@ -503,6 +523,11 @@ def main() -> int:
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
         if args.brute_force:
             workload += ", brute-force LDS-tiled sweeps"
+        # a non-default triangle walk is another workload for the PMC table (its counters are
+        # not the default walk's): RT_TRI_PRUNE 0 = box culling, 2 = the round-3 slack (not exact)
+        prune = os.environ.get("RT_TRI_PRUNE", "1")
+        if prune != "1" and int(scene.flatten()[2].shape[0]) > 0:
+            workload += f", triangle pruning mode {prune}"
         build_hash = native_build.source_hash()
         pmc, pmc_why = pmc_entry(f"{workload} | frame_batch {fb}", build_hash) if world == 1 else (None, "N>1")
         result = {
@@ -573,9 +598,12 @@ def main() -> int:
         }
         result.update(cadences)
         if cadences:
-            result["cadence_note"] = (f"secondary: the same {args.steps} steps in single-frame launches (library "
-                                      f"default) and in launches of {DISPLAY_CADENCE_FRAMES} (the reference's "
-                                      "0.8 ms compute / 5 ms display pacing); `value` uses frame_batch")
+            result["cadence_note"] = (f"secondary: the same {args.steps} steps as the reference's loop calls the "
+                                      "default ABI (one rt_compute_frame per frame, no rt_set_frame_batch, "
+                                      f"rt_copy_output_to_device every {DISPLAY_CADENCE_FRAMES} frames), in "
+                                      "single-frame launches (rt_set_frame_batch(1)), and in submitted launches of "
+                                      f"{DISPLAY_CADENCE_FRAMES}; `value` uses frame_batch")
+            result["reference_pattern_vs_headline"] = cadences["ms_per_step_reference_pattern"] / result["ms_per_step"]
         if args.driver == "group":
             result["driver"] = "c-abi group (rt_create_multi + rt_gather_frame, one process)"
         if dist_run:
@@ -586,9 +614,10 @@ def main() -> int:
                 result["gather_payload"] = args.gather
                 result["gather_image_ms"] = m["t_gather_image_max"] * 1e3
                 result["gather_accum_ms"] = m["t_gather_accum_max"] * 1e3
-                # the same run priced with the accumulation gather (16 B/px) in place of
-                # the --gather one: rays / (render time + the accumulation gather's time)
+                # the same run priced with the other payload's gather in place of the --gather
+                # one: rays / (render time + that gather's time, timed alone)
                 result["value_with_accum_gather"] = m["rays_total"] / (m["t_render_max"] + m["t_gather_accum_max"]) / 1e6
+                result["value_with_image_gather"] = m["rays_total"] / (m["t_render_max"] + m["t_gather_image_max"]) / 1e6
             if weak is not None:
                 result["weak"] = weak
         if world == 1 and not args.no_cpu_baseline:

@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 10
+#define RT_ABI_VERSION 11
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -253,9 +253,14 @@ RT_API int rt_submit_frames(rt_ctx* ctx, uint32_t bounces, uint32_t count);
  * persistent grid's fill and drain are paid once per batch, and that a tile
  * split over N GPUs keeps N x the units per launch. Non-accumulating batches
  * (every frame the same frame) run each pixel's frames back to back on a lane.
- * 1 (the default; env RT_FRAME_BATCH) launches each frame at once.
+ * The default is RT_DEFAULT_FRAME_BATCH (ABI 11; it was 1, one launch per frame): a
+ * host that mirrors the reference's event loop -- one rt_compute_frame per frame and
+ * a display copy every few frames (src/renderer.rs:201-283, src/main.rs:88-92,
+ * 365-375) -- gets launches of the frames between two displays without calling
+ * this. 1 launches each frame at once (env RT_FRAME_BATCH overrides the default).
  * max_frames in [1, 64]. rt_frame_batch reports the setting and the frames
  * queued; rt_flush launches them now. */
+#define RT_DEFAULT_FRAME_BATCH 16
 RT_API int rt_set_frame_batch(rt_ctx* ctx, uint32_t max_frames);
 RT_API int rt_frame_batch(const rt_ctx* ctx, uint32_t* max_frames, uint32_t* pending);
 RT_API int rt_flush(rt_ctx* ctx);
@@ -278,6 +283,15 @@ RT_API int rt_read_accumulation(rt_ctx* ctx, float* rgba_f32_out);
  * window width to a multiple of 64 pixels, src/main.rs:51-53 -- any pitch
  * works here). Padding bytes are left untouched. Synchronous. */
 RT_API int rt_read_output_pitched(rt_ctx* ctx, uint8_t* dst, uint32_t bytes_per_row);
+
+/* Renderer::update_texture on the device (new, ABI 11): the copy_buffer_to_texture of
+ * src/renderer.rs:254-283 -- the packed RGBA8 output copied row by row into device
+ * memory at `dst_device` (a display texture's staging buffer on the context's device),
+ * rows `bytes_per_row` bytes apart (>= 4*width; padding untouched). Stream-ordered
+ * after the frames submitted so far (queued frames are launched first), asynchronous:
+ * the display observation point of a render loop, with no PCIe transfer and no host
+ * wait, as in the reference (which never reads the frame back to the host). */
+RT_API int rt_copy_output_to_device(rt_ctx* ctx, void* dst_device, uint32_t bytes_per_row);
 
 /* calculate_bytes_per_row (src/renderer.rs:285-295): 4*width rounded up to
  * `alignment` (a power of two; the reference uses wgpu's 256). 0 on bad input. */
@@ -390,7 +404,7 @@ RT_API int rt_unpack_output_ranks(rt_ctx* ctx, const void* src_device, uint64_t 
  * threads, workgroups launched, dynamic LDS bytes per workgroup, and the LDS
  * staging mode (0: scene in global memory, 1: spheres/materials/objects/sphere
  * BVH staged in LDS, 2: also the triangle accelerator). */
-RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
+RT_API int rt_launch_config(rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
                             uint32_t* scene_in_lds);
 
 /* The kernels the last rt_dispatch ran (diagnostics, ABI 7), a mask of RT_PASS_*:
@@ -400,7 +414,7 @@ RT_API int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* bloc
 #define RT_PASS_PRIMARY 2u
 #define RT_PASS_RESOLVE 4u
 #define RT_PASS_BRUTE 8u
-RT_API int rt_last_launch_passes(const rt_ctx* ctx, uint32_t* passes);
+RT_API int rt_last_launch_passes(rt_ctx* ctx, uint32_t* passes);
 
 /* Diagnostic counters (filled only by builds compiled with -DRT_DIAG or
  * -DRT_DIAG_TAIL, zeros otherwise): out[0..n) receives up to 8 u64 counters
@@ -453,6 +467,17 @@ RT_API int rt_srgb_table(float out[256]);
 typedef struct rt_group rt_group;
 
 RT_API int rt_create_multi(const rt_create_info* info, const int32_t* devices, uint32_t n_devices, rt_group** out);
+/* rt_create_multi with flags (new, ABI 11). RT_GROUP_COPY_TRANSPORT: no RCCL
+ * communicators; rt_gather_frame moves each rank's packed block to the root with a
+ * stream-ordered device-to-device copy (hipMemcpyPeerAsync on the sender's stream,
+ * after the root's previous unpack; the root's unpack waits for every copy), and a
+ * device may be listed more than once -- several ranks of one group on one GPU, which
+ * runs the group's N-rank logic (one host thread and context per rank, tile ownership,
+ * the root's N receive slots) on a one-GPU machine, or a group where RCCL is absent.
+ * The assembled frame is the same bits either way. flags 0 == rt_create_multi. */
+#define RT_GROUP_COPY_TRANSPORT 1u
+RT_API int rt_create_multi_ex(const rt_create_info* info, const int32_t* devices, uint32_t n_devices, uint32_t flags,
+                              rt_group** out);
 RT_API void rt_destroy_multi(rt_group* g);
 RT_API const char* rt_group_last_error(const rt_group* g);
 RT_API uint32_t rt_group_size(const rt_group* g);

@@ -111,6 +111,7 @@ SIGNATURES = {
     "rt_flush": (ctypes.c_int, [_P]),
     "rt_synchronize": (ctypes.c_int, [_P]),
     "rt_read_output": (ctypes.c_int, [_P, _P]),
+    "rt_copy_output_to_device": (ctypes.c_int, [_P, _P, _U32]),
     "rt_read_accumulation": (ctypes.c_int, [_P, _P]),
     "rt_read_output_pitched": (ctypes.c_int, [_P, _P, _U32]),
     "rt_bytes_per_row": (_U32, [_U32, _U32]),
@@ -155,6 +156,8 @@ SIGNATURES = {
     # several GPUs in one process (rt_multi.cpp)
     "rt_create_multi": (ctypes.c_int, [ctypes.POINTER(rt_create_info), ctypes.POINTER(ctypes.c_int32), _U32,
                                        ctypes.POINTER(_P)]),
+    "rt_create_multi_ex": (ctypes.c_int, [ctypes.POINTER(rt_create_info), ctypes.POINTER(ctypes.c_int32), _U32, _U32,
+                                          ctypes.POINTER(_P)]),
     "rt_destroy_multi": (None, [_P]),
     "rt_group_last_error": (ctypes.c_char_p, [_P]),
     "rt_group_size": (_U32, [_P]),
@@ -182,6 +185,8 @@ SIGNATURES = {
     "rt_group_read_accumulation": (ctypes.c_int, [_P, _U32, _P]),
 }
 
+RT_DEFAULT_FRAME_BATCH = 16  # include/rt_abi.h (ABI 11)
+RT_GROUP_COPY_TRANSPORT = 1  # rt_create_multi_ex flags
 RT_GATHER_IMAGE = 0
 RT_GATHER_ACCUMULATION = 1
 

@@ -778,6 +778,183 @@ __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs&
     ts.pending = kNoLeaf;
 }
 
+// ---- Cooperative leaf batches (walks from global memory) --------------------
+//
+// A per-lane leaf test loads its up-to-7 triangles with three lane-distinct 16-B loads each:
+// 21 L1 tag lookups per leaf, and the L1's tag rate (about one line per cycle per CU) is what
+// the global-memory walk is bound by. Here a leaf batch tests the wave's
+// pending leaves together instead: the pending lanes publish their ray and leaf in a per-wave
+// LDS scratch, and each round 8 lanes per leaf -- lane j the leaf's triangle j -- load the
+// leaf's triangle block (KernelArgs::tri_leaftris: piece p of slots 0..7 in one 128-B line),
+// so the 21 loads become 3 lines shared by 8 lanes, and 8 leaves are tested per round on all
+// 64 lanes. Each lane runs the reference's test (compute_shader.wgsl:445-500) with the same
+// f32 operations as tri_leaf; the group's candidates are reduced to the lexicographic minimum
+// of (distance, sweep position) and an "any NaN distance" flag, which the leaf's lane then
+// merges exactly as tri_leaf's sequential loop would: the sub-object box test (:441) runs if a
+// candidate beats the lane's best hit or has a NaN distance; if it fails, nothing of the leaf
+// counts; else the NaN flag and the best candidate are taken. (Within a leaf the sequential
+// loop's result is that minimum: a candidate's test does not depend on the running best other
+// than through "distance < best", which is the minimum's own comparison.)
+#ifndef RT_COOP_LEAVES
+#define RT_COOP_LEAVES 1
+#endif
+template <int kMode, bool kTris, bool kWide>
+constexpr bool kCoopLeaves = RT_COOP_LEAVES && kTris && !kWide && kMode <= 1;
+
+// LDS written by some lanes of a wave and read by others: the wave's LDS operations complete in
+// order, so only the compiler must not move them across this point.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One step of the 8-lane (distance, sequence) minimum: the candidate of lane (DPP `ctrl`).
+template <int kCtrl>
+__device__ __forceinline__ void coop_min_step(float& cd, uint32_t& cs, uint32_t& ct) {
+    const float od = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(cd), kCtrl, 0xf, 0xf, false));
+    const uint32_t os = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cs, kCtrl, 0xf, 0xf, false);
+    const uint32_t ot = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ct, kCtrl, 0xf, 0xf, false);
+    const bool take = od < cd || (od == cd && os < cs);
+    cd = take ? od : cd;
+    cs = take ? os : cs;
+    ct = take ? ot : ct;
+}
+
+// The lane's index in its wave, computed where it is used: an opaque value, so that the compiler
+// does not hoist it (and what is derived from it) out of the traversal loop into a register
+// held across every node step.
+__device__ __forceinline__ uint32_t lane_id_here() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// `active`: this lane traverses and holds a deferred leaf (a triangle leaf, or a sphere group in
+// the sphere phase, which is tested on the spot as in leaf_step). Wave-uniform call; the scratch
+// is this wave's 64 x 3 float4 of LDS at ka.lds_leafbatch_offset.
+__device__ __forceinline__ void coop_leaf_batch(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
+                                                bool active, unsigned char* lds) {
+    bool want = false;
+    uint32_t prim = 0u, range = 0u, seq0 = 0u, obj = 0u, sub = 0u;
+    if (active) {
+        if (ts.phase == 0) {
+            prim = ts.pending & 0xffffffu;
+            uint32_t skip = 0u;
+#if RT_LEAFCERT_DEFER
+            if ((ts.pending >> 24) & 1u) {  // the certificate test deferred by node_step
+                const uint4* rec = reinterpret_cast<const uint4*>(ka.tri_leafcert + prim);
+                const uint4 c0 = rec[0], c1 = rec[1];
+                const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                skip = tri_leafcert_skips_gap(w, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), ts.tri.t, ts.cert_gap);
+            }
+#endif
+            if (skip != kLeafCertAll) {
+                const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base, range
+                const RtObject& ob = sv.obj[pr.x];
+                if (ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) {  // :431
+                    if (pr.w != kPrimRangeNone && (pr.w >> 27) < kLeafTriSlots) {
+                        want = true;
+                        range = pr.w;
+                        seq0 = pr.z;
+                        obj = pr.x;
+                        sub = pr.y;
+                    } else {  // a leaf of more than 7 triangles: the per-lane test (no certificate mask)
+                        tri_leaf<true>(sv, ka, o, d, ts, prim);
+                        ts.limit = tri_limit(sv, ka, o, ts);
+                    }
+                }
+            }
+        } else {
+            test_sphere_group(sv, ts.pending, o, d, ts.a4, ts.a2, ts.sph);
+            ts.limit = prune_limit(ts);
+        }
+        ts.pending = kNoLeaf;
+    }
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4* const scratch = reinterpret_cast<float4*>(lds + ka.lds_leafbatch_offset + wave * kLeafBatchWaveBytes);
+    const uint32_t n = (uint32_t)__popcll(wm);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
+    if (want) {
+        float4* sl = scratch + 3u * rank;
+        sl[0] = make_float4(o.x, o.y, o.z, __uint_as_float(prim));
+        sl[1] = make_float4(d.x, d.y, d.z, __uint_as_float(range));
+        sl[2] = make_float4(__uint_as_float(seq0), __uint_as_float(obj), __uint_as_float(sub), 0.0f);
+    }
+    wave_lds_sync();
+    const uint32_t lane = lane_id_here(), g = lane >> 3, j = lane & 7u;
+    for (uint32_t base = 0; base < n; base += 8u) {
+        const uint32_t kk = base + g;
+        float cd = __builtin_inff();  // no candidate: never accepted (a distance is always < inf there)
+        uint32_t cs = 0xffffffffu, ct = 0u;
+        bool cnan = false;
+        if (kk < n) {
+            const float4* sl = scratch + 3u * kk;
+            const float4 s0 = sl[0], s1 = sl[1];
+            const uint32_t rg = __float_as_uint(s1.w);
+            if (j < (rg >> 27)) {
+                const uint4* blk = ka.tri_leaftris + (size_t)__float_as_uint(s0.w) * kLeafTriWords + j;
+                const uint4 q0 = blk[0], q1 = blk[kLeafTriSlots], q2 = blk[2u * kLeafTriSlots];
+                const float4 p0 = make_float4(__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z),
+                                              __uint_as_float(q0.w));
+                const float4 p1 = make_float4(__uint_as_float(q1.x), __uint_as_float(q1.y), __uint_as_float(q1.z),
+                                              __uint_as_float(q1.w));
+                const float4 p2 = make_float4(__uint_as_float(q2.x), __uint_as_float(q2.y), __uint_as_float(q2.z),
+                                              __uint_as_float(q2.w));
+                const TriGeom tg{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x),
+                                 mk(p2.y, p2.z, p2.w)};
+                const f3 ro = mk(s0.x, s0.y, s0.z), rd = mk(s1.x, s1.y, s1.z);
+                // the reference's test, tri_leaf's operations (:449-481)
+                const float det = -dot(rd, tg.cn);
+                const float inv_det = 1.0f / det;
+                const f3 ao = ro - tg.a;
+                const float dist = dot(ao, tg.cn) * inv_det;
+                const f3 dao = cross(ao, rd);
+                const float v = -dot(tg.ab, dao) * inv_det;
+                const float u = dot(tg.ac, dao) * inv_det;
+                const float w = 1.0f - u - v;
+                if (!(dist < 0.0f) && !(v < 0.0f) && !(u < 0.0f) && !(w < 0.0f)) {
+                    if (dist != dist) {
+                        cnan = true;
+                    } else {
+                        cd = dist;
+                        cs = __float_as_uint(sl[2].x) + j;
+                        ct = min((rg & ((1u << 27) - 1u)) + j, ka.triangle_count - 1u) | (det > 0.0f ? 0x80000000u : 0u);
+                    }
+                }
+            }
+        }
+        // the group's minimum on every lane of it: xor 1, xor 2 (quad), then the other quad
+        coop_min_step<0xB1>(cd, cs, ct);
+        coop_min_step<0x4E>(cd, cs, ct);
+        coop_min_step<0x141>(cd, cs, ct);
+        const uint64_t nm = __ballot(cnan);
+        if (j == 0u && kk < n)  // slot kk's ray is no longer needed: its result goes there
+            scratch[3u * kk] = make_float4(cd, __uint_as_float(cs), __uint_as_float(ct),
+                                           __uint_as_float(((nm >> (8u * g)) & 0xffu) != 0u ? 1u : 0u));
+    }
+    wave_lds_sync();
+    if (want) {
+        const float4 r = scratch[3u * rank];
+        const float4 r2 = scratch[3u * rank + 2u];
+        obj = __float_as_uint(r2.y);
+        sub = __float_as_uint(r2.z);
+        const float rd = r.x;
+        const uint32_t rs = __float_as_uint(r.y), rt = __float_as_uint(r.z);
+        const bool rnan = __float_as_uint(r.w) != 0u;
+        const bool beats = rd < ts.tri.t || (rd == ts.tri.t && rs < ts.tri.seq);
+        if (rnan || beats) {
+            const RtSubObject so = sv.sub[sub];  // :441, run when the leaf would change the result
+            if (ray_in_bounds(o, ts.inv, so.min_bounds, so.max_bounds)) {
+                if (rnan) ts.nan_hit = true;
+                if (beats) ts.tri = TriHit{rd, rs, rt & 0x7fffffffu, obj, (rt >> 31) != 0u};
+            }
+        }
+        ts.limit = tri_limit(sv, ka, o, ts);
+    }
+}
+
 // trace_ray's result (:342-353): the sphere wins only if strictly closer.
 template <bool kTris>
 __device__ __forceinline__ Hit trace_end(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, const TraceState& ts) {
@@ -1671,7 +1848,20 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #ifdef RT_DIAG
             const unsigned long long tl0 = stamp();
 #endif
-            if (mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
+            bool batched = false;
+            if constexpr (kCoopLeaves<kMode, kTris, kWide>) {
+                if (leaves && ka.tri_leaftris) {  // the wave's deferred leaves, cooperatively
+                    RT_ISA_MARK("coop_leaf_batch");
+                    const bool act = mode == kTrav && ts.pending != kNoLeaf;
+                    coop_leaf_batch(sv, ka, p.o, p.d, ts, act, lds);
+                    if (act) {
+                        phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                        if (ts.phase == 2) mode = kDone;
+                    }
+                    batched = true;
+                }
+            }
+            if (!batched && mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
                 if (kDeferLeaves<kTris> && leaves) {
                     RT_ISA_MARK("leaf_batch");
                     leaf_step<kTris, kWide, (kMode <= 1)>(sv, ka, p.o, p.d, ts);

@@ -50,6 +50,8 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            hipStream_t stream);
 hipError_t rt_launch_tri_leafcert(const SubObjectPrim* prims, uint32_t n_prims, const RtSubObject* subs,
                                   const RtTriangleHot* tris, uint32_t n_tri, TriLeafCert* out, hipStream_t stream);
+hipError_t rt_launch_tri_leaftris(const SubObjectPrim* prims, uint32_t n_prims, const RtTriangleHot* tris,
+                                  uint32_t n_tri, uint4* out, hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
@@ -166,7 +168,7 @@ struct rt_ctx {
     uint32_t k = 1;      // Renderer::accumulation_index (src/renderer.rs:37)
     rt_ray_camera camera{};
     // frame batching (rt_set_frame_batch): queued rt_compute_frame calls
-    uint32_t frame_batch = 1;     // frames per launch at most (1: one launch per frame)
+    uint32_t frame_batch = RT_DEFAULT_FRAME_BATCH;  // frames per launch at most (1: one launch per frame)
     uint32_t pending_frames = 0;  // queued, not yet launched (their k already advanced)
     uint32_t pending_bounces = 0;
     bool frame_parallel = true;     // RT_FRAME_PARALLEL=0: batches run frames back to back per lane (A/B switch)
@@ -282,6 +284,13 @@ struct rt_ctx {
     TriLeafCert* d_tri_lcert = nullptr;
     size_t tri_lcert_cap = 0;
     bool cones_dirty = true;
+    // cooperative leaf batches of the walks from global memory (pathtrace.hip coop_leaf_batch):
+    // the leaves' triangle blocks, rebuilt with the certificates; RT_COOP_LEAVES=0: per-lane leaf
+    // tests (A/B switch)
+    bool use_coop_leaves = true;
+    uint4* d_tri_ltris = nullptr;
+    size_t tri_ltris_cap = 0;
+    bool ltris_dirty = true;
     // the 4-wide accelerator (tri_wide.h), RT_TRI_WIDE=1 (A/B switch): measured slower than the
     // binary one on C3-C5, so off by default
     bool use_tri_wide = false;
@@ -581,6 +590,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         return rc;
     ctx->qnodes_dirty = true;
     ctx->cones_dirty = true;
+    ctx->ltris_dirty = true;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
     ctx->tri_prim_count = (uint32_t)acc.prims.size();
     ctx->tri_octants_built = false;
@@ -675,6 +685,7 @@ bool build_compact_triangles(const rt_scene_triangle* t, uint32_t n, std::vector
 int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     if (n == 0) return RT_OK;
     ctx->cones_dirty = true;
+    ctx->ltris_dirty = true;
     // the vertex table describes the whole buffer only when this upload rewrites all of it
     ctx->compact_valid = false;
     if (n == ctx->cap_tri) {
@@ -921,6 +932,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->use_qnodes = env[0] != '0';
         env = std::getenv("RT_TRI_LEAFCERT_LDS");
         if (env) ctx->use_leafcert_lds = env[0] == '1';
+        env = std::getenv("RT_COOP_LEAVES");
+        if (env) ctx->use_coop_leaves = env[0] != '0';
         env = std::getenv("RT_TRI_LDS_COMPACT");
         if (env) ctx->use_lds_compact = env[0] == '1';
         env = std::getenv("RT_STAGE_SUBS");
@@ -1003,7 +1016,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
                     ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
-                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx};
+                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx, ctx->d_tri_ltris};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1528,6 +1541,30 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         ka.tri_leafcert = ctx->d_tri_lcert;
     }
+    // cooperative leaf batches (walks from global memory): the leaves' triangle blocks
+    ka.tri_leaftris = nullptr;
+    const bool coop = tris && !wide && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0 && ka.tri_prim_count != 0 &&
+                      ctx->use_coop_leaves;
+    if (coop) {
+        const size_t bytes = (size_t)ka.tri_prim_count * kLeafTriWords * sizeof(uint4);
+        if (ctx->tri_ltris_cap < bytes) {  // (re)allocate: nothing may still read them
+            RT_HIP(ctx, join_aux(ctx));
+            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->d_tri_ltris) RT_HIP(ctx, hipFree(ctx->d_tri_ltris));
+            ctx->d_tri_ltris = nullptr;
+            ctx->tri_ltris_cap = 0;
+            RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_ltris), bytes));
+            ctx->tri_ltris_cap = bytes;
+            ctx->ltris_dirty = true;
+        }
+        if (ctx->ltris_dirty) {
+            RT_HIP(ctx, rt_launch_tri_leaftris(ctx->d_tri_prims, ka.tri_prim_count, ctx->d_tri, ctx->n_tri_dev,
+                                               ctx->d_tri_ltris, ctx->stream));
+            ctx->ltris_dirty = false;
+            ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
+        }
+        ka.tri_leaftris = ctx->d_tri_ltris;
+    }
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
@@ -1539,13 +1576,16 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.lds_srgb_offset = 0;
         lds_bytes = kLdsTailBytes;
     }
+    // per-thread LDS after the scene image: the wide walk's stack, or the cooperative leaf
+    // batch's per-wave scratch
+    const size_t lane_pt = wide ? stack_pt : coop ? (size_t)kLeafBatchWaveBytes / 64u : 0u;
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode ||
-        ctx->occ_tris != tris || ctx->occ_wide != wide || ctx->occ_stack_pt != stack_pt) {
+        ctx->occ_tris != tris || ctx->occ_wide != wide || ctx->occ_stack_pt != lane_pt) {
         int per_cu = 0;
         uint32_t threads = 0;
-        hipError_t oe = rt_pathtrace_pick_config(mode, tris, wide, lds_bytes, stack_pt, ctx->force_threads,
+        hipError_t oe = rt_pathtrace_pick_config(mode, tris, wide, lds_bytes, lane_pt, ctx->force_threads,
                                                  ctx->waves_cap, &threads, &per_cu);
         if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
         ctx->occ_blocks_per_cu = per_cu;
@@ -1554,11 +1594,12 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ctx->occ_mode = mode;
         ctx->occ_tris = tris;
         ctx->occ_wide = wide;
-        ctx->occ_stack_pt = stack_pt;
+        ctx->occ_stack_pt = lane_pt;
     }
     // the stack after the scene image and its tail
     ka.lds_stack_offset = (uint32_t)al16(lds_bytes);
-    if (wide) lds_bytes = ka.lds_stack_offset + (size_t)ctx->occ_threads * stack_pt;
+    ka.lds_leafbatch_offset = ka.lds_stack_offset;
+    if (wide || coop) lds_bytes = ka.lds_stack_offset + (size_t)ctx->occ_threads * lane_pt;
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
     const uint64_t wanted = ((uint64_t)ka.queue_units + waves_per_block - 1) / waves_per_block;
@@ -1756,6 +1797,16 @@ int rt_synchronize(rt_ctx* ctx) {
     return RT_OK;
 }
 
+int rt_copy_output_to_device(rt_ctx* ctx, void* dst_device, uint32_t bytes_per_row) {
+    RT_ENTER(ctx);  // queued frames launched first: the copy sees the last frame's output
+    if (!dst_device) return fail(ctx, RT_E_INVALID, "rt_copy_output_to_device: dst_device is NULL");
+    if ((uint64_t)bytes_per_row < 4ull * ctx->width)
+        return fail(ctx, RT_E_INVALID, "rt_copy_output_to_device: bytes_per_row < 4 * width");
+    RT_HIP(ctx, hipMemcpy2DAsync(dst_device, bytes_per_row, ctx->d_out, 4u * (size_t)ctx->width,
+                                 4u * (size_t)ctx->width, ctx->height, hipMemcpyDeviceToDevice, ctx->stream));
+    return RT_OK;
+}
+
 int rt_read_output(rt_ctx* ctx, uint32_t* out) {
     RT_ENTER(ctx);
     if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
@@ -1862,6 +1913,7 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
         ctx->qnodes_dirty = true;
     }
     ctx->cones_dirty = true;  // the triangles changed
+    ctx->ltris_dirty = true;
     return RT_OK;
 }
 
@@ -2178,9 +2230,10 @@ int rt_debug_check_leaf_certificates(rt_ctx* ctx, uint32_t* mismatches, uint32_t
     return RT_OK;
 }
 
-int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
+int rt_launch_config(rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uint32_t* lds_bytes,
                      uint32_t* scene_in_lds) {
-    if (!ctx || !threads || !blocks || !lds_bytes || !scene_in_lds) return RT_E_INVALID;
+    RT_ENTER(ctx);  // the last launch: queued frames launched first
+    if (!threads || !blocks || !lds_bytes || !scene_in_lds) return RT_E_INVALID;
     *threads = ctx->occ_threads;
     *blocks = ctx->last_blocks;
     *lds_bytes = ctx->last_lds;
@@ -2188,8 +2241,9 @@ int rt_launch_config(const rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, uin
     return RT_OK;
 }
 
-int rt_last_launch_passes(const rt_ctx* ctx, uint32_t* passes) {
-    if (!ctx || !passes) return RT_E_INVALID;
+int rt_last_launch_passes(rt_ctx* ctx, uint32_t* passes) {
+    RT_ENTER(ctx);  // the last launch: queued frames launched first
+    if (!passes) return RT_E_INVALID;
     *passes = ctx->last_passes;
     return RT_OK;
 }

@@ -95,6 +95,13 @@ constexpr uint32_t kOrderBuckets = RT_ORDER_BUCKETS;
 constexpr size_t kLdsTailBytes = 1024 + 160;
 static_assert(kLdsTailBytes >= (kOrderBuckets * 16 + 1) * 4, "sort scratch fits the LDS tail");
 
+// Cooperative leaf batches (pathtrace.hip coop_leaf_batch): a leaf record's triangle block, and
+// the per-wave LDS scratch (one 48-B slot per lane: the ray and leaf of a pending lane, then its
+// leaf's result).
+constexpr uint32_t kLeafTriSlots = 8;                       // triangle slots per block (7 used)
+constexpr uint32_t kLeafTriWords = 3 * kLeafTriSlots;       // uint4 per block (384 B)
+constexpr uint32_t kLeafBatchWaveBytes = 64 * 48;
+
 // Diagnostic counters ahead of the per-wave records in KernelArgs::diag
 // (RT_DIAG: 10 counters; RT_DIAG_TAIL: 8, then 2 words per wave from here).
 constexpr uint32_t kDiagHeaderWords = 12;
@@ -180,6 +187,12 @@ struct KernelArgs {
     uint32_t tri_prune_mode;
     float tri_prune;
     const TriLeafCert* __restrict__ tri_leafcert;
+    // Leaf triangle blocks (walks from global memory, RT_COOP_LEAVES): per leaf record (tri_prims'
+    // indexing) kLeafTriWords uint4 -- piece p (0..2) of triangle slot j (0..7) at [8p + j], the
+    // first 48 B of the triangle's RtTriangleHot record, so piece p of a leaf's triangles is one
+    // 128-B line; slots past the leaf's count are zero. Null: the leaf batches test per lane.
+    const uint4* __restrict__ tri_leaftris;
+    uint32_t lds_leafbatch_offset;  // per wave kLeafBatchWaveBytes of LDS for the cooperative leaf batch
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     // Frame-parallel batch (frames > 1, accumulating): the queue holds one unit per

@@ -100,6 +100,10 @@ struct Worker {
     size_t send_cap = 0;
     void* recv_buf = nullptr;  // root only: world x stride blocks
     size_t recv_cap = 0;
+    // copy transport (RT_GROUP_COPY_TRANSPORT): this rank's block copied to the root on its own
+    // stream (ev_sent), the root's unpack done (ev_unpacked, root only), both on this device
+    hipEvent_t ev_sent = nullptr, ev_unpacked = nullptr;
+    bool unpacked_recorded = false;
 
     void run() {
         (void)hipSetDevice(device);
@@ -144,7 +148,8 @@ struct Worker {
 
 struct rt_group {
     std::vector<Worker*> workers;
-    std::vector<ncclComm_t> comms;
+    std::vector<ncclComm_t> comms;  // empty with the copy transport
+    bool copy_transport = false;
     rt_params params{};  // what the contexts were last given (the gather's divisor needs compute_per_frame)
     std::string err;
 };
@@ -192,6 +197,9 @@ void destroy_group(rt_group* g) {
                 if (wk.send_buf) (void)hipFree(wk.send_buf);
                 if (wk.recv_buf) (void)hipFree(wk.recv_buf);
                 wk.send_buf = wk.recv_buf = nullptr;
+                if (wk.ev_sent) (void)hipEventDestroy(wk.ev_sent);
+                if (wk.ev_unpacked) (void)hipEventDestroy(wk.ev_unpacked);
+                wk.ev_sent = wk.ev_unpacked = nullptr;
                 rt_destroy(wk.ctx);
                 wk.ctx = nullptr;
                 return RT_OK;
@@ -216,7 +224,15 @@ void destroy_group(rt_group* g) {
 extern "C" {
 
 int rt_create_multi(const rt_create_info* info, const int32_t* devices, uint32_t n_devices, rt_group** out) {
+    return rt_create_multi_ex(info, devices, n_devices, 0u, out);
+}
+
+int rt_create_multi_ex(const rt_create_info* info, const int32_t* devices, uint32_t n_devices, uint32_t flags,
+                       rt_group** out) {
     rt_set_global_error("");
+    if ((flags & ~RT_GROUP_COPY_TRANSPORT) != 0u)
+        return group_fail(nullptr, RT_E_INVALID, "rt_create_multi_ex: unknown flags");
+    const bool copy = (flags & RT_GROUP_COPY_TRANSPORT) != 0u;
     if (!info || !devices || !out) return group_fail(nullptr, RT_E_INVALID, "rt_create_multi: NULL argument");
     *out = nullptr;
     if (n_devices == 0) return group_fail(nullptr, RT_E_INVALID, "rt_create_multi: n_devices must be >= 1");
@@ -224,7 +240,7 @@ int rt_create_multi(const rt_create_info* info, const int32_t* devices, uint32_t
         return group_fail(nullptr, RT_E_INVALID,
                           "rt_create_multi: info must describe the whole frame (rank 0, world_size 0 or 1); "
                           "the group assigns rank r to devices[r]");
-    for (uint32_t i = 0; i < n_devices; i++)
+    for (uint32_t i = 0; i < n_devices && !copy; i++)
         for (uint32_t j = 0; j < i; j++)
             if (devices[i] == devices[j])
                 return group_fail(nullptr, RT_E_INVALID,
@@ -236,12 +252,12 @@ int rt_create_multi(const rt_create_info* info, const int32_t* devices, uint32_t
     for (uint32_t i = 0; i < n_devices; i++)
         if (devices[i] < 0 || devices[i] >= n_dev)
             return group_fail(nullptr, RT_E_NODEVICE, "rt_create_multi: device ordinal out of range");
-    Rccl& R = rccl();
-    if (!R.loaded) return group_fail(nullptr, RT_E_NODEVICE, "rt_create_multi: " + R.error);
+    if (!copy && !rccl().loaded) return group_fail(nullptr, RT_E_NODEVICE, "rt_create_multi: " + rccl().error);
 
     rt_group* g = new (std::nothrow) rt_group();
     if (!g) return group_fail(nullptr, RT_E_NOMEM, "out of host memory");
     g->params = info->params;
+    g->copy_transport = copy;
     for (uint32_t r = 0; r < n_devices; r++) {
         Worker* w = new (std::nothrow) Worker();
         if (!w) {
@@ -268,7 +284,12 @@ int rt_create_multi(const rt_create_info* info, const int32_t* devices, uint32_t
         destroy_group(g);
         return group_fail(nullptr, rc, "rt_create_multi: " + msg);
     }
+    if (copy) {  // no communicators: the gather copies blocks device to device
+        *out = g;
+        return RT_OK;
+    }
     // one communicator per device, in this process
+    Rccl& R = rccl();
     g->comms.assign(n_devices, nullptr);
     std::vector<int> devlist(devices, devices + n_devices);
     const ncclResult_t nr = R.comm_init_all(g->comms.data(), (int)n_devices, devlist.data());
@@ -397,32 +418,81 @@ int rt_gather_frame(rt_group* g, uint32_t root, uint32_t payload) {
         return group_fail(g, RT_E_INVALID,
                           "rt_gather_frame: a non-accumulating render never writes its accumulation "
                           "(compute_shader.wgsl:171-178); gather the image");
-    Rccl& R = rccl();
     const size_t px_bytes = payload == RT_GATHER_IMAGE ? 4 : 16;
     // every block padded to rank 0's (the largest) pixel count
     uint64_t stride_px = 0;
     if (rt_owned_pixel_count(g->workers[0]->ctx, 0, n, &stride_px) != RT_OK)
         return group_fail(g, RT_E_INVALID, "rt_gather_frame: bad context");
     const size_t block = (size_t)stride_px * px_bytes;
-    // 1. on every device: queued frames launched, its tiles packed on its stream
-    std::vector<hipStream_t> streams(n, nullptr);
+    Worker* rw = g->workers[root];
+    const bool copy = g->copy_transport;
+    // 0. buffers (the root's receive slots must exist before another rank copies into them)
     int rc = run_all(g, [&](Worker& w) {
         int r = ensure_device_buffer(w, &w.send_buf, &w.send_cap, block);
         if (r == RT_OK && w.rank == root) r = ensure_device_buffer(w, &w.recv_buf, &w.recv_cap, block * n);
-        if (r != RT_OK) return r;
-        r = payload == RT_GATHER_IMAGE ? rt_pack_owned_output(w.ctx, w.send_buf)
-                                       : rt_pack_owned_accumulation(w.ctx, w.send_buf);
-        if (r != RT_OK) return r;
-        streams[w.rank] = static_cast<hipStream_t>(rt_stream(w.ctx));
-        return streams[w.rank] ? RT_OK : RT_E_HIP;
+        if (r == RT_OK && copy) {
+            if (!w.ev_sent && hipEventCreateWithFlags(&w.ev_sent, hipEventDisableTiming) != hipSuccess) r = RT_E_HIP;
+            if (!w.ev_unpacked && hipEventCreateWithFlags(&w.ev_unpacked, hipEventDisableTiming) != hipSuccess)
+                r = RT_E_HIP;
+        }
+        return r;
     });
     if (rc != RT_OK) return rc;
+    // 1. on every device: queued frames launched, its tiles packed on its stream (copy
+    // transport: then copied into slot r of the root's receive buffer on the same stream,
+    // once the root has unpacked the previous gather out of it)
+    std::vector<hipStream_t> streams(n, nullptr);
+    uint8_t* const recv = static_cast<uint8_t*>(rw->recv_buf);
+    const int root_dev = rw->device;
+    hipEvent_t const prev_unpacked = rw->unpacked_recorded ? rw->ev_unpacked : nullptr;
+    rc = run_all(g, [&](Worker& w) {
+        int r = payload == RT_GATHER_IMAGE ? rt_pack_owned_output(w.ctx, w.send_buf)
+                                           : rt_pack_owned_accumulation(w.ctx, w.send_buf);
+        if (r != RT_OK) return r;
+        hipStream_t s = static_cast<hipStream_t>(rt_stream(w.ctx));
+        streams[w.rank] = s;
+        if (!s) return RT_E_HIP;
+        if (copy) {
+            if (prev_unpacked && hipStreamWaitEvent(s, prev_unpacked, 0) != hipSuccess) return RT_E_HIP;
+            if (hipMemcpyPeerAsync(recv + (size_t)w.rank * block, root_dev, w.send_buf, w.device, block, s) !=
+                    hipSuccess ||
+                hipEventRecord(w.ev_sent, s) != hipSuccess)
+                return RT_E_HIP;
+        }
+        return RT_OK;
+    });
+    if (rc != RT_OK) return rc;
+    if (copy) {
+        // 3. the root waits for every copy, unpacks every block, and marks its receive
+        // buffer free for the next gather's copies
+        uint32_t k = 1;
+        (void)rt_accumulation_index(rw->ctx, &k);
+        const uint32_t divisor = std::max<uint32_t>(k - 1, 1) * std::max<uint32_t>(g->params.compute_per_frame, 1);
+        std::vector<hipEvent_t> sent(n);
+        for (uint32_t r = 0; r < n; r++) sent[r] = g->workers[r]->ev_sent;
+        const uint64_t t = rw->post([=](Worker& w) {
+            hipStream_t s = static_cast<hipStream_t>(rt_stream(w.ctx));
+            for (hipEvent_t ev : sent)
+                if (hipStreamWaitEvent(s, ev, 0) != hipSuccess) return (int)RT_E_HIP;
+            const int r = payload == RT_GATHER_IMAGE ? rt_unpack_output_ranks(w.ctx, w.recv_buf, stride_px, n, n)
+                                                     : rt_unpack_accumulation_ranks(w.ctx, w.recv_buf, stride_px, n,
+                                                                                    n, divisor);
+            if (r != RT_OK) return r;
+            if (hipEventRecord(w.ev_unpacked, s) != hipSuccess) return (int)RT_E_HIP;
+            w.unpacked_recorded = true;
+            return (int)RT_OK;
+        });
+        std::string msg;
+        rc = rw->wait(t, &msg);
+        if (rc != RT_OK) g->err = msg.empty() ? "rt_gather_frame: copy transport failed" : msg;
+        return rc;
+    }
+    Rccl& R = rccl();
     // 2. one grouped send/recv: rank r's block to slot r of the root's buffer
     // (the root's own block too, a local copy: one unpack launch then covers every
     // block, and a one-GPU group moves its data through RCCL like any other)
     if (R.group_start() != ncclSuccess) return group_fail(g, RT_E_HIP, "ncclGroupStart failed");
     ncclResult_t nr = ncclSuccess;
-    Worker* rw = g->workers[root];
     for (uint32_t r = 0; r < n && nr == ncclSuccess; r++) {
         Worker* w = g->workers[r];
         nr = R.send(w->send_buf, block, ncclUint8, (int)root, g->comms[r], streams[r]);

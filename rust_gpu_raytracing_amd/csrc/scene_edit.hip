@@ -446,3 +446,37 @@ hipError_t rt_launch_tri_leafcert(const SubObjectPrim* prims, uint32_t n_prims, 
                        subs, tris, n_tri, out);
     return hipGetLastError();
 }
+
+// Leaf triangle blocks (KernelArgs::tri_leaftris), one per leaf record, for the cooperative leaf
+// batches of the walks from global memory (pathtrace.hip coop_leaf_batch): piece p (0..2) of
+// triangle slot j at word 8p + j -- the record's own first 48 B (a, edge_ab, edge_ac,
+// calc_normal), bit for bit, at the same index clamp as the per-lane leaf test -- so that the
+// 8 lanes testing one leaf read one 128-B line per piece. Slots past the leaf's count, and
+// leaves whose triangle range is not in the record (kPrimRangeNone: those are tested per
+// lane), are zero. Rebuilt with the certificates after every change of the accelerator or the
+// triangles. One thread per word.
+extern "C" __global__ void __launch_bounds__(256) rt_tri_leaftris_kernel(const SubObjectPrim* __restrict__ prims,
+                                                                        uint32_t n_prims,
+                                                                        const RtTriangleHot* __restrict__ tris,
+                                                                        uint32_t n_tri, uint4* __restrict__ out) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (uint64_t)n_prims * kLeafTriWords) return;
+    const uint32_t i = (uint32_t)(gid / kLeafTriWords), w = (uint32_t)(gid % kLeafTriWords);
+    const uint32_t j = w % kLeafTriSlots, piece = w / kLeafTriSlots;
+    const uint32_t range = prims[i].range;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (range != kPrimRangeNone && j < (range >> 27) && n_tri != 0u) {
+        const uint4* t = reinterpret_cast<const uint4*>(tris + min((range & ((1u << 27) - 1u)) + j, n_tri - 1u));
+        v = t[piece];
+    }
+    out[gid] = v;
+}
+
+hipError_t rt_launch_tri_leaftris(const SubObjectPrim* prims, uint32_t n_prims, const RtTriangleHot* tris,
+                                  uint32_t n_tri, uint4* out, hipStream_t stream) {
+    if (n_prims == 0 || !out) return hipSuccess;
+    const uint64_t n = (uint64_t)n_prims * kLeafTriWords;
+    hipLaunchKernelGGL(rt_tri_leaftris_kernel, dim3((uint32_t)((n + 255u) / 256u)), dim3(256), 0, stream, prims,
+                       n_prims, tris, n_tri, out);
+    return hipGetLastError();
+}

@@ -28,7 +28,11 @@ GATHER_PAYLOADS = {"image": N.RT_GATHER_IMAGE, "accumulation": N.RT_GATHER_ACCUM
 
 class RendererGroup:
     def __init__(self, scene: RenderScene, devices, *, accumulate: bool = True, compute_per_frame: int = 1,
-                 camera_rays: np.ndarray | None = None, frame_batch: int = 1, lib=None):
+                 camera_rays: np.ndarray | None = None, frame_batch: int | None = None, copy_transport: bool = False,
+                 lib=None):
+        """``copy_transport``: rt_create_multi_ex(RT_GROUP_COPY_TRANSPORT) -- no RCCL; the gather
+        copies blocks device to device, and a device may be listed more than once (several
+        ranks on one GPU: the group's N-rank logic on a one-GPU machine)."""
         self._lib = N.load_library() if lib is None else lib
         self.scene = scene
         self.accumulate = accumulate
@@ -54,7 +58,8 @@ class RendererGroup:
         info.rank, info.world_size = 0, 1
         devs = (ctypes.c_int32 * len(self.devices))(*self.devices)
         g = ctypes.c_void_p()
-        rc = self._lib.rt_create_multi(ctypes.byref(info), devs, len(self.devices), ctypes.byref(g))
+        flags = N.RT_GROUP_COPY_TRANSPORT if copy_transport else 0
+        rc = self._lib.rt_create_multi_ex(ctypes.byref(info), devs, len(self.devices), flags, ctypes.byref(g))
         N.check(None, rc, self._lib)
         self._g = g
         tex = np.ascontiguousarray(scene.textures, np.uint8)
@@ -63,7 +68,7 @@ class RendererGroup:
         env = np.ascontiguousarray(scene.environment_map, np.uint8)
         eh, ew, _ = env.shape
         self._call("rt_group_upload_env_map", N.ptr(env), ew, eh)
-        if frame_batch != 1:
+        if frame_batch is not None:
             self._call("rt_group_set_frame_batch", frame_batch)
 
     def _params(self, accumulation_index: int) -> np.ndarray:
@@ -104,6 +109,15 @@ class RendererGroup:
     def update_ray_directions(self, rays: np.ndarray) -> None:
         rays = np.ascontiguousarray(rays, dtype=B.RAY)
         self._call("rt_group_update_ray_directions", N.ptr(rays), rays.shape[0])
+
+    def update_camera(self, camera) -> None:
+        """src/renderer.rs:109-129 on every device: reset, new origin, new ray directions."""
+        self.scene.camera = camera
+        self.reset_accumulation()
+        rc = N.rt_ray_camera()
+        rc.origin[:] = [float(x) for x in camera.position]
+        self._call("rt_group_update_camera", ctypes.byref(rc))
+        self.update_ray_directions(camera.recalculate_ray_directions())
 
     def update_materials(self, materials: np.ndarray) -> None:
         m = np.ascontiguousarray(materials, dtype=B.MATERIAL)

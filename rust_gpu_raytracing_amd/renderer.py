@@ -43,7 +43,7 @@ class Renderer:
         world_size: int = 1,
         camera_rays: np.ndarray | None = None,
         device_rays: bool | None = None,
-        frame_batch: int = 1,
+        frame_batch: int | None = None,
         lib=None,
     ):
         """``camera_rays``: explicit per-pixel directions (the reference's ray buffer;
@@ -53,7 +53,8 @@ class Renderer:
         2% slower on C2 than reading the buffer, so off by default).
         ``frame_batch``: frames one launch may render (rt_set_frame_batch): with
         F > 1, ``compute_frame`` queues frames and launches F at a time (or at the
-        next readback / update / sync), each frame's results written as before."""
+        next readback / update / sync), each frame's results written as before.
+        None keeps the library's default (RT_DEFAULT_FRAME_BATCH, include/rt_abi.h)."""
         self._lib = N.load_library() if lib is None else lib
         self.scene = scene
         self.accumulate = accumulate
@@ -86,7 +87,7 @@ class Renderer:
         self.device_rays = bool(device_rays)
         if self.device_rays:
             self._set_camera_matrices(scene.camera)
-        if frame_batch != 1:
+        if frame_batch is not None:
             self.set_frame_batch(frame_batch)
 
     # ------------------------------------------------------------------ helpers
@@ -273,6 +274,12 @@ class Renderer:
         out = np.zeros((self.height, bpr), np.uint8)
         self._call("rt_read_output_pitched", N.ptr(out), bpr)
         return out
+
+    def copy_output_to_device(self, dst_device_ptr: int, bytes_per_row: int) -> None:
+        """``Renderer::update_texture`` on the device (src/renderer.rs:254-283): the packed
+        output copied into device memory at ``dst_device_ptr`` with a row pitch, stream-ordered
+        and asynchronous (rt_copy_output_to_device) -- a display loop's observation point."""
+        self._call("rt_copy_output_to_device", ctypes.c_void_p(dst_device_ptr), bytes_per_row)
 
     def image(self) -> np.ndarray:
         """The displayed frame as an (height, width, 4) RGBA8 array (R first)."""

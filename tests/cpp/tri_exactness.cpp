@@ -108,6 +108,12 @@ static uint32_t g_subtree_max = 0;
 // experiment (TRI_DEPTH_HIST): the certified walk's node visits by tree depth (octant layouts)
 static std::vector<uint8_t> g_depth;
 static long g_depth_visits[64] = {0};
+// the kernel's default walk since round 5 (pathtrace.hip): the certificate test deferred to the
+// leaf batch through the gap node_step records (tri_leafcert_skips_gap, RT_LEAFCERT_DEFER) and the
+// leaf's triangles tested as a cooperative batch -- every candidate on its own, then the
+// lexicographic minimum and a NaN flag merged by the leaf's lane (coop_leaf_batch)
+static bool g_kernel_default = false;
+static long g_gap_checked = 0, g_gap_skipped = 0, g_coop_leaves = 0, g_coop_nan = 0;
 
 static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
                  const std::vector<rt_scene_triangle>& tr, V o, V d, float scale) {
@@ -171,8 +177,18 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
             const float t1x = fminf(fmaf(nd.bmin[0], sr.ix, sr.lx), fmaf(nd.bmax[0], sr.ix, sr.hx));
             const float t1y = fminf(fmaf(nd.bmin[1], sr.iy, sr.ly), fmaf(nd.bmax[1], sr.iy, sr.hy));
             const float t1z = fminf(fmaf(nd.bmin[2], sr.iz, sr.lz), fmaf(nd.bmax[2], sr.iz, sr.hz));
-            skip = tri_leafcert_skips((*g_lcert)[nd.leaf & 0xffffffu].w, tcr, best, t1x, t1y, t1z, fabsf(sr.ix),
-                                      fabsf(sr.iy), fabsf(sr.iz));
+            if (g_kernel_default) {
+                // node_step's gap (pathtrace.hip, RT_LEAFCERT_DEFER), then the leaf batch's test
+                const float tbs = best * (1.0f + 0x1p-20f);
+                const float gx = (t1x - tbs) * fabsf(d.x), gy = (t1y - tbs) * fabsf(d.y), gz = (t1z - tbs) * fabsf(d.z);
+                const float gap = fmaxf(fmaxf(gx, gy), gz) * (1.0f - 0x1p-20f);
+                skip = gap > 0.0f ? tri_leafcert_skips_gap((*g_lcert)[nd.leaf & 0xffffffu].w, tcr, best, gap) : 0u;
+                g_gap_checked += gap > 0.0f;
+                g_gap_skipped += skip == kLeafCertAll;
+            } else {
+                skip = tri_leafcert_skips((*g_lcert)[nd.leaf & 0xffffffu].w, tcr, best, t1x, t1y, t1z, fabsf(sr.ix),
+                                          fabsf(sr.iy), fabsf(sr.iz));
+            }
             g_lcert_leaves++;
             if (skip == kLeafCertAll) {
                 hit = false;
@@ -191,7 +207,45 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
                 printf("PRIM RANGE mismatch\n");
                 exit(1);
             }
-            if (rib(o, inv, OB.min_bounds, OB.max_bounds) && (lazy || rib(o, inv, s.min_bounds, s.max_bounds))) {
+            if (g_kernel_default && lazy && count < 8u && rib(o, inv, OB.min_bounds, OB.max_bounds)) {
+                // coop_leaf_batch: every triangle tested on its own (lane j), the group's minimum of
+                // (distance, sweep position) and NaN flag, then the leaf's lane merges
+                g_coop_leaves++;
+                float cd = INFINITY;
+                uint32_t cs = 0xffffffffu;
+                int cti = -1, cfront = 0;
+                bool cnan = false;
+                for (uint32_t j = 0; j < count; j++) {
+                    g_exact_tests++;
+                    const rt_scene_triangle& t = tr[std::min<uint32_t>(first + j, (uint32_t)tr.size() - 1u)];
+                    V cn = ld(t.calc_normal);
+                    float det = -dot(d, cn), inv_det = 1.0f / det;
+                    V ao = sub(o, ld(t.a));
+                    float dist = dot(ao, cn) * inv_det;
+                    V dao = cross(ao, d);
+                    float v = -dot(ld(t.edge_ab), dao) * inv_det;
+                    float u = dot(ld(t.edge_ac), dao) * inv_det;
+                    float w = 1.0f - u - v;
+                    if (dist < 0.0f || v < 0.0f || u < 0.0f || w < 0.0f) continue;
+                    if (dist != dist) { cnan = true; continue; }
+                    const uint32_t seq = p.seq_base + j;
+                    if (dist < cd || (dist == cd && seq < cs)) {
+                        cd = dist;
+                        cs = seq;
+                        cti = (int)(first + j);
+                        cfront = det > 0.0f;
+                    }
+                }
+                const bool beats = cd < best || (cd == best && cs < best_seq);
+                if ((cnan || beats) && rib(o, inv, s.min_bounds, s.max_bounds)) {
+                    if (cnan) { nan_hit = true; g_coop_nan++; }
+                    if (beats) {
+                        best = cd;
+                        best_seq = cs;
+                        r = {cd, cti, (int)p.object, cfront};
+                    }
+                }
+            } else if (rib(o, inv, OB.min_bounds, OB.max_bounds) && (lazy || rib(o, inv, s.min_bounds, s.max_bounds))) {
                 for (uint32_t j = 0; j < count; j++) {
                     if ((skip >> j) & 1u) {
                         g_lcert_tris++;
@@ -444,19 +498,29 @@ int main(int argc, char** argv) {
         // the certified walk (tri_cone.h leaf certificates) over the same layouts
         g_lcert = &lcert;
         Res x = accel(A, ob, sb, tr, o, d, scale);
+        // the kernel's default walk (round 5): deferred certificate test + cooperative leaf batches
+        g_kernel_default = true;
+        const long saved_nodes = g_exact_nodes, saved_tests = g_exact_tests;
+        Res y = accel(A, ob, sb, tr, o, d, scale);
+        g_exact_nodes = saved_nodes;
+        g_exact_tests = saved_tests;
+        g_kernel_default = false;
         g_lcert = nullptr;
         g_oct = nullptr;
         g_qoct = nullptr;
         g_q = nullptr;
         g_lazy = false;
-        for (const Res* x : {&b, &c, &e, &f, &h, &x}) {
+        const Res* const walks[] = {&b, &c, &e, &f, &h, &x, &y};
+        const char* const names[] = {"binary", "wide", "qnodes", "qnodes+lazy", "octants+prune", "certified",
+                                     "kernel-default"};
+        for (int wi = 0; wi < 7; wi++) {
+            const Res* w = walks[wi];
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
-            memcpy(&tb, &x->t, 4);
-            if (ta != tb || a.tri != x->tri || a.obj != x->obj || a.front != x->front) {
+            memcpy(&tb, &w->t, 4);
+            if (ta != tb || a.tri != w->tri || a.obj != w->obj || a.front != w->front) {
                 printf("MISMATCH (%s) ray %ld o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) sweep=(%d/%d %.9g) accel=(%d/%d %.9g)\n",
-                       x == &b ? "binary" : x == &c ? "wide" : x == &e ? "qnodes" : x == &f ? "qnodes+lazy" : x == &h ? "octants+prune" : "certified", i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, x->obj, x->tri,
-                       x->t);
+                       names[wi], i, o.x, o.y, o.z, d.x, d.y, d.z, a.obj, a.tri, a.t, w->obj, w->tri, w->t);
                 return 1;
             }
         }
@@ -473,6 +537,7 @@ int main(int argc, char** argv) {
            (double)g_lcert_leaves / n, (double)g_lcert_skipped / n, (double)g_lcert_tris / n, lcert_valid,
            lcert.size());
     printf("heuristic_misses %ld\n", g_heur_miss);
+    printf("kernel_default %ld %ld %ld %ld\n", g_gap_checked, g_gap_skipped, g_coop_leaves, g_coop_nan);
     if (!g_depth.empty()) {  // depth, visits per ray at that depth, nodes of one layout at that depth
         std::vector<long> per(64, 0);
         for (size_t i = 0; i < A.nodes.size(); i++) per[std::min<int>(g_depth[i], 63)]++;

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.rt_abi_version() == 10
+    assert native_lib.rt_abi_version() == 11
 
 
 def test_library_built_from_these_sources(native_lib):
@@ -147,3 +147,27 @@ def test_null_group_calls_fail_cleanly(native_lib):
     assert native_lib.rt_group_size(None) == 0
     assert native_lib.rt_group_context(None, 0) is None
     native_lib.rt_destroy_multi(None)
+
+
+def test_create_multi_ex_flags_without_device(native_lib):
+    """rt_create_multi_ex: unknown flags are refused; with RT_GROUP_COPY_TRANSPORT a device may
+    repeat (several ranks on one GPU), so [0, 0, 0] passes the argument checks and, with no GPU
+    in the CPU suite, stops at RT_E_NODEVICE instead of the "listed twice" refusal."""
+    info = N.rt_create_info()
+    info.width, info.height = 16, 8
+    devs = (ctypes.c_int32 * 3)(0, 0, 0)
+    g = ctypes.c_void_p()
+    rc = native_lib.rt_create_multi_ex(ctypes.byref(info), devs, 3, 0x80, ctypes.byref(g))
+    assert rc == N.RT_E_INVALID and not g.value and b"flags" in native_lib.rt_last_error(None)
+    rc = native_lib.rt_create_multi_ex(ctypes.byref(info), devs, 3, 0, ctypes.byref(g))
+    assert rc == N.RT_E_INVALID and b"twice" in native_lib.rt_last_error(None)
+    rc = native_lib.rt_create_multi_ex(ctypes.byref(info), devs, 3, N.RT_GROUP_COPY_TRANSPORT, ctypes.byref(g))
+    assert rc in (N.RT_E_NODEVICE, N.RT_OK)
+    if rc == N.RT_OK:  # pragma: no cover - a box with a GPU
+        native_lib.rt_destroy_multi(g)
+
+
+def test_header_constants_match_binding():
+    text = HEADER.read_text()
+    assert re.search(r"#define RT_DEFAULT_FRAME_BATCH (\d+)", text).group(1) == str(N.RT_DEFAULT_FRAME_BATCH)
+    assert re.search(r"#define RT_GROUP_COPY_TRANSPORT (\d+)u", text).group(1) == str(N.RT_GROUP_COPY_TRANSPORT)

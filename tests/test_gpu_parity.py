@@ -37,13 +37,17 @@ def gpu_render(scene, bounces, frames, *, spp=1, accumulate=1, rays=None, **kw):
         return r.read_accumulation(), r.read_output(), r.ray_count()
 
 
+# frame_batch None: the library default (frames queued, launched at the readback: batched
+# launches); 1: one launch per compute_frame, the reference's dispatch pattern
+@pytest.mark.parametrize("batch", [None, 1])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_gpu_matches_golden(gpu, name):
+def test_gpu_matches_golden(gpu, name, batch):
     g = load(name)
     case = CASES[name]
     scene = scene_from_inputs(g)
     acc, out, rays = gpu_render(scene, case["bounces"], case["frames"], spp=case["spp"],
-                                accumulate=case["accumulate"], rays=g["camera_rays"].astype(B.RAY))
+                                accumulate=case["accumulate"], rays=g["camera_rays"].astype(B.RAY),
+                                frame_batch=batch)
     assert_same(acc, out, rays, g["accum"], g["out"], int(g["rays"]))
 
 
@@ -54,10 +58,11 @@ def test_gpu_matches_golden(gpu, name):
     ("c4_mixed", 256, 144, 2, dict(env_size=(1024, 512))),
     ("c5_heightfield", 192, 112, 2, dict(nx=160, nz=80)),
 ])
-def test_gpu_matches_oracle_full_frame(gpu, oracle_lib, config, w, h, frames, kw):
+@pytest.mark.parametrize("batch", [None, 1])
+def test_gpu_matches_oracle_full_frame(gpu, oracle_lib, config, w, h, frames, kw, batch):
     scene, bounces = build_config(config, width=w, height=h, **kw)
     acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, frames)
-    acc, out, rays = gpu_render(scene, bounces, frames)
+    acc, out, rays = gpu_render(scene, bounces, frames, frame_batch=batch)
     assert_same(acc, out, rays, acc_o, out_o, rays_o)
 
 
@@ -419,6 +424,42 @@ def test_gpu_sub_objects_in_lds(gpu, oracle_lib, monkeypatch, stage):
     assert_same(acc, out, n, acc_o, out_o, n_o)
 
 
+def test_gpu_default_batching_and_device_display_copy(gpu, oracle_lib):
+    """ABI 11: by default rt_compute_frame queues its frame (RT_DEFAULT_FRAME_BATCH) and the
+    next observation launches the queue. The reference's loop -- one compute_frame per frame,
+    a display copy every ~6 frames (src/renderer.rs:201-283, src/main.rs:88-92) -- through
+    rt_copy_output_to_device (update_texture's buffer-to-texture copy, on the device, with
+    the 256-B row pitch): every displayed image equals the oracle's output after that frame."""
+    import torch
+
+    scene, bounces = build_config("c2_rtiow", width=200, height=112)
+    rays = scene.camera.recalculate_ray_directions()
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc_o = np.zeros((o.height, o.width, 4), np.float32)
+    out_o = np.zeros((o.height, o.width), np.uint32)
+    with Renderer(scene, camera_rays=rays) as r:
+        assert r.frame_batch() == (N.RT_DEFAULT_FRAME_BATCH, 0)
+        lib = r._lib
+        bpr = int(lib.rt_bytes_per_row(r.width, 256))
+        disp = torch.full((r.height * bpr,), 0xAB, dtype=torch.uint8, device="cuda")
+        shown = 0
+        for k in range(1, 21):
+            r.compute_frame(bounces)
+            o.render_frame(scene.params(accumulation_index=k), bounces, acc_o, out_o)
+            assert r.frame_batch()[1] == k - 6 * shown  # queued, nothing launched yet
+            if k % 6 == 0:
+                r.copy_output_to_device(disp.data_ptr(), bpr)
+                shown += 1
+                assert r.frame_batch()[1] == 0
+                r.synchronize()  # the copy is ordered on the renderer's stream, not torch's
+                img = disp.cpu().numpy().reshape(r.height, bpr)
+                assert np.array_equal(img[:, : 4 * r.width].copy().view(np.uint32), out_o)
+                assert (img[:, 4 * r.width:] == 0xAB).all()  # the pitch padding untouched
+        with pytest.raises(RtError):
+            r.copy_output_to_device(disp.data_ptr(), 4 * r.width - 4)
+        assert np.array_equal(r.read_accumulation().view(np.uint32), acc_o.view(np.uint32))
+
+
 def test_gpu_last_launch_passes(gpu):
     """rt_last_launch_passes names the kernels a dispatch ran (the bench's roofline uses it)."""
     scene, bounces = build_config("c2_rtiow", width=64, height=48)
@@ -758,7 +799,7 @@ def test_gpu_capacity_and_validation(gpu):
 
 def test_gpu_determinism_and_timing(gpu):
     scene, bounces = build_config("c2_rtiow", width=256, height=144)
-    with Renderer(scene) as r:
+    with Renderer(scene, frame_batch=1) as r:  # one timed launch per frame
         r.set_timing(True)
         for _ in range(3):
             r.compute_frame(bounces)

@@ -124,6 +124,9 @@ def test_nan_distance_falls_back_to_the_sweep(harness, tmp_path):
     out = run(harness, tmp_path, objs, o.sub_object_info.astype(B.SUB_OBJECT_INFO), t, rays)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
     assert int(out.stdout.splitlines()[0].split()[-1]) >= 1  # the fallback ran
+    # the kernel's default walk (cooperative leaf batches) met the NaN distance in its merge too
+    gap_checked, gap_skipped, coop_leaves, coop_nan = map(int, line(out, "kernel_default"))
+    assert coop_leaves > 0 and coop_nan > 0
 
 
 def test_margin_is_load_bearing(harness, tmp_path):
@@ -191,6 +194,13 @@ def test_adversarial_grazing_rays_certified_pruning(harness, tmp_path, seed, h_r
     assert int(valid) == int(total)  # every leaf of the grid carries a certificate
     if c_range[1] >= 1e-3:
         assert float(skipped) > 0  # and where the bound allows, the certified walk does skip leaves
+    # the kernel's default walk on the same rays (exact: checked ray by ray above): the certificate
+    # test deferred through node_step's gap (tri_leafcert_skips_gap) and the cooperative leaf batch's
+    # merge; the deferred test does run, and skips whole leaves where the bound allows
+    gap_checked, gap_skipped, coop_leaves, coop_nan = map(int, line(out, "kernel_default"))
+    assert gap_checked > 0 and coop_leaves > 0
+    if c_range[1] >= 1e-3:
+        assert gap_skipped > 0
 
 
 def test_certified_pruning_real_scenes(harness, tmp_path):
