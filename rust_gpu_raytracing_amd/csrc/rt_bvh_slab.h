@@ -68,32 +68,68 @@ RT_SLAB_FN SlabRay slab_ray(float ox, float oy, float oz, float inv_x, float inv
     return r;
 }
 
-// Culling bounds of the sphere BVH for one ray, with X =
-// |o| + extent >= |o - C| for every BVH sphere (centre C, radius r in
-// [r_min, r_max]) and u = 2^-24:
+// Culling bounds of the sphere BVH for one ray. A BVH sphere (centre C, f32
+// radius r, rho = fl(r * r), r' = sqrt(rho) <= r (1 + u)) may be skipped only where the
+// reference's own test (check_spheres, compute_shader.wgsl:372-391) cannot accept it. Inputs are
+// the f32 values the kernel reads; u = 2^-24, gamma_k = k u / (1 - k u); x = o - C exactly,
+// X = |o| + extent >= |x| + r (extent = max over BVH spheres of |C| + r, rounded up).
 //
-//  * lateral (position units, the box inflation). The reference's float
-//    discriminant (:372-379) differs from the exact 4|d|^2 (r^2 - p^2) (p = the
-//    distance from C to the ray line) by at most |d|^2 (80u X^2 + 24u r^2) to
-//    first order, so `disc >= 0` implies p^2 <= r^2 (1 + 8u) + 20u X^2, i.e.
-//    p - r <= min(10u X^2 / r, sqrt(20u) X) + 4u r. Taken 4x, plus the
-//    builder's f32 box rounding and this slab test's own (<= ~2u X each, 16u X
-//    allowed).
-//  * slack (parameter units, for the depth tests `far >= -slack` and
-//    `near <= limit + slack`). The float near root lies at most
-//    sqrt(|E|) / (2|d|^2) <= sqrt(20u) (X + r) / |d| (+ ~6u X / |d| of
-//    rounding) before the exact entry point, or -- for a line that misses the
-//    exact sphere but still has disc >= 0 -- before the closest-approach point,
-//    which lies inside the laterally inflated box. Taken 4x.
+// The reference computes, one rounding per operation: oc = fl(o - C) (|oc - x| <= u |x|),
+// a = fl(d.d), g = fl(d.oc), b = 2 g, q = fl(oc.oc), c = fl(q - rho), disc = fl(fl(b b) -
+// fl(4 a c)). Its exact counterpart D = B^2 - 4 A Cc with A = d.d, B = 2 d.x, Cc = x.x - rho is
+// 4 |d|^2 (rho - p^2), p the distance from C to the ray's line. With the standard dot-product
+// bound |fl(v.w) - v.w| <= gamma_3 |v| |w|:
+//   |g - d.x|       <= (gamma_3 (1 + u) + u) |d| X                  =: e_g |d| X,  e_g <= 4.01u
+//   |fl(b b) - B^2| <= |d|^2 X^2 (8 e_g + 4 e_g^2 + 4u (1 + e_g)^2)  <= 36.2u |d|^2 X^2
+//   |a - A|         <= gamma_3 |d|^2
+//   |q - x.x|       <= (2u + u^2 + gamma_3 (1 + u)^2) X^2           =: e_q X^2,    e_q <= 5.01u
+//   |c - Cc|        <= e_q X^2 + u (q + rho) <= (e_q + u (1 + e_q)) X^2 + u rho
+//   |fl(4 a c) - 4 A Cc| <= 4 |d|^2 ((gamma_3 + e_q + u) X^2 + (gamma_3 + u) rho) (1 + 4u)
+//                        + 4u |d|^2 (1 + gamma_3) (X^2 + rho)  <= |d|^2 (40.1u X^2 + 20.1u rho)
+//   |disc - D| <= the two above + u |fl(b b) - fl(4 a c)|, and |fl(b b) - fl(4 a c)| <=
+//   |D| + both <= 4.01 |d|^2 (X^2 + rho), so
+//       |disc - D| <= |d|^2 (81u X^2 + 25u rho) + E_sub,
+// every second-order term above absorbed in the rounded-up integer coefficients (they are
+// O(u^2), below 10^-5 of u), and E_sub <= 20 x 2^-150 the absolute rounding of products that
+// underflow. Overflow cannot let the test accept: an infinite or NaN b b, 4 a c or disc makes
+// disc NaN, -inf, or +inf with t = -inf or NaN, all rejected by `t > 0`. The bound is used only
+// for |d|^2 >= 2^-60 (below that E_sub / |d|^2 is not negligible: sphere_cull_bounds returns
+// infinite bounds, the walk culls nothing and tests every BVH sphere -- exact).
 //
-// With the RTIOW field (r = 0.2, X ~ 30) the lateral inflation is ~0.011
-// instead of the 0.12 of the r-independent sqrt(u) X bound alone.
+//  * lateral (position units, the box inflation). disc >= 0 => D >= -|disc - D| =>
+//    p^2 <= rho + delta, delta = 6.25u rho + 20.25u X^2 + E_sub / (4 |d|^2) (<= 6.25u rho + 20.25u
+//    X^2 + 1e-27), so p - r' <= min(delta / (2 r'), sqrt(delta)) <= min(13.25u X^2 / r_min,
+//    7 sqrt(u) X) + 1e-13 (X >= r' >= r_min). The box the builder stores contains C +- r rounded
+//    outward, and r' - r <= u r; this slab test's own rounding in position units is <= 4u (|lo| +
+//    |o| + m) <= 16u X (its FMA form, above). The margin below uses 40u X^2 / r_min and
+//    4.4e-3 X (>= 3x and 2.5x the derived terms) + 16u X + 16u r_max + 1e-6.
+//  * slack (parameter units, for the depth tests `far >= -slack` and `near <= limit + slack`).
+//    The accepted root t = fl(fl(-b - fl(sqrt(disc))) / fl(2 a)) is within
+//    (|b - B| + sqrt|disc - D| + u |b + s|) / (2 a) (1 + gamma_3) + 3u |t| of t_ref = (-B -
+//    sqrt(max(D, 0))) / (2 A): the exact entry point when the line meets the sphere, else the
+//    closest-approach parameter, whose point lies within the lateral bound of C. So |t - t_ref|
+//    <= (4.5 sqrt(u) X + 2.5 sqrt(u) r' + 12u X) / |d| + 3u |t| <= (1.1e-3 X + 6.2e-4 r_max +
+//    15u X) / |d| (|t| <= X / |d| for an accepted root), and the point o + t_ref d lies in the
+//    laterally inflated box: its slab entry is <= t_ref <= t + slack, its exit >= t - slack. The
+//    slack below is 4.4e-3 (X + r_max) + 32u X, over |d| rounded down (>= 2.5x the derived one).
+// Hence a box whose inflated entry lies beyond limit + slack (limit = the best sphere's t x
+// 1.00001, or the triangle hit: a sphere wins only if strictly closer, :347, :391), or whose
+// exit lies before -slack, holds no sphere the reference accepts with a distance that could win.
+// With the RTIOW field (r = 0.2, X ~ 30) the lateral inflation is ~0.011.
+// Evidence: tests/cpp/bvh_exactness.cpp (RTIOW-like scene, replayed frames, and the adversarial
+// sets: radii 1e-3..1e3, tangent rays with the discriminant within a few ulp of 0 from 1..1e6
+// radii away, |d| from 1e-12 to 1e6); the lateral bound cut to 0.03x fails there.
 RT_SLAB_FN void sphere_cull_bounds(float olen, float extent, float r_min, float r_max, float inv_dlen,
                                    float& lateral, float& slack) {
+    if (!(inv_dlen <= 0x1p30f)) {  // |d|^2 < 2^-60 (or not finite): outside the bound's range, no culling
+        lateral = INFINITY;
+        slack = INFINITY;
+        return;
+    }
     const float u = 5.9604645e-8f;  // 2^-24
     const float X = (olen + extent) * 1.0000005f;
-    const float quad = r_min > 0.0f ? ((40.0f * u) * (X * X)) * rcp_up(r_min) : INFINITY;  // 4 x 10u X^2 / r
-    const float lin = 4.4e-3f * X;                                               // ~4 x sqrt(20u) X
+    const float quad = r_min > 0.0f ? ((40.0f * u) * (X * X)) * rcp_up(r_min) : INFINITY;  // >= 3 x 13.25u X^2 / r_min
+    const float lin = 4.4e-3f * X;                                               // >= 2.5 x 7 sqrt(u) X
     lateral = fminf(quad, lin) + (16.0f * u) * X + (16.0f * u) * r_max + 1.0e-6f;
     slack = (4.4e-3f * (X + r_max) + (32.0f * u) * X) * (inv_dlen * 1.01f) + 1.0e-30f;
 }

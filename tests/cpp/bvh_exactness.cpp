@@ -214,10 +214,83 @@ static int replay(const char* rays_path, const char* sph_path) {
     return (bad || g_slab_diff) ? 1 : 0;
 }
 
+// Adversarial sets for the derived bound (rt_bvh_slab.h): BVH spheres with
+// radii log-uniform over 1e-3..1e3 (centres 1e3..2e3 from the origin, so every sphere is in the
+// BVH), and rays tangent to a random sphere in exact arithmetic -- the reference's discriminant
+// within a few ulp of 0 -- from origins 1..1e6 radii away along the tangent, nudged across the
+// tangent by a few ulp; plus rays aimed at the centre from far away, and directions scaled to
+// |d| from 1e-12 (below the bound's admitted range: no culling) to 1e6.
+static int adversarial(long n_rays, unsigned seed) {
+    std::mt19937 rng(seed);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    std::vector<rt_scene_sphere> s;
+    for (int i = 0; i < 600; i++) {
+        double th = U(rng) * 6.283185307179586, ph = std::acos(2.0 * U(rng) - 1.0), R = 1000.0 + 1000.0 * U(rng);
+        rt_scene_sphere sp{};
+        sp.position[0] = (float)(R * std::sin(ph) * std::cos(th));
+        sp.position[1] = (float)(R * std::cos(ph));
+        sp.position[2] = (float)(R * std::sin(ph) * std::sin(th));
+        sp.radius = (float)std::pow(10.0, -3.0 + 6.0 * U(rng));
+        sp.material_index = (uint32_t)i;
+        s.push_back(sp);
+    }
+    SphereSlots sl;
+    build_sphere_slots(s.data(), (uint32_t)s.size(), true, &sl);
+    if (sl.nodes.empty() || sl.n_always != 0) { printf("adversarial scene not fully in the BVH\n"); return 2; }
+    long hits = 0, near_zero = 0;
+    for (long r = 0; r < n_rays; r++) {
+        const rt_scene_sphere& sp = s[rng() % s.size()];
+        const double C[3] = {sp.position[0], sp.position[1], sp.position[2]}, rad = sp.radius;
+        double n[3] = {U(rng) - 0.5, U(rng) - 0.5, U(rng) - 0.5};
+        double ln = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        for (double& v : n) v /= ln;
+        double t[3] = {U(rng) - 0.5, U(rng) - 0.5, U(rng) - 0.5};  // a tangent direction: t - (t.n) n
+        const double tn = t[0] * n[0] + t[1] * n[1] + t[2] * n[2];
+        for (int k = 0; k < 3; k++) t[k] -= tn * n[k];
+        const double lt = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        for (double& v : t) v /= lt;
+        const double L = rad * std::pow(10.0, 6.0 * U(rng));  // |o - tangent point| / r in 1..1e6
+        V o, d;
+        const int kind = (int)(r % 4);
+        if (kind <= 2) {  // tangent in exact arithmetic, nudged by a few ulp across it
+            const double nudge = (double)((int)(rng() % 9) - 4) * std::ldexp(1.0, std::ilogb((float)rad) - 23);
+            o = {(float)(C[0] + (rad + nudge) * n[0] - L * t[0]), (float)(C[1] + (rad + nudge) * n[1] - L * t[1]),
+                 (float)(C[2] + (rad + nudge) * n[2] - L * t[2])};
+            d = {(float)t[0], (float)t[1], (float)t[2]};
+            if (kind == 2) d = {(float)(t[0] + 1e-7 * n[0]), (float)(t[1] + 1e-7 * n[1]), (float)(t[2] + 1e-7 * n[2])};
+        } else {  // aimed at the centre from 1..1e6 radii away (the near root far from the origin)
+            o = {(float)(C[0] + L * n[0]), (float)(C[1] + L * n[1]), (float)(C[2] + L * n[2])};
+            d = {(float)-n[0], (float)-n[1], (float)-n[2]};
+        }
+        const float scale = (float)std::pow(10.0, -12.0 + 18.0 * U(rng) * U(rng) + (r % 16 == 0 ? 0.0 : 11.0));
+        d = {d.x * scale, d.y * scale, d.z * scale};
+        {
+            // how often the reference's discriminant sits near 0 for the chosen sphere (within 2^-16 of b^2)
+            V oc = sub(o, V{sp.position[0], sp.position[1], sp.position[2]});
+            float b = 2.0f * dot(d, oc), c = dot(oc, oc) - sp.radius * sp.radius;
+            float disc = b * b - 4.0f * dot(d, d) * c;
+            near_zero += std::fabs(disc) <= std::ldexp(std::fabs(b * b), -16);
+        }
+        Res a = brute(s, o, d), b = kernel_like(sl, o, d);
+        uint32_t ta, tb;
+        memcpy(&ta, &a.t, 4);
+        memcpy(&tb, &b.t, 4);
+        if (a.idx != b.idx || ta != tb) {
+            printf("MISMATCH adversarial ray %ld kind %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) brute=(%d %.9g) bvh=(%d %.9g)\n",
+                   r, kind, o.x, o.y, o.z, d.x, d.y, d.z, a.idx, a.t, b.idx, b.t);
+            return 1;
+        }
+        hits += a.idx >= 0;
+    }
+    printf("ok adversarial %ld %ld %.1f near_zero_disc %ld\n", n_rays, hits, (double)g_tests / n_rays, near_zero);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc > 3 && strcmp(argv[1], "--replay") == 0) return replay(argv[2], argv[3]);
     long n_rays = argc > 1 ? atol(argv[1]) : 200000;
     unsigned seed = argc > 2 ? (unsigned)atoi(argv[2]) : 1;
+    if (argc > 3 && strcmp(argv[3], "adv") == 0) return adversarial(n_rays, seed);
     std::mt19937 rng(seed);
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
     // RTIOW-like field + ground + a few big spheres + duplicates (ties) + touching spheres
