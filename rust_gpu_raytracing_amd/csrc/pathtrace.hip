@@ -78,6 +78,9 @@ struct SceneView {
     const float4* cverts;
     const uint16_t* cidx;
     bool lazy_sub;
+    // the 4-wide quantized accelerator (tri_q4.h; null: the binary walk), decoded on the grid above;
+    // its per-lane stack is `stk` (entry e at stk[e * stk_stride])
+    const uint4* tri_q4;
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -199,12 +202,8 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
 #ifndef RT_LEAFCERT_DEFER
 #define RT_LEAFCERT_DEFER 1
 #endif
-// The LDS vertex table (mode 2, compact_tri): build switch, off by default --
-// compiled in, its code cost the LDS-resident instances more registers than its smaller
-// triangle reads saved (C3 0.304 -> 0.317 ms per frame with it off at run time, 0.349 on).
-#ifndef RT_LDS_COMPACT
-#define RT_LDS_COMPACT 0
-#endif
+// RT_LDS_COMPACT (the LDS vertex table's build switch) is defined in rt_kernel_args.h, where the
+// host sees it too.
 // A triangle from the LDS vertex table (mode 2): edge_ab, edge_ac and calc_normal recomputed
 // with SceneTriangle::new's f32 operations (src/buffers.rs:66-95; tri_wide.h
 // wide_tri_from_vertices) -- the record's own bits, checked for every triangle when the table
@@ -355,7 +354,8 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
     if (kTris && phase == 0) {  // the accelerator layout ordered for this ray's direction octant (global walks)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
                              ((__float_as_uint(ts.inv.z) >> 31) << 2);
-        ts.node = oct * ka.tri_octant_stride;
+        ts.node = sv.tri_q4 ? 0u : oct * ka.tri_octant_stride;  // the 4-wide walk starts at its root
+        ts.sp = 0u;
     }
     if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
@@ -544,6 +544,152 @@ __device__ __forceinline__ void tri_leaf_wide(const SceneView& sv, const KernelA
     }
 }
 
+// ---- the 4-wide quantized walk (tri_q4.h) --------------------------------
+// One 64-B node per step: its four child boxes decoded on the grid and tested with the ray's
+// culling slab (rt_bvh_slab.h, the binary walk's margin), the hit children ordered by entry
+// distance (a 5-exchange sorting network), the nearest taken next and the others pushed on the
+// lane's LDS stack, farthest first. A hit leaf is deferred to the wave's leaf batch
+// (ts.pending) with its certified gap beyond the best hit measured now, from the child's box
+// (node_step's test: the leaf batch runs tri_leafcert_skips_gap); a leaf waiting on the stack
+// carries that gap in 11 bits (tri_q4.h q4_gap_code, a lower bound). A lane whose leaf is still
+// deferred when it pops another leaf waits until the batch. A push beyond kQ4StackEntries
+// restarts the lane on the binary walk (ts.sp = kQ4Binary), which is complete and merges into
+// the same lexicographic minimum.
+constexpr uint32_t kQ4Binary = 0x80000000u;  // TraceState::sp: this walk fell back to the binary tree
+
+// The lane's index in its wave, computed where it is used: an opaque value, so that the compiler
+// does not hoist it (and what is derived from it) out of the traversal loop into a register
+// held across every node step.
+__device__ __forceinline__ uint32_t lane_id_here() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// The dynamic LDS of the kernel (the same block as the kernels' own extern declaration).
+extern __shared__ __attribute__((aligned(16))) unsigned char rt_dyn_lds[];
+
+// Entry `e` of this lane's 4-wide walk stack (lane-interleaved: entry e of thread t at
+// [e * threads + t]), addressed from the thread index where it is used rather than a pointer held
+// in a register across the walk (the walk's instances are at their VGPR limit).
+__device__ __forceinline__ uint32_t* q4_stack_entry(const KernelArgs& ka, uint32_t e) {
+    const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u) + lane_id_here();
+    return reinterpret_cast<uint32_t*>(rt_dyn_lds + ka.lds_q4stack_offset) + e * blockDim.x + t;
+}
+
+__device__ __forceinline__ void q4_child(const SceneView& sv, const KernelArgs& ka, f3 d, const TraceState& ts,
+                                         uint32_t w0, uint32_t w1, uint32_t w2, uint32_t ref, float& key,
+                                         uint32_t& ent) {
+    const float lx = fmaf((float)(w0 & 0xffffu), sv.qsx, sv.qox), ly = fmaf((float)(w0 >> 16), sv.qsy, sv.qoy);
+    const float lz = fmaf((float)(w1 & 0xffffu), sv.qsz, sv.qoz), hx = fmaf((float)(w1 >> 16), sv.qsx, sv.qox);
+    const float hy = fmaf((float)(w2 & 0xffffu), sv.qsy, sv.qoy), hz = fmaf((float)(w2 >> 16), sv.qsz, sv.qoz);
+    float t1x, t1y, t1z, far_t;
+    slab_hit_axes(ts.slab, lx, ly, lz, hx, hy, hz, t1x, t1y, t1z, far_t);
+    const float near_t = fmaxf(fmaxf(t1x, t1y), t1z);  // slab_hit's near_t
+    const bool hit = ref != kQ4Empty && near_t <= far_t && far_t >= 0.0f;
+    key = hit ? near_t : __builtin_inff();
+    ent = ref;
+    if (hit && (ref & kQ4Leaf) && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max) {
+        // the leaf box's gap beyond the best hit (node_step's, pathtrace.hip RT_LEAFCERT_DEFER)
+        const float tbs = ts.tri.t * (1.0f + 0x1p-20f);
+        const float gx = (t1x - tbs) * fabsf(d.x), gy = (t1y - tbs) * fabsf(d.y), gz = (t1z - tbs) * fabsf(d.z);
+        ent = ref | (q4_gap_code(fmaxf(fmaxf(gx, gy), gz) * (1.0f - 0x1p-20f)) << 20);
+    }
+}
+
+// A leaf entry into the deferred slot (the caller checked it is free).
+__device__ __forceinline__ void q4_defer_leaf(TraceState& ts, uint32_t e) {
+#if RT_LEAFCERT_DEFER
+    const uint32_t code = (e >> 20) & 0x7ffu;
+    ts.pending = (e & 0xfffffu) | (code != 0u ? (1u << 24) : 0u);  // bit 24: test the certificate in the batch
+    ts.cert_gap = q4_gap_decode(code);
+#else
+    ts.pending = e & 0xfffffu;  // (bits 24-30 would be a skip mask in this build: no certificate test)
+#endif
+}
+
+__device__ __forceinline__ void q4_fallback(const KernelArgs& ka, TraceState& ts) {
+    // the binary walk from the start of the ray's octant layout (phase_setup's)
+    const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
+                         ((__float_as_uint(ts.inv.z) >> 31) << 2);
+    ts.node = oct * ka.tri_octant_stride;
+    ts.sp = kQ4Binary;
+}
+
+__device__ __forceinline__ void q4_node_step(const SceneView& sv, const KernelArgs& ka, f3 d, TraceState& ts) {
+    uint32_t n = ts.node;
+    if (n == kQ4None) {
+        if (ts.sp == 0u) return;  // walk over (phase_end)
+        const uint32_t e = *q4_stack_entry(ka, ts.sp - 1u);
+        if (e & kQ4Leaf) {
+            if (ts.pending != kNoLeaf) return;  // blocked until the batch tests the deferred leaf
+            q4_defer_leaf(ts, e);
+            ts.sp -= 1u;
+            return;
+        }
+        n = e;
+        ts.sp -= 1u;
+    }
+    const uint4* nd = sv.tri_q4 + 4u * n;
+    const uint4 b0 = nd[0], b1 = nd[1], b2 = nd[2], rf = nd[3];
+    float k0, k1, k2, k3;
+    uint32_t e0, e1, e2, e3;
+    q4_child(sv, ka, d, ts, b0.x, b0.y, b0.z, rf.x, k0, e0);
+    q4_child(sv, ka, d, ts, b0.w, b1.x, b1.y, rf.y, k1, e1);
+    q4_child(sv, ka, d, ts, b1.z, b1.w, b2.x, rf.z, k2, e2);
+    q4_child(sv, ka, d, ts, b2.y, b2.z, b2.w, rf.w, k3, e3);
+    // nearest first: misses (inf) sort last
+#define RT_Q4_CX(ka_, ea_, kb_, eb_)               \
+    {                                               \
+        const bool sw = kb_ < ka_;                  \
+        const float tk = sw ? kb_ : ka_;            \
+        kb_ = sw ? ka_ : kb_;                       \
+        ka_ = tk;                                   \
+        const uint32_t te = sw ? eb_ : ea_;         \
+        eb_ = sw ? ea_ : eb_;                       \
+        ea_ = te;                                   \
+    }
+    RT_Q4_CX(k0, e0, k1, e1)
+    RT_Q4_CX(k2, e2, k3, e3)
+    RT_Q4_CX(k0, e0, k2, e2)
+    RT_Q4_CX(k1, e1, k3, e3)
+    RT_Q4_CX(k1, e1, k2, e2)
+#undef RT_Q4_CX
+    ts.node = kQ4None;
+    if (k0 == __builtin_inff()) return;  // no child hit
+    const uint32_t n_push = (k1 != __builtin_inff() ? 1u : 0u) + (k2 != __builtin_inff() ? 1u : 0u) +
+                            (k3 != __builtin_inff() ? 1u : 0u);
+    // the nearest child: a leaf that cannot be deferred now waits on the stack too
+    const bool e0_waits = (e0 & kQ4Leaf) && ts.pending != kNoLeaf;
+    if (ts.sp + n_push + (e0_waits ? 1u : 0u) > kQ4StackEntries) {
+        q4_fallback(ka, ts);
+        return;
+    }
+    uint32_t* st = q4_stack_entry(ka, ts.sp);
+    const uint32_t stride = blockDim.x;
+    if (n_push == 3u) {
+        st[0] = e3;
+        st += stride;
+    }
+    if (n_push >= 2u) {
+        st[0] = e2;
+        st += stride;
+    }
+    if (n_push >= 1u) {
+        st[0] = e1;
+        st += stride;
+    }
+    ts.sp += n_push;
+    if (!(e0 & kQ4Leaf)) {
+        ts.node = e0;
+    } else if (e0_waits) {
+        st[0] = e0;
+        ts.sp += 1u;
+    } else {
+        q4_defer_leaf(ts, e0);
+    }
+}
+
 // One node of the 4-wide walk (tri_wide.h): the four child boxes, inflated by the
 // ray's margin, tested together (rt_bvh_slab.h). Hit leaves are deferred to the
 // wave's leaf batches (ts.pending: the node's leaf records still to test); the
@@ -612,7 +758,9 @@ template <bool kTris, bool kWide = false>
 __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     if (ts.pending != kNoLeaf) return;
     if (kTris && ts.phase == 0) {
-        if (kWide ? (ts.node != kWideNone || ts.sp != 0u) : (ts.node < ka.tri_nodes)) return;
+        if (kWide ? (ts.node != kWideNone || ts.sp != 0u)
+                  : (sv.tri_q4 && ts.sp != kQ4Binary) ? (ts.node != kQ4None || ts.sp != 0u) : (ts.node < ka.tri_nodes))
+            return;
 #ifdef RT_DIAG_TAIL
         if (ts.nan_hit) atomicAdd(ka.diag + 6, 1ull);
 #endif
@@ -675,6 +823,12 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     if (kWide && tri) {
         wide_node_step(sv, ts);
         return;
+    }
+    if constexpr (kTris && !kWide) {
+        if (tri && sv.tri_q4 && ts.sp != kQ4Binary) {
+            q4_node_step(sv, ka, d, ts);
+            return;
+        }
     }
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
@@ -818,15 +972,6 @@ __device__ __forceinline__ void coop_min_step(float& cd, uint32_t& cs, uint32_t&
     cd = take ? od : cd;
     cs = take ? os : cs;
     ct = take ? ot : ct;
-}
-
-// The lane's index in its wave, computed where it is used: an opaque value, so that the compiler
-// does not hoist it (and what is derived from it) out of the traversal loop into a register
-// held across every node step.
-__device__ __forceinline__ uint32_t lane_id_here() {
-    uint32_t l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
 }
 
 // `active`: this lane traverses and holds a deferred leaf (a triangle leaf, or a sphere group in
@@ -1472,11 +1617,24 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                  ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
                  ka.tri_wide,     nullptr,        kThreads,       ka.sub_objects};
     if constexpr (kWide) sv.stk = reinterpret_cast<uint32_t*>(lds + ka.lds_stack_offset) + tid;
+    sv.tri_q4 = nullptr;
     if constexpr (kTris && !kWide && kMode <= 1) {
         if (ka.tri_qnodes) {
             const float4 g0 = ka.tri_qgrid[0], g1 = ka.tri_qgrid[1];
             if (g0.w != 0.0f) {
                 sv.tri_q = ka.tri_qnodes;
+                sv.qox = g0.x;
+                sv.qoy = g0.y;
+                sv.qoz = g0.z;
+                sv.qsx = g1.x;
+                sv.qsy = g1.y;
+                sv.qsz = g1.z;
+            }
+        }
+        if (ka.tri_q4) {  // the 4-wide walk, on the same grid (both from the binary root, tri_qgrid)
+            const float4 g0 = ka.tri_q4grid[0], g1 = ka.tri_q4grid[1];
+            if (g0.w != 0.0f) {
+                sv.tri_q4 = ka.tri_q4;
                 sv.qox = g0.x;
                 sv.qoy = g0.y;
                 sv.qoz = g0.z;
@@ -1541,6 +1699,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             for (uint32_t i = tid; i < ka.sub_object_count; i += kThreads) l_sub[i] = ka.sub_objects[i];
             sv.sub = l_sub;
         }
+#if RT_LDS_COMPACT
         if (ka.lds_cidx_offset) {  // the vertex-indexed triangles, when they fit
             float4* l_cv = reinterpret_cast<float4*>(lds + ka.lds_cvert_offset);
             uint32_t* l_ci = reinterpret_cast<uint32_t*>(lds + ka.lds_cidx_offset);
@@ -1551,6 +1710,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             sv.cidx = reinterpret_cast<const uint16_t*>(l_ci);
             sv.lazy_sub = ka.lds_sub_offset == 0;  // records in global memory: test them lazily
         }
+#endif
     }
     for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];
     float* l_cam = l_srgb + 256;  // camera block for device-side primary rays
@@ -2170,6 +2330,106 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
     }
 }
 
+// ---- the 4-wide accelerator as a packet (rt_primary_kernel, tri_q4.h) --------------------
+// The wave walks one node at a time (wave-uniform address: one load serves the packet); each
+// lane tests the four child boxes with its own culling slab, and a child is entered when any
+// lane's ray enters it, by exactly those lanes. The node's hit leaves are tested at once by the
+// lanes that reached them (certificate first, as the binary packet walk does: tri_leaf_skips on
+// the child's box), in the order of the first hitting lane's entry distances; of the internal
+// children the nearest is walked next and the others wait on the wave's LDS stack with the mask
+// of their lanes (kQ4PacketStack entries of {node, mask}: enough for 3 per level of a tree of
+// depth <= 21, which the host checks). Every lane still gets the lexicographic minimum over a
+// superset of its own candidates -- its own result.
+__device__ __forceinline__ void q4_packet_walk(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
+                                               bool valid, uint32_t* wst) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    uint32_t node = 0u, sp = 0u;  // wave-uniform
+    bool act = valid;
+    while (true) {
+        if (node == kQ4None) {
+            if (sp == 0u) break;
+            sp -= 1u;
+            wave_lds_sync();
+            node = __builtin_amdgcn_readfirstlane(wst[3u * sp]);
+            const uint64_t m = (uint64_t)wst[3u * sp + 1u] | ((uint64_t)wst[3u * sp + 2u] << 32);
+            act = ((m >> lane) & 1ull) != 0ull;
+        }
+        const uint4* nd = sv.tri_q4 + 4u * node;
+        const uint4 b0 = nd[0], b1 = nd[1], b2 = nd[2], rf = nd[3];
+        const uint32_t w[12] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w};
+        const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
+        bool hit[4];
+        uint64_t mask[4];
+        float key[4];
+        uint32_t slot[4] = {0u, 1u, 2u, 3u};
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; k++) {
+            const uint32_t w0 = w[3u * k], w1 = w[3u * k + 1u], w2 = w[3u * k + 2u];
+            const float4 lo = make_float4(fmaf((float)(w0 & 0xffffu), sv.qsx, sv.qox),
+                                          fmaf((float)(w0 >> 16), sv.qsy, sv.qoy),
+                                          fmaf((float)(w1 & 0xffffu), sv.qsz, sv.qoz), 0.0f);
+            const float4 hi = make_float4(fmaf((float)(w1 >> 16), sv.qsx, sv.qox),
+                                          fmaf((float)(w2 & 0xffffu), sv.qsy, sv.qoy),
+                                          fmaf((float)(w2 >> 16), sv.qsz, sv.qoz), 0.0f);
+            float near_t, far_t;
+            slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+            bool h = act && ref[k] != kQ4Empty && near_t <= far_t && far_t >= 0.0f;
+            if (h && (ref[k] & kQ4Leaf) && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max &&
+                tri_leaf_skips(ka, ref[k] & 0xfffffu, ts.slab, o, d, ts.tri.t, lo, hi) == kLeafCertAll)
+                h = false;  // certified: no triangle of the leaf can win
+            hit[k] = h;
+            mask[k] = __ballot(h);
+            float kk = __builtin_inff();
+            if (mask[k])
+                kk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(near_t), (uint32_t)__builtin_ctzll(mask[k])));
+            key[k] = kk;
+        }
+        // the order of the first hitting lanes' entry distances (wave-uniform)
+#define RT_Q4_SX(a, b)                                           \
+        if (key[b] < key[a]) {                                    \
+            const float tk = key[a];                              \
+            key[a] = key[b];                                      \
+            key[b] = tk;                                          \
+            const uint32_t ts_ = slot[a];                         \
+            slot[a] = slot[b];                                    \
+            slot[b] = ts_;                                        \
+        }
+        RT_Q4_SX(0, 1) RT_Q4_SX(2, 3) RT_Q4_SX(0, 2) RT_Q4_SX(1, 3) RT_Q4_SX(1, 2)
+#undef RT_Q4_SX
+        // the hit leaves, nearest first
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; j++) {
+            const uint32_t k = slot[j];
+            if (mask[k] == 0ull || !(ref[k] & kQ4Leaf)) continue;
+            if (hit[k]) {
+                tri_leaf<true>(sv, ka, o, d, ts, ref[k] & 0xfffffu);
+                ts.limit = tri_limit(sv, ka, o, ts);
+            }
+        }
+        // the nearest internal child next, the others on the stack (farthest first)
+        node = kQ4None;
+        uint32_t first = 4u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; j++) {
+            const uint32_t k = slot[3u - j];
+            if (mask[k] == 0ull || (ref[k] & kQ4Leaf)) continue;
+            if (first != 4u) {  // the previously found (farther) one waits
+                if (lane == 0u) {
+                    wst[3u * sp] = ref[first];
+                    wst[3u * sp + 1u] = (uint32_t)mask[first];
+                    wst[3u * sp + 2u] = (uint32_t)(mask[first] >> 32);
+                }
+                sp += 1u;
+            }
+            first = k;
+        }
+        if (first != 4u) {
+            node = ref[first];
+            act = hit[first];
+        }
+    }
+}
+
 // ---- coherent primary rays: a packet pre-pass -----------------------------------
 //
 // The first segment of every path starts at the camera, and the 64 primary rays
@@ -2229,6 +2489,23 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
             sv.sub = l_sub;
         }
     }
+    // the 4-wide packet walk (global-memory accelerators): its grid, and this wave's stack
+    uint32_t* q4_wstack = nullptr;
+    if constexpr (kTris && kMode <= 1) {
+        if (ka.tri_q4 && ka.lds_q4packet_offset) {
+            const float4 g0 = ka.tri_q4grid[0], g1 = ka.tri_q4grid[1];
+            if (g0.w != 0.0f) {
+                sv.tri_q4 = ka.tri_q4;
+                sv.qox = g0.x;
+                sv.qoy = g0.y;
+                sv.qoz = g0.z;
+                sv.qsx = g1.x;
+                sv.qsy = g1.y;
+                sv.qsz = g1.z;
+                q4_wstack = reinterpret_cast<uint32_t*>(lds + ka.lds_q4packet_offset) + (tid >> 6) * (3u * kQ4PacketStack);
+            }
+        }
+    }
     if (tid < 16u) {
         l_cam[tid] = ka.inv_proj[tid];
         l_cam[16u + tid] = ka.inv_view[tid];
@@ -2262,6 +2539,13 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
         TraceState ts;
         trace_begin<kTris>(sv, ka, o, d, ts);  // brute-force spheres, slab constants, phase
         if constexpr (kTris) {
+            if (kMode <= 1 && ts.phase == 0 && sv.tri_q4) {
+                q4_packet_walk(sv, ka, o, d, ts, valid, q4_wstack);
+                if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
+                ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
+                ts.node = 0;
+                if (ts.phase == 1) phase_setup<kTris>(sv, ka, o, ts.a2 * 0.5f, 1, ts);
+            }
             if (ts.phase == 0) {
                 // the triangle accelerator as a packet: wave-uniform node (the layout of the
                 // first lane's direction octant), per-lane culling and pruning

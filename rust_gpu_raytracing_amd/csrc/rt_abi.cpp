@@ -50,6 +50,8 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            hipStream_t stream);
 hipError_t rt_launch_tri_leafcert(const SubObjectPrim* prims, uint32_t n_prims, const RtSubObject* subs,
                                   const RtTriangleHot* tris, uint32_t n_tri, TriLeafCert* out, hipStream_t stream);
+hipError_t rt_launch_tri_q4_fill(const SphereBvhNode* bin, uint32_t n_bin, const uint32_t* src, uint32_t n_q4,
+                                 TriQ4Node* q4, float4* grid, hipStream_t stream);
 hipError_t rt_launch_tri_leaftris(const SubObjectPrim* prims, uint32_t n_prims, const RtTriangleHot* tris,
                                   uint32_t n_tri, uint4* out, hipStream_t stream);
 hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
@@ -288,6 +290,16 @@ struct rt_ctx {
     // the leaves' triangle blocks, rebuilt with the certificates; RT_COOP_LEAVES=0: per-lane leaf
     // tests (A/B switch)
     bool use_coop_leaves = true;
+    // the 4-wide quantized accelerator (tri_q4.h) over the binary one, for walks from global
+    // memory: its links and child -> binary node map are built on the host at upload, its boxes on
+    // the device (after every upload or refit); RT_TRI_Q4=0: the binary walk (A/B switch)
+    bool use_q4 = false;
+    bool q4_built = false, q4_dirty = true;
+    uint32_t q4_nodes = 0, q4_depth = 0;
+    TriQ4Node* d_tri_q4 = nullptr;
+    uint32_t* d_tri_q4src = nullptr;
+    float4* d_tri_q4grid = nullptr;
+    size_t tri_q4_cap = 0, tri_q4src_cap = 0, tri_q4grid_cap = 0;
     uint4* d_tri_ltris = nullptr;
     size_t tri_ltris_cap = 0;
     bool ltris_dirty = true;
@@ -589,6 +601,7 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         (rc = upload_raw(ctx, ctx->d_tri_prims, acc.prims.data(), pb)))
         return rc;
     ctx->qnodes_dirty = true;
+    ctx->q4_dirty = true;
     ctx->cones_dirty = true;
     ctx->ltris_dirty = true;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
@@ -608,6 +621,25 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
             (rc = upload_raw(ctx, ctx->d_tri_skip8, skip.data(), b8)))
             return rc;
         ctx->tri_octants_built = true;
+    }
+    ctx->q4_built = false;
+    if (ctx->use_q4 && acc.nodes.size() > 1) {
+        std::vector<TriQ4Node> q4;
+        std::vector<uint32_t> q4src;
+        uint32_t q4depth = 0;
+        if (build_tri_q4(acc.nodes, &q4, &q4src, &q4depth)) {
+            // the links now; the boxes on the device (rt_tri_q4_fill_kernel, at the next launch)
+            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_q4), &ctx->tri_q4_cap, q4.size() * sizeof(TriQ4Node))) ||
+                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_q4src), &ctx->tri_q4src_cap, q4src.size() * 4)) ||
+                (rc = upload_raw(ctx, ctx->d_tri_q4, q4.data(), q4.size() * sizeof(TriQ4Node))) ||
+                (rc = upload_raw(ctx, ctx->d_tri_q4src, q4src.data(), q4src.size() * 4)))
+                return rc;
+            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_q4grid), &ctx->tri_q4grid_cap, 2 * sizeof(float4))))
+                return rc;
+            ctx->q4_nodes = (uint32_t)q4.size();
+            ctx->q4_depth = q4depth;
+            ctx->q4_built = true;
+        }
     }
     // depth levels for the device refit (preorder: a node precedes its children)
     std::vector<uint32_t> depth(acc.nodes.size(), 0);
@@ -688,30 +720,39 @@ int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     ctx->ltris_dirty = true;
     // the vertex table describes the whole buffer only when this upload rewrites all of it
     ctx->compact_valid = false;
-    if (n == ctx->cap_tri) {
+    // the table is an option (a -DRT_LDS_COMPACT=1 build with RT_TRI_LDS_COMPACT=1): built only
+    // then, and an allocation failure here only leaves it invalid (the records are read)
+    if (kLdsCompactBuilt && ctx->use_lds_compact && n == ctx->cap_tri) {
         std::vector<float4> verts;
         std::vector<uint16_t> idx;
         if (build_compact_triangles(t, n, &verts, &idx)) {
             const size_t bv = verts.size() * sizeof(float4), bi = idx.size() * sizeof(uint16_t);
-            if (ctx->cverts_cap < bv || ctx->cidx_cap < bi) {
+            bool room = ctx->cverts_cap >= bv && ctx->cidx_cap >= bi;
+            if (!room) {
                 RT_HIP(ctx, join_aux(ctx));
                 RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-                if (ctx->d_cverts) RT_HIP(ctx, hipFree(ctx->d_cverts));
-                if (ctx->d_cidx) RT_HIP(ctx, hipFree(ctx->d_cidx));
+                if (ctx->d_cverts) (void)hipFree(ctx->d_cverts);
+                if (ctx->d_cidx) (void)hipFree(ctx->d_cidx);
                 ctx->d_cverts = nullptr;
                 ctx->d_cidx = nullptr;
                 ctx->cverts_cap = ctx->cidx_cap = 0;
-                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_cverts), bv));
-                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_cidx), bi));
-                ctx->cverts_cap = bv;
-                ctx->cidx_cap = bi;
+                if (hipMalloc(reinterpret_cast<void**>(&ctx->d_cverts), bv) == hipSuccess &&
+                    hipMalloc(reinterpret_cast<void**>(&ctx->d_cidx), bi) == hipSuccess) {
+                    ctx->cverts_cap = bv;
+                    ctx->cidx_cap = bi;
+                    room = true;
+                } else {
+                    (void)hipGetLastError();  // the optional table stays off; not a context error
+                }
             }
-            int rc;
-            if ((rc = upload_raw(ctx, ctx->d_cverts, verts.data(), bv)) ||
-                (rc = upload_raw(ctx, ctx->d_cidx, idx.data(), bi)))
-                return rc;
-            ctx->cvert_count = (uint32_t)verts.size();
-            ctx->compact_valid = true;
+            if (room) {
+                int rc;
+                if ((rc = upload_raw(ctx, ctx->d_cverts, verts.data(), bv)) ||
+                    (rc = upload_raw(ctx, ctx->d_cidx, idx.data(), bi)))
+                    return rc;
+                ctx->cvert_count = (uint32_t)verts.size();
+                ctx->compact_valid = true;
+            }
         }
     }
     void* p;
@@ -932,10 +973,12 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->use_qnodes = env[0] != '0';
         env = std::getenv("RT_TRI_LEAFCERT_LDS");
         if (env) ctx->use_leafcert_lds = env[0] == '1';
+        env = std::getenv("RT_TRI_Q4");
+        if (env) ctx->use_q4 = env[0] != '0';
         env = std::getenv("RT_COOP_LEAVES");
         if (env) ctx->use_coop_leaves = env[0] != '0';
         env = std::getenv("RT_TRI_LDS_COMPACT");
-        if (env) ctx->use_lds_compact = env[0] == '1';
+        if (env) ctx->use_lds_compact = kLdsCompactBuilt && env[0] == '1';
         env = std::getenv("RT_STAGE_SUBS");
         if (env) ctx->stage_subs = env[0] != '0';
         env = std::getenv("RT_FRAME_BATCH");
@@ -1016,7 +1059,8 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
                     ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
-                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx, ctx->d_tri_ltris};
+                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx, ctx->d_tri_ltris, ctx->d_tri_q4, ctx->d_tri_q4src,
+                    ctx->d_tri_q4grid};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1491,6 +1535,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qnodes), (size_t)n_out * sizeof(uint4)));
             ctx->qnodes_cap = n_out;
             ctx->qnodes_dirty = true;
+            ctx->q4_dirty = true;
         }
         if (!ctx->d_tri_qgrid) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qgrid), 2 * sizeof(float4)));
         if (ctx->qnodes_dirty || ctx->derived_octants != octants || ctx->derived_qnodes != qnodes) {
@@ -1565,6 +1610,21 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         ka.tri_leaftris = ctx->d_tri_ltris;
     }
+    // the 4-wide quantized walk (needs the cooperative leaf batches' LDS layout beside it)
+    ka.tri_q4 = nullptr;
+    ka.tri_q4grid = nullptr;
+    const bool q4 = coop && ctx->q4_built && ctx->use_q4 && ctx->tri_prune_mode != 2;  // (mode 2: the binary walk's slack)
+    if (q4) {
+        if (ctx->q4_dirty) {
+            RT_HIP(ctx, rt_launch_tri_q4_fill(reinterpret_cast<const SphereBvhNode*>(ctx->d_tri_bvh), ctx->tri_nodes,
+                                              ctx->d_tri_q4src, ctx->q4_nodes, ctx->d_tri_q4, ctx->d_tri_q4grid,
+                                              ctx->stream));
+            ctx->q4_dirty = false;
+            ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
+        }
+        ka.tri_q4 = reinterpret_cast<const uint4*>(ctx->d_tri_q4);
+        ka.tri_q4grid = ctx->d_tri_q4grid;
+    }
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
@@ -1578,7 +1638,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     // per-thread LDS after the scene image: the wide walk's stack, or the cooperative leaf
     // batch's per-wave scratch
-    const size_t lane_pt = wide ? stack_pt : coop ? (size_t)kLeafBatchWaveBytes / 64u : 0u;
+    const size_t lane_pt =
+        wide ? stack_pt : coop ? (size_t)kLeafBatchWaveBytes / 64u + (q4 ? 4u * kQ4StackEntries : 0u) : 0u;
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode ||
@@ -1599,6 +1660,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // the stack after the scene image and its tail
     ka.lds_stack_offset = (uint32_t)al16(lds_bytes);
     ka.lds_leafbatch_offset = ka.lds_stack_offset;
+    // the 4-wide walk's stacks after the leaf batch scratch: entry e of thread t at [e * threads + t]
+    ka.lds_q4stack_offset = ka.lds_stack_offset + (uint32_t)(ctx->occ_threads / 64u) * kLeafBatchWaveBytes;
     if (wide || coop) lds_bytes = ka.lds_stack_offset + (size_t)ctx->occ_threads * lane_pt;
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
@@ -1698,9 +1761,17 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         pka.primary = ctx->d_primary[pi];
         pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile)
         pka.primary_tile_major = ctx->primary_tile_major ? 1u : 0u;
-        const size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
+        size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
+        // the 4-wide packet walk's per-wave stacks after the image (3 entries per level at most)
+        pka.lds_q4packet_offset = 0;
+        if (q4 && mode <= 1 && 3u * ctx->q4_depth <= kQ4PacketStack) {
+            pka.lds_q4packet_offset = (uint32_t)al16(image);
+            const uint32_t pthreads = ctx->primary_threads ? ctx->primary_threads : 1024u;
+            image = pka.lds_q4packet_offset + (size_t)(pthreads / 64u) * kQ4PacketStack * 12u;
+        }
+        // (the 4-wide packet walk needs ~90 VGPRs: the 64-VGPR variant would spill)
         RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, mode == 2 ? 1024u : ctx->primary_threads,
-                                      mode == 2 ? 0u : ctx->primary_min_waves, S));
+                                      (mode == 2 || pka.lds_q4packet_offset) ? 0u : ctx->primary_min_waves, S));
         ka.primary = pka.primary;
     }
     hipError_t e = rt_launch_pathtrace(ka, mode, tris, wide, ctx->occ_threads, lds_bytes, blocks, S);
@@ -1911,6 +1982,7 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
         RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,
                                     ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
         ctx->qnodes_dirty = true;
+        ctx->q4_dirty = true;
     }
     ctx->cones_dirty = true;  // the triangles changed
     ctx->ltris_dirty = true;
@@ -2039,9 +2111,7 @@ int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
 
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
-    // (RT_DIAG builds keep 16 more counters in the first per-wave record words, which only
-    // RT_DIAG_TAIL builds fill: cleared too)
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters + 16) * sizeof(unsigned long long), ctx->stream));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters) * sizeof(unsigned long long), ctx->stream));
     RT_HIP(ctx, hipMemsetAsync(ctx->d_stream, 0, sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }

@@ -144,6 +144,19 @@ RT_SLAB_FN void slab_hit(const SlabRay& r, float lox, float loy, float loz, floa
     far_t = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
 }
 
+// slab_hit with the per-axis entry parameters kept (near_t = their maximum, the same operations):
+// the certified pruning's gap of a leaf box beyond the best hit reads them (tri_cone.h).
+RT_SLAB_FN void slab_hit_axes(const SlabRay& r, float lox, float loy, float loz, float hix, float hiy, float hiz,
+                              float& t1x, float& t1y, float& t1z, float& far_t) {
+    const float tx0 = fmaf(lox, r.ix, r.lx), tx1 = fmaf(hix, r.ix, r.hx);
+    const float ty0 = fmaf(loy, r.iy, r.ly), ty1 = fmaf(hiy, r.iy, r.hy);
+    const float tz0 = fmaf(loz, r.iz, r.lz), tz1 = fmaf(hiz, r.iz, r.hz);
+    t1x = fminf(tx0, tx1);
+    t1y = fminf(ty0, ty1);
+    t1z = fminf(tz0, tz1);
+    far_t = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+}
+
 // Box-ordered layouts (order_bvh_by_octant with swap_boxes): layout k stores
 // every box as (near corner, far corner) for rays of direction octant k, i.e.
 // bmin/bmax swapped on the axes where bit k is set (the ray travels towards

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "tri_cone.h"
+#include "tri_q4.h"
 #include "tri_wide.h"
 
 
@@ -103,8 +104,17 @@ constexpr uint32_t kLeafTriWords = 3 * kLeafTriSlots;       // uint4 per block (
 constexpr uint32_t kLeafBatchWaveBytes = 64 * 48;
 
 // Diagnostic counters ahead of the per-wave records in KernelArgs::diag
-// (RT_DIAG: 10 counters; RT_DIAG_TAIL: 8, then 2 words per wave from here).
-constexpr uint32_t kDiagHeaderWords = 12;
+// (RT_DIAG: words 0-25; RT_DIAG_TAIL: words 0-7, then 2 words per wave from here).
+constexpr uint32_t kDiagHeaderWords = 32;
+
+// The LDS vertex table (mode 2, pathtrace.hip compact_tri): build switch, off
+// by default -- compiled in, its code cost the LDS-resident instances more registers than its
+// smaller triangle reads saved (C3 0.304 -> 0.317 ms per frame with it off at run time, 0.349
+// on). Without it the host builds no table and leaves the LDS offsets at 0.
+#ifndef RT_LDS_COMPACT
+#define RT_LDS_COMPACT 0
+#endif
+constexpr bool kLdsCompactBuilt = RT_LDS_COMPACT != 0;
 
 struct KernelArgs {
     // framebuffer (bindings 1, 2, 6)
@@ -193,6 +203,13 @@ struct KernelArgs {
     // 128-B line; slots past the leaf's count are zero. Null: the leaf batches test per lane.
     const uint4* __restrict__ tri_leaftris;
     uint32_t lds_leafbatch_offset;  // per wave kLeafBatchWaveBytes of LDS for the cooperative leaf batch
+    // The 4-wide quantized accelerator (tri_q4.h): TriQ4Node[] as 4 uint4 each, its grid ({origin,
+    // valid}, {scale, 0}); null: the binary walk. Its walk's per-lane stacks in LDS at
+    // lds_q4stack_offset (kQ4StackEntries u32 per thread, entry e of thread t at [e * threads + t]).
+    const uint4* __restrict__ tri_q4;
+    const float4* __restrict__ tri_q4grid;
+    uint32_t lds_q4stack_offset;
+    uint32_t lds_q4packet_offset;  // rt_primary_kernel: per wave kQ4PacketStack x 3 u32 of packet stack (0: none)
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     // Frame-parallel batch (frames > 1, accumulating): the queue holds one unit per

@@ -29,6 +29,7 @@
 #include "rt_scene_math.h"
 #include "sphere_bvh.h"
 #include "tri_cone.h"
+#include "tri_q4.h"
 #include "tri_qnode.h"
 #include "tri_wide.h"
 
@@ -478,5 +479,50 @@ hipError_t rt_launch_tri_leaftris(const SubObjectPrim* prims, uint32_t n_prims, 
     const uint64_t n = (uint64_t)n_prims * kLeafTriWords;
     hipLaunchKernelGGL(rt_tri_leaftris_kernel, dim3((uint32_t)((n + 255u) / 256u)), dim3(256), 0, stream, prims,
                        n_prims, tris, n_tri, out);
+    return hipGetLastError();
+}
+
+// ---- the 4-wide quantized accelerator (tri_q4.h) --------------------------------------
+// Child boxes of every 4-wide node from the binary nodes they stand for (src[4 i + k]), on the
+// binary accelerator's quantization grid (tri_qgrid of its root): after every upload or refit,
+// so device-side edits keep the two trees the same. grid[0] = {origin.xyz, valid}, grid[1] =
+// {scale.xyz, 0}: with valid = 0 (a root box that is not finite) the walks use the binary tree.
+extern "C" __global__ void __launch_bounds__(256) rt_tri_q4_fill_kernel(const SphereBvhNode* __restrict__ bin,
+                                                                       uint32_t n_bin, const uint32_t* __restrict__ src,
+                                                                       uint32_t n_q4, TriQ4Node* __restrict__ q4,
+                                                                       float4* __restrict__ grid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    TriQGrid g{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, false};
+    if (n_bin != 0) g = tri_qgrid(bin[0]);
+    if (i == 0) {
+        grid[0] = make_float4(g.origin[0], g.origin[1], g.origin[2], g.valid ? 1.f : 0.f);
+        grid[1] = make_float4(g.scale[0], g.scale[1], g.scale[2], 0.f);
+    }
+    if (i >= 4u * n_q4 || !g.valid) return;
+    TriQ4Node& nd = q4[i >> 2];
+    const uint32_t k = i & 3u;
+    const uint32_t sk = src[i];
+    uint32_t w[3];
+    if (sk == kQ4Empty) {
+        w[0] = 0u;
+        w[1] = 0xffff0000u;
+        w[2] = 0xffffffffu;
+    } else {
+        uint32_t qq[4];
+        tri_qnode(bin[sk], g, qq);
+        w[0] = qq[0];
+        w[1] = qq[1];
+        w[2] = qq[2];
+    }
+    nd.box[k][0] = w[0];
+    nd.box[k][1] = w[1];
+    nd.box[k][2] = w[2];
+}
+
+hipError_t rt_launch_tri_q4_fill(const SphereBvhNode* bin, uint32_t n_bin, const uint32_t* src, uint32_t n_q4,
+                                 TriQ4Node* q4, float4* grid, hipStream_t stream) {
+    const uint32_t n = 4u * n_q4;
+    hipLaunchKernelGGL(rt_tri_q4_fill_kernel, dim3(n ? (n + 255u) / 256u : 1u), dim3(256), 0, stream, bin, n_bin, src,
+                       n_q4, q4, grid);
     return hipGetLastError();
 }

@@ -62,59 +62,15 @@ RT_TC_FN float f_up(double v) {
 }
 RT_TC_FN double len3(double x, double y, double z) { return sqrt(x * x + y * y + z * z); }
 
-// Running state of a coefficient build over a leaf's triangles (double).
+// One triangle's certificate terms (double): its unit normal and error coefficients b, k.
 struct Acc {
-    double ax, ay, az;  // axis (unit), valid when n > 0
-    double phi;         // half-angle (radians), an upper bound
+    double ax, ay, az;  // the unit normal N / |N|, valid when n > 0
     double b, k;
-    uint32_t n;         // triangles (or children) merged
+    uint32_t n;         // 1 once a triangle was added
     bool valid;
 };
 
-RT_TC_FN Acc acc_empty() { return Acc{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0u, true}; }
-
-RT_TC_FN double angle_between(double x0, double y0, double z0, double x1, double y1, double z1) {
-    // both unit; |cos| folded (N and -N alike); acos error covered by the +1e-9 slack of the callers
-    double c = fabs(x0 * x1 + y0 * y1 + z0 * z1);
-    c = c > 1.0 ? 1.0 : c;
-    return acos(c);
-}
-
-// Adds a cone (unit axis x, half-angle p) to acc: the new axis is the sign-aligned
-// sum of the two axes, the new half-angle the larger of (angle to each old axis +
-// its half-angle). Conservative: every direction in either cone is in the result.
-// (A single triangle's Acc holds its unit normal as the axis.)
-RT_TC_FN void acc_add_cone(Acc& acc, double x, double y, double z, double p) {
-    if (acc.n == 0u) {
-        acc.ax = x;
-        acc.ay = y;
-        acc.az = z;
-        acc.phi = p;
-        acc.n = 1u;
-        return;
-    }
-    const double s = (acc.ax * x + acc.ay * y + acc.az * z) < 0.0 ? -1.0 : 1.0;
-    // weight the running axis by its count so a leaf's axis is near the normals' mean
-    const double w = (double)acc.n;
-    double nx = acc.ax * w + s * x, ny = acc.ay * w + s * y, nz = acc.az * w + s * z;
-    const double l = len3(nx, ny, nz);
-    if (!(l > 1e-12)) {  // opposite axes cancel: keep the old axis
-        nx = acc.ax;
-        ny = acc.ay;
-        nz = acc.az;
-    } else {
-        nx /= l;
-        ny /= l;
-        nz /= l;
-    }
-    const double p_old = angle_between(nx, ny, nz, acc.ax, acc.ay, acc.az) + acc.phi;
-    const double p_new = angle_between(nx, ny, nz, x, y, z) + p;
-    acc.ax = nx;
-    acc.ay = ny;
-    acc.az = nz;
-    acc.phi = (p_old > p_new ? p_old : p_new) + 1e-9;
-    acc.n += 1u;
-}
+RT_TC_FN Acc acc_empty() { return Acc{0.0, 0.0, 0.0, 0.0, 0.0, 0u, true}; }
 
 // One triangle record (the f32 values the kernel reads: a, edge_ab, edge_ac,
 // calc_normal) of a leaf whose sub-object box is [lo, hi].
@@ -154,7 +110,10 @@ RT_TC_FN void acc_add_triangle(Acc& acc, const float a[3], const float ab[3], co
     const double k = b * pa + (pab + pac) * (e + 8.0 * kU * nn) / NN + excess + 2.0 * kU * (pab + pac) + 1e-15;
     acc.b = fmax(acc.b, b);
     acc.k = fmax(acc.k, k);
-    acc_add_cone(acc, Nx / NN, Ny / NN, Nz / NN, 1e-9);
+    acc.ax = Nx / NN;
+    acc.ay = Ny / NN;
+    acc.az = Nz / NN;
+    acc.n = 1u;
 }
 
 }  // namespace tricone

@@ -316,8 +316,8 @@ class Renderer:
 
     def set_triangle_pruning(self, mode: int) -> None:
         """rt_set_triangle_pruning: distance pruning of the triangle walk.
-        1 (default): certified by per-node normal cones and a derived f32 error bound, exact
-        by construction; 0: box culling only (exact); 2: the round-3 relative slack (faster
+        1 (default): per-leaf certificates (each triangle's own normal and a derived f32 error
+        bound), exact by construction; 0: box culling only (exact); 2: the round-3 relative slack (faster
         on incoherent meshes, not exact)."""
         self._call("rt_set_triangle_pruning", int(mode))
 

@@ -600,18 +600,34 @@ def test_gpu_lds_vertex_indexed_triangles(gpu, oracle_lib, monkeypatch, compact,
     SceneTriangle::new's arithmetic reproduces every record from its vertices; the leaves then
     recompute edge_ab / edge_ac / calc_normal (src/buffers.rs:66-95). On (chess), off, and with
     records that do not follow from their vertices (calc_normal a few ulp off on some
-    triangles: the table is refused and the 64-B records are read): the oracle's result."""
-    monkeypatch.setenv("RT_TRI_LDS_COMPACT", compact)
+    triangles: the table is refused and the 64-B records are read): the oracle's result.
+    The table is a build switch (-DRT_LDS_COMPACT=1, off in the product build): whether the
+    loaded library stages it is read from the launch's LDS image (the table adds to it), and the
+    'on' cases skip when it does not."""
     scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
+    rays = scene.camera.recalculate_ray_directions()
+
+    def lds_bytes(env):
+        monkeypatch.setenv("RT_TRI_LDS_COMPACT", env)
+        with Renderer(scene, camera_rays=rays) as r:
+            r.compute_frame(bounces)
+            cfg = r.launch_config()
+            assert cfg["scene_in_lds"] == 2
+            return cfg["lds_bytes"]
+
+    off = lds_bytes("0")
+    if compact == "1":
+        on = lds_bytes("1")
+        if on == off:
+            pytest.skip("library built without -DRT_LDS_COMPACT=1: no vertex table to test")
+        assert on > off  # the table is staged for the consistent records
     if perturb:
         obj = scene.objects[3]
         obj.triangles = obj.triangles.copy()
         obj.triangles["calc_normal"][::5] *= np.float32(1.0000002)
-    rays = scene.camera.recalculate_ray_directions()
+        assert lds_bytes(compact) == off  # refused: the records are read
+    monkeypatch.setenv("RT_TRI_LDS_COMPACT", compact)
     acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
-    with Renderer(scene, camera_rays=rays) as r:
-        r.compute_frame(bounces)
-        assert r.launch_config()["scene_in_lds"] == 2
     assert_same(acc, out, n, *oracle_frames(oracle_lib, scene, bounces, 2, rays))
 
 
@@ -874,6 +890,31 @@ def test_gpu_triangle_accelerators(gpu, oracle_lib, monkeypatch, config, kw, wid
     scene, bounces = build_config(config, width=96, height=64, **kw)
     acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
     assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
+
+
+@pytest.mark.parametrize("env", [
+    {"RT_TRI_Q4": "1"},
+    {"RT_TRI_Q4": "1", "RT_PRIMARY_PASS": "1"},
+    {"RT_TRI_Q4": "1", "RT_TRI_PRUNE": "0"},
+    {"RT_COOP_LEAVES": "0"},
+    {"RT_TRI_Q4": "1", "RT_BLOCK_THREADS": "256"},
+])
+@pytest.mark.parametrize("config,kw", [("c4_mixed", dict(env_size=(256, 128))), ("c5_heightfield", dict(nx=60, nz=30)),
+                                       ("c3_chess", dict(env_size=(512, 256)))])
+def test_gpu_global_walk_variants(gpu, oracle_lib, monkeypatch, config, kw, env):
+    """The walks from global memory (scene not staged in LDS: RT_LDS_MODE=1): the 4-wide
+    quantized accelerator with its per-lane LDS stack (tri_q4.h, RT_TRI_Q4=1; with the primary
+    pre-pass's packet walk, without pruning, at 256 threads), and per-lane leaf tests instead of
+    the cooperative leaf batches (RT_COOP_LEAVES=0): the oracle's images and ray counts."""
+    monkeypatch.setenv("RT_LDS_MODE", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scene, bounces = build_config(config, width=96, height=64, **kw)
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
+    assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
+    with Renderer(scene) as r:
+        r.compute_frame(bounces)
+        assert r.launch_config()["scene_in_lds"] <= 1
 
 
 def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):

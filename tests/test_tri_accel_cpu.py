@@ -201,6 +201,10 @@ def test_adversarial_grazing_rays_certified_pruning(harness, tmp_path, seed, h_r
     assert gap_checked > 0 and coop_leaves > 0
     if c_range[1] >= 1e-3:
         assert gap_skipped > 0
+    q4 = line(out, "q4")  # the 4-wide walk, its certificate gaps carried through the stack in 11 bits
+    assert q4[0] == "1" and float(q4[2]) > 0
+    if c_range[1] >= 1e-3:
+        assert float(q4[4]) > 0
 
 
 def test_certified_pruning_real_scenes(harness, tmp_path):
@@ -215,3 +219,7 @@ def test_certified_pruning_real_scenes(harness, tmp_path):
     assert int(valid) == int(total)
     box_tests = float(out.stdout.splitlines()[0].split()[3])
     assert float(skipped) > 0 and float(tests) < box_tests
+    # the 4-wide quantized walk (tri_q4.h) ran on every ray, exact (checked ray by ray), with a
+    # quarter or less of the binary walk's dependent node loads
+    q4 = line(out, "q4")
+    assert q4[0] == "1" and 0 < float(q4[1]) < 0.5 * float(nodes)

@@ -17,7 +17,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from rust_gpu_raytracing_amd import Renderer  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
-HEADER = 12  # kDiagHeaderWords (csrc/rt_kernel_args.h): counters ahead of the per-wave records
+HEADER = 32  # kDiagHeaderWords (csrc/rt_kernel_args.h): counters ahead of the per-wave records
 argv = sys.argv[1:]
 fb = 1
 rank, world = 0, 1
