@@ -167,6 +167,20 @@ __device__ __forceinline__ bool ray_in_bounds(f3 o, f3 inv, const float* mn, con
     return near_t <= far_t && far_t >= 0.0f;
 }
 
+// ray_in_bounds on a 32-B record read as two float4 ({min, first}, {max, count}), with the
+// x/y subtractions and products as packed f32 pairs (v_pk_add_f32 / v_pk_mul_f32: the same
+// IEEE operations two lanes per instruction) and z's min/max pair as the third: the same
+// values, the same minNum/maxNum folds, the same result as ray_in_bounds.
+typedef float rt_v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool ray_in_box_pk(rt_v2f oxy, rt_v2f ozz, rt_v2f ixy, rt_v2f izz, float4 lo, float4 hi) {
+    const rt_v2f t1 = (rt_v2f{lo.x, lo.y} - oxy) * ixy;   // tminx, tminy
+    const rt_v2f t2 = (rt_v2f{hi.x, hi.y} - oxy) * ixy;   // tmaxx, tmaxy
+    const rt_v2f tz = (rt_v2f{lo.z, hi.z} - ozz) * izz;   // tminz, tmaxz
+    const float near_t = fmax_nn(fmax_nn(fmin_nn(t1.x, t2.x), fmin_nn(t1.y, t2.y)), fmin_nn(tz.x, tz.y));
+    const float far_t = fmin_nn(fmin_nn(fmax_nn(t1.x, t2.x), fmax_nn(t1.y, t2.y)), fmax_nn(tz.x, tz.y));
+    return near_t <= far_t && far_t >= 0.0f;
+}
+
 // Closest triangle found so far: distance, position in the reference's sweep
 // order (tie-break), triangle and object index, facing.
 struct TriHit {
@@ -2159,12 +2173,11 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 constexpr uint32_t kBruteThreads = 256;     // 4 8x8 tiles per workgroup
 constexpr uint32_t kBruteTileSubs = 1024;   // sub-object records per LDS tile (32 KB)
 
+// The brute-force kernels' LDS scene image (the persistent kernel's mode 1: spheres in slot
+// order, materials + glass constants, objects, sRGB table and camera block); the caller
+// synchronises before reading it. Returns the view of it; `cam` receives the camera block.
 template <bool kTris>
-__global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint32_t block_rays;
-    const uint32_t tid = threadIdx.x;
-    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
+__device__ __forceinline__ SceneView brute_stage(const KernelArgs& ka, unsigned char* lds, uint32_t tid, float*& l_cam) {
     // scene staging as the persistent kernel's mode 1 (spheres in slot order, materials + glass
     // constants, objects, sRGB table), then the sub-object tile
     float4* l_sph = reinterpret_cast<float4*>(lds);
@@ -2174,7 +2187,6 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
     uint32_t* l_orig = reinterpret_cast<uint32_t*>(lds + ka.lds_orig_offset);
     uint32_t* l_smat = reinterpret_cast<uint32_t*>(lds + ka.lds_smat_offset);
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
-    RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_stack_offset);
     for (uint32_t i = tid; i < ka.sphere_slot_count; i += kBruteThreads) {
         l_sph[i] = ka.sphere_slots[i];
         l_orig[i] = ka.sphere_orig[i];
@@ -2195,18 +2207,52 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
     if constexpr (kTris)
         for (uint32_t i = tid; i < ka.object_count; i += kBruteThreads) l_obj[i] = ka.objects[i];
     for (uint32_t i = tid; i < 256u; i += kBruteThreads) l_srgb[i] = ka.srgb[i];
-    float* l_cam = l_srgb + 256;  // camera block for device-side primary rays
+    l_cam = l_srgb + 256;  // camera block for device-side primary rays
     if (tid < 16u) {
         l_cam[tid] = ka.inv_proj[tid];
         l_cam[16u + tid] = ka.inv_view[tid];
     }
-    if (tid == 0) {
-        l_cam[32] = ka.aspect;
-        block_rays = 0;
+    if (tid == 0) l_cam[32] = ka.aspect;
+    return SceneView{l_sph, l_orig, l_smat, nullptr, l_mat, l_aux, l_obj, l_srgb, nullptr, nullptr, 0.0f,
+                     nullptr, nullptr, 0u,     ka.sub_objects};
+}
+
+// The triangles of one sub-object whose box the ray entered, in the sweep's order (:449-481):
+// `>=` rejects a later equal distance, a NaN distance is accepted and then accepts every later one.
+__device__ __forceinline__ void brute_sub_triangles(const KernelArgs& ka, f3 o, f3 d, uint32_t first_tri,
+                                                    uint32_t count, uint32_t oi, float& closest, TriHit& best) {
+    for (uint32_t j = 0; j < count; ++j) {
+        const uint32_t ti = min(first_tri + j, ka.triangle_count - 1u);
+        const TriGeom g = load_tri(ka.triangles, ti);
+        const float det = -dot(d, g.cn);
+        const float inv_det = 1.0f / det;
+        const f3 ao = o - g.a;
+        const float dist = dot(ao, g.cn) * inv_det;
+        if (dist < 0.0f || dist >= closest) continue;
+        const f3 dao = cross(ao, d);
+        const float v = -dot(g.ab, dao) * inv_det;
+        if (v < 0.0f) continue;
+        const float u = dot(g.ac, dao) * inv_det;
+        if (u < 0.0f) continue;
+        const float w = 1.0f - u - v;
+        if (w < 0.0f) continue;
+        closest = dist;
+        best = TriHit{dist, 0u, ti, oi, det > 0.0f};
     }
+}
+
+template <bool kTris>
+__global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t block_rays;
+    const uint32_t tid = threadIdx.x;
+    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
+    float* l_cam;
+    const SceneView sv = brute_stage<kTris>(ka, lds, tid, l_cam);
+    RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_stack_offset);
+    const RtObject* l_obj = sv.obj;
+    if (tid == 0) block_rays = 0;
     __syncthreads();
-    SceneView sv{l_sph, l_orig, l_smat, nullptr, l_mat, l_aux, l_obj, l_srgb, nullptr, nullptr, 0.0f,
-                 nullptr, nullptr, 0u,     ka.sub_objects};
 
     // this thread's pixel: local tile blockIdx * 4 + tid / 64 (global tile local * world + rank)
     const uint32_t local_tile = blockIdx.x * (kBruteThreads / 64u) + (tid >> 6);
@@ -2265,24 +2311,8 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
                             for (uint32_t k = 0; k < nt; ++k) {
                                 const RtSubObject& sub = l_sub[k];  // broadcast read
                                 if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
-                                for (uint32_t j = 0; j < sub.triangle_count; ++j) {
-                                    const uint32_t ti = min(sub.first_triangle_index + j, ka.triangle_count - 1u);
-                                    const TriGeom g = load_tri(ka.triangles, ti);
-                                    const float det = -dot(d, g.cn);
-                                    const float inv_det = 1.0f / det;
-                                    const f3 ao = o - g.a;
-                                    const float dist = dot(ao, g.cn) * inv_det;
-                                    if (dist < 0.0f || dist >= closest) continue;
-                                    const f3 dao = cross(ao, d);
-                                    const float v = -dot(g.ab, dao) * inv_det;
-                                    if (v < 0.0f) continue;
-                                    const float u = dot(g.ac, dao) * inv_det;
-                                    if (u < 0.0f) continue;
-                                    const float w = 1.0f - u - v;
-                                    if (w < 0.0f) continue;
-                                    closest = dist;
-                                    ts.tri = TriHit{dist, 0u, ti, oi, det > 0.0f};
-                                }
+                                brute_sub_triangles(ka, o, d, sub.first_triangle_index, sub.triangle_count, oi,
+                                                    closest, ts.tri);
                             }
                         }
                     }
@@ -2317,6 +2347,224 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) 
             al = clamp01(p.light.w);
         }
         ka.output[index] = pack_rgba8(r, g, b, al);
+    }
+    atomicAdd(&block_rays, rays);
+    __syncthreads();
+    if (tid == 0) {
+        if (block_rays) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
+        if (streamed && ka.stream_bytes) atomicAdd(ka.stream_bytes, (unsigned long long)streamed * 32ull);
+    }
+    if (ka.launch_clock) {
+        __syncthreads();
+        if (tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
+    }
+}
+
+// ---- the brute-force sweep as a wavefront (rt_brute_wf_kernel) ---------------------------
+//
+// rt_brute_kernel keeps a workgroup's 256 paths in lockstep: it sweeps the sub-object array
+// for every bounce while any of its paths is alive, so most of its lanes idle once paths end at
+// different bounces (C5: ~2 segments per path on average, but a workgroup runs until its
+// longest path ends; PMC: half the lanes of each VALU instruction masked off). Here the paths
+// live in HBM (KernelArgs::brute_paths, 64 B per pixel slot) and each launch advances one
+// bounce level of one pass (frame, sample) over a compacted queue of the slots still alive:
+// every lane of a sweep carries a live ray. The sweep itself is the reference's (:422-517, the
+// same tests in the same order per ray, brute_sub_triangles); the sub-object records stream
+// through two LDS tiles, the next tile's loads in flight while the current one is tested, one
+// barrier per tile. Per pixel the passes run in order and a finished path adds its light to the
+// accumulation then, the reference's sum order (:164-178).
+#ifndef RT_BRUTE_TILE
+#define RT_BRUTE_TILE 512
+#endif
+#ifndef RT_BRUTE_GROUP
+#define RT_BRUTE_GROUP 4
+#endif
+constexpr uint32_t kBruteGroup = RT_BRUTE_GROUP;  // boxes tested per group (see the sweep)
+constexpr uint32_t kBruteWfTileSubs = RT_BRUTE_TILE;  // sub-object records per LDS tile (x2 buffers)
+constexpr uint32_t kBruteWfLoads = 2u * kBruteWfTileSubs / kBruteThreads;  // 16-B loads per thread and tile
+static_assert(kBruteWfLoads * kBruteThreads == 2u * kBruteWfTileSubs, "tile = whole 16-B loads per thread");
+
+template <bool kTris>
+__global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t block_rays;
+    const uint32_t tid = threadIdx.x;
+    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
+    const uint32_t n_slots = ka.owned_tiles * 64u;
+    const uint32_t level = ka.brute_level;
+    uint32_t* counts = ka.brute_counts + (size_t)ka.brute_pass * kBruteLevels;
+    const uint32_t n_in = level == 0u ? n_slots : counts[level];
+    if (blockIdx.x * kBruteThreads >= n_in) {  // nothing for this workgroup (the queue shrank)
+        if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
+        return;
+    }
+    float* l_cam;
+    const SceneView sv = brute_stage<kTris>(ka, lds, tid, l_cam);
+    uint4* l_tile = reinterpret_cast<uint4*>(lds + ka.lds_stack_offset);  // 2 x kBruteWfTileSubs records
+    if (tid == 0) block_rays = 0;
+    __syncthreads();
+
+    const bool accumulate = ka.accumulate == 1u;
+    const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;
+    const uint32_t frame = ka.brute_pass / samples, sample = ka.brute_pass % samples;
+    const bool last_pass = ka.brute_pass + 1u == ka.frames * samples;
+    const uint32_t random_index = ka.accumulation_index + (accumulate ? frame : 0u) + sample;
+    const uint32_t* q_in = ka.brute_queue + (size_t)(level & 1u) * n_slots;
+    uint32_t* q_out = ka.brute_queue + (size_t)((level + 1u) & 1u) * n_slots;
+    float4* pl0 = ka.brute_paths;
+    float4* pl1 = pl0 + n_slots;
+    float4* pl2 = pl1 + n_slots;
+    float4* pl3 = pl2 + n_slots;
+    uint32_t rays = 0;
+    uint64_t streamed = 0;
+    for (uint32_t c = blockIdx.x; c * kBruteThreads < n_in; c += gridDim.x) {
+        const uint32_t qi = c * kBruteThreads + tid;
+        const bool have = qi < n_in;
+        const uint32_t s = have ? (level == 0u ? qi : q_in[qi]) : 0u;
+        const uint32_t local_tile = s >> 6, lane_slot = s & 63u;
+        const uint32_t gt = local_tile * ka.world_size + ka.rank;
+        const uint32_t x = (gt % ka.tiles_x) * 8u + (lane_slot & 7u);
+        const uint32_t y = (gt / ka.tiles_x) * 8u + (lane_slot >> 3);
+        const bool valid = have && local_tile < ka.owned_tiles && x < ka.width && y < ka.height;
+        const uint32_t index = valid ? y * ka.width + x : 0u;
+        Path p;
+        if (level == 0u) {
+            if (valid) start_sample(ka, index, random_index, pixel_ray(ka, l_cam, index, x, y), p);
+        } else if (valid) {
+            const float4 a = pl0[s], b = pl1[s];
+            p.o = mk(a.x, a.y, a.z);
+            p.seed = __float_as_uint(a.w);
+            p.d = mk(b.x, b.y, b.z);
+            p.bounce = __float_as_uint(b.w);
+            const float4 l = pl2[s], k = pl3[s];
+            p.light = f4{l.x, l.y, l.z, l.w};
+            p.contrib = f4{k.x, k.y, k.z, k.w};
+        }
+        const bool alive = valid && p.bounce < ka.bounces;
+        // check_spheres (:355-404), every sphere
+        TraceState ts;
+        ts.sph = SphereHit{kF32Max, 0u, 0u};
+        ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
+        const f3 o = p.o, d = p.d;
+        if (alive) {
+            const float a = dot(d, d);
+            for (uint32_t i = 0; i < ka.sphere_slot_count; i += 4u) test_sphere_group(sv, i, o, d, 4.0f * a, 2.0f * a, ts.sph);
+        }
+        // check_triangles (:422-517): objects in order, their sub-objects through the LDS tiles
+        if constexpr (kTris) {
+            const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+            float closest = kF32Max;
+            for (uint32_t oi = 0; oi < ka.object_count; ++oi) {
+                const RtObject& ob = sv.obj[oi];
+                const bool in_obj = alive && ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds);
+                if (!__syncthreads_or(in_obj)) continue;  // (a barrier: the tiles are free)
+                const uint32_t first = ob.first_sub_object_index, n_sub = ob.sub_object_count;
+                const uint32_t n_tiles = (n_sub + kBruteWfTileSubs - 1u) / kBruteWfTileSubs;
+                const uint4* src = reinterpret_cast<const uint4*>(ka.sub_objects);
+                const uint32_t last_sub = ka.sub_object_count - 1u;
+                uint4 r[kBruteWfLoads];
+                auto load_tile = [&](uint32_t t) {
+                    const uint32_t base = t * kBruteWfTileSubs, nt = min(kBruteWfTileSubs, n_sub - base);
+#pragma unroll
+                    for (uint32_t k = 0; k < kBruteWfLoads; ++k) {
+                        const uint32_t q = tid + k * kBruteThreads;
+                        if (q < 2u * nt) r[k] = src[2u * min(first + base + (q >> 1), last_sub) + (q & 1u)];
+                    }
+                };
+                auto store_tile = [&](uint32_t t) {
+                    uint4* dst = l_tile + (size_t)(t & 1u) * 2u * kBruteWfTileSubs;
+                    const uint32_t nt = min(kBruteWfTileSubs, n_sub - t * kBruteWfTileSubs);
+#pragma unroll
+                    for (uint32_t k = 0; k < kBruteWfLoads; ++k) {
+                        const uint32_t q = tid + k * kBruteThreads;
+                        if (q < 2u * nt) dst[q] = r[k];
+                    }
+                };
+                if (n_tiles) {
+                    load_tile(0u);
+                    store_tile(0u);
+                }
+                for (uint32_t t = 0; t < n_tiles; ++t) {
+                    __syncthreads();  // tile t stored; every reader of tile t - 1's buffer done
+                    const uint32_t nt = min(kBruteWfTileSubs, n_sub - t * kBruteWfTileSubs);
+                    if (tid == 0) streamed += nt;
+                    const bool more = t + 1u < n_tiles;
+                    if (more) load_tile(t + 1u);  // in flight during the tests
+                    if (in_obj) {
+                        const float4* tile = reinterpret_cast<const float4*>(l_tile + (size_t)(t & 1u) * 2u * kBruteWfTileSubs);
+                        const rt_v2f oxy = {o.x, o.y}, ozz = {o.z, o.z}, ixy = {inv.x, inv.y}, izz = {inv.z, inv.z};
+                        // groups of kBruteGroup boxes: the box tests of a group issue together (their
+                        // LDS reads in flight at once), then the hit sub-objects' triangles in order
+                        uint32_t k = 0;
+                        for (; k + kBruteGroup <= nt; k += kBruteGroup) {
+                            RT_ISA_MARK("brute_box");
+                            bool any = false;
+#pragma unroll
+                            for (uint32_t j = 0; j < kBruteGroup; ++j)  // broadcast reads
+                                any |= ray_in_box_pk(oxy, ozz, ixy, izz, tile[2u * (k + j)], tile[2u * (k + j) + 1u]);
+                            if (any) {  // (rare) the group's boxes again, one at a time, in order
+                                for (uint32_t j = 0; j < kBruteGroup; ++j) {
+                                    const float4 lo = tile[2u * (k + j)], hi = tile[2u * (k + j) + 1u];
+                                    if (!ray_in_box_pk(oxy, ozz, ixy, izz, lo, hi)) continue;
+                                    brute_sub_triangles(ka, o, d, __float_as_uint(lo.w), __float_as_uint(hi.w), oi,
+                                                        closest, ts.tri);
+                                }
+                            }
+                        }
+                        for (; k < nt; ++k) {
+                            const float4 lo = tile[2u * k], hi = tile[2u * k + 1u];
+                            if (!ray_in_box_pk(oxy, ozz, ixy, izz, lo, hi)) continue;
+                            brute_sub_triangles(ka, o, d, __float_as_uint(lo.w), __float_as_uint(hi.w), oi, closest, ts.tri);
+                        }
+                    }
+                    if (more) store_tile(t + 1u);
+                }
+            }
+        }
+        bool done = valid && !alive;  // bounces == 0: the path ends untraced
+        if (alive) {
+            ++rays;
+            const Hit h = trace_end<kTris>(sv, ka, o, d, ts);
+            done = shade<true>(sv, ka, p, h);
+        }
+        const bool cont = alive && !done;
+        if (cont) {
+            pl0[s] = make_float4(p.o.x, p.o.y, p.o.z, __uint_as_float(p.seed));
+            pl1[s] = make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.bounce));
+            pl2[s] = make_float4(p.light.x, p.light.y, p.light.z, p.light.w);
+            pl3[s] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.contrib.w);
+        }
+        // the live slots to the next level's queue (wave-aggregated)
+        const uint64_t m = __ballot(cont);
+        if (m) {
+            const uint32_t lane = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            uint32_t base = 0u;
+            if ((tid & 63u) == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(counts + level + 1u, (uint32_t)__popcll(m));
+            base = __builtin_amdgcn_readlane(base, (uint32_t)__builtin_ctzll(m));
+            if (cont) q_out[base + lane] = s;
+        }
+        if (done) {  // the sample's light (:164-178), in pass order per pixel
+            float r, g, b, al;
+            if (accumulate) {
+                float4 pix = ka.accum[index];
+                pix.x = pix.x + p.light.x;
+                pix.y = pix.y + p.light.y;
+                pix.z = pix.z + p.light.z;
+                pix.w = pix.w + p.light.w;
+                ka.accum[index] = pix;
+                const float div = (float)((ka.accumulation_index + ka.frames - 1u) * ka.compute_per_frame);
+                r = clamp01(pix.x / div);
+                g = clamp01(pix.y / div);
+                b = clamp01(pix.z / div);
+                al = clamp01(pix.w / div);
+            } else {
+                r = clamp01(p.light.x);
+                g = clamp01(p.light.y);
+                b = clamp01(p.light.z);
+                al = clamp01(p.light.w);
+            }
+            if (last_pass) ka.output[index] = pack_rgba8(r, g, b, al);
+        }
     }
     atomicAdd(&block_rays, rays);
     __syncthreads();
@@ -2659,6 +2907,24 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 }
 
 size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
+
+size_t rt_brute_wf_tile_bytes() { return 2u * (size_t)kBruteWfTileSubs * sizeof(RtSubObject); }
+
+// One (pass, bounce level) of the wavefront; `blocks` workgroups stride over the level's queue.
+hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, size_t lds_bytes, uint32_t blocks, hipStream_t stream) {
+    if (blocks == 0) return hipSuccess;
+    if (lds_bytes > 64u * 1024u) {
+        const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_wf_kernel<true>)
+                              : reinterpret_cast<const void*>(&rt_brute_wf_kernel<false>);
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        if (e != hipSuccess) return hipErrorInvalidConfiguration;
+    }
+    if (tris)
+        hipLaunchKernelGGL(rt_brute_wf_kernel<true>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+    else
+        hipLaunchKernelGGL(rt_brute_wf_kernel<false>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+    return hipGetLastError();
+}
 
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream) {

@@ -58,6 +58,8 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
 size_t rt_brute_tile_bytes();
+hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, size_t lds_bytes, uint32_t blocks, hipStream_t stream);
+size_t rt_brute_wf_tile_bytes();
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
                              uint32_t samples, uint32_t frames, unsigned long long* clock, hipStream_t stream);
@@ -333,6 +335,12 @@ struct rt_ctx {
     uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
     size_t primary_cap = 0;
     unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
+    // the brute-force wavefront (rt_brute_wf_kernel; RT_BRUTE_WF=0: the lockstep rt_brute_kernel)
+    bool brute_wf = true;
+    float4* d_brute_paths = nullptr;
+    uint32_t* d_brute_queue = nullptr;
+    uint32_t* d_brute_counts = nullptr;
+    size_t brute_paths_cap = 0, brute_queue_cap = 0, brute_counts_cap = 0;
     uint32_t tri_nodes = 0, tri_prim_count = 0;
     float* d_tri_extent = nullptr;   // margin extent, in device memory (refit updates it)
     uint32_t* d_tri_order = nullptr; // node indices by depth, deepest level first (refit)
@@ -812,6 +820,21 @@ int dev_alloc(rt_ctx* ctx, T** p, size_t count) {
     return RT_OK;
 }
 
+// A device buffer of at least `bytes`, reallocated (after the streams drain) when smaller.
+int grow_buffer(rt_ctx* ctx, void** p, size_t* cap, size_t bytes) {
+    if (*p && *cap >= bytes) return RT_OK;
+    RT_HIP(ctx, join_aux(ctx));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (*p) RT_HIP(ctx, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    const size_t alloc = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(p, alloc);
+    if (e != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    *cap = alloc;
+    return RT_OK;
+}
+
 int collect_timing(rt_ctx* ctx) {
     if (ctx->clock_pending.empty()) return RT_OK;
     RT_HIP(ctx, join_aux(ctx));
@@ -941,6 +964,8 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (ctx->primary_threads != 256u) ctx->primary_min_waves = 0;  // the 64-VGPR variant is built at 256
         env = std::getenv("RT_BRUTE_FORCE");
         ctx->brute = env && env[0] == '1';
+        env = std::getenv("RT_BRUTE_WF");
+        if (env) ctx->brute_wf = env[0] != '0';
         env = std::getenv("RT_TRI_COMPACT");
         if (env) ctx->tri_compact = env[0] == '0' ? 0 : 1;
         env = std::getenv("RT_SPHERE_LEAF");
@@ -1060,7 +1085,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
                     ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
                     ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx, ctx->d_tri_ltris, ctx->d_tri_q4, ctx->d_tri_q4src,
-                    ctx->d_tri_q4grid};
+                    ctx->d_tri_q4grid, ctx->d_brute_paths, ctx->d_brute_queue, ctx->d_brute_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1476,7 +1501,11 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         carve(1, kLdsSceneBudget);
         ka.lds_srgb_offset = (uint32_t)(mode1_bytes - kLdsTailBytes);
         ka.lds_stack_offset = (uint32_t)al16(mode1_bytes);
-        const size_t lds = ka.lds_stack_offset + rt_brute_tile_bytes();
+        const uint32_t samples = ka.accumulate == 1u ? ka.compute_per_frame : 1u;
+        const uint64_t passes = (uint64_t)frames * samples;
+        // the wavefront: every pass (frame, sample) in order, one launch per bounce level
+        const bool wf = ctx->brute_wf && passes > 0 && passes <= (1u << 20) && bounces + 2u <= kBruteLevels;
+        const size_t lds = ka.lds_stack_offset + (wf ? rt_brute_wf_tile_bytes() : rt_brute_tile_bytes());
         int dev = 0, max_optin = 0;
         RT_HIP(ctx, hipGetDevice(&dev));
         RT_HIP(ctx, hipDeviceGetAttribute(&max_optin, hipDeviceAttributeSharedMemPerBlockOptin, dev));
@@ -1502,8 +1531,34 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ka.launch_clock = ctx->d_clock + kClockWords * (size_t)slot;  // zero: dev_alloc / collect_timing
             ctx->clock_pending.push_back(slot);
         }
-        RT_HIP(ctx, rt_launch_brute(ka, tris, lds, ctx->stream));
-        ctx->last_blocks = (ctx->owned_tiles + 3u) / 4u;
+        if (wf) {
+            const size_t n_slots = (size_t)ctx->owned_tiles * 64u;
+            int rc;
+            if ((rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_paths), &ctx->brute_paths_cap,
+                                  4 * n_slots * sizeof(float4))) ||
+                (rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_queue), &ctx->brute_queue_cap,
+                                  2 * n_slots * sizeof(uint32_t))) ||
+                (rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_counts), &ctx->brute_counts_cap,
+                                  passes * kBruteLevels * sizeof(uint32_t))))
+                return rc;
+            RT_HIP(ctx, hipMemsetAsync(ctx->d_brute_counts, 0, passes * kBruteLevels * sizeof(uint32_t), ctx->stream));
+            ka.brute_paths = ctx->d_brute_paths;
+            ka.brute_queue = ctx->d_brute_queue;
+            ka.brute_counts = ctx->d_brute_counts;
+            // workgroups per launch: enough for every chunk of 256 slots, at most 16 per CU
+            const uint32_t chunks = (uint32_t)((n_slots + 255u) / 256u);
+            const uint32_t blocks = std::min<uint32_t>(chunks, 16u * (uint32_t)std::max<int>(1, (int)ctx->n_cu));
+            for (uint64_t pass = 0; pass < passes; ++pass)
+                for (uint32_t level = 0; level < std::max(1u, bounces); ++level) {
+                    ka.brute_pass = (uint32_t)pass;
+                    ka.brute_level = level;
+                    RT_HIP(ctx, rt_launch_brute_wf(ka, tris, lds, blocks, ctx->stream));
+                }
+            ctx->last_blocks = blocks;
+        } else {
+            RT_HIP(ctx, rt_launch_brute(ka, tris, lds, ctx->stream));
+            ctx->last_blocks = (ctx->owned_tiles + 3u) / 4u;
+        }
         ctx->last_passes = RT_PASS_BRUTE;
         ctx->last_lds = (uint32_t)lds;
         ctx->occ_threads = 256;

@@ -103,6 +103,10 @@ constexpr uint32_t kLeafTriSlots = 8;                       // triangle slots pe
 constexpr uint32_t kLeafTriWords = 3 * kLeafTriSlots;       // uint4 per block (384 B)
 constexpr uint32_t kLeafBatchWaveBytes = 64 * 48;
 
+// The brute-force wavefront: counters per pass (bounce levels 0..kBruteLevels-1, the last two
+// words the pass's claim counters); a launch has at most kBruteLevels - 2 bounces per path.
+constexpr uint32_t kBruteLevels = 64;
+
 // Diagnostic counters ahead of the per-wave records in KernelArgs::diag
 // (RT_DIAG: words 0-25; RT_DIAG_TAIL: words 0-7, then 2 words per wave from here).
 constexpr uint32_t kDiagHeaderWords = 32;
@@ -229,6 +233,16 @@ struct KernelArgs {
     uint32_t primary_tile_major;  // the pre-pass takes its (frame, tile) units tile-major (1) or frame-major
     // brute-force launches (rt_brute_kernel): bytes of sub-object records streamed through LDS
     unsigned long long* __restrict__ stream_bytes;
+    // the brute-force wavefront (rt_brute_wf_kernel): per owned pixel slot the path state (4
+    // planes of float4: o + seed, d + bounce, light, contribution, plane stride = owned slots),
+    // two queues of live slots (ping-pong by bounce level), per pass kBruteLevels counters
+    // (entries of each level's queue); this launch's pass (frame * compute_per_frame + sample)
+    // and bounce level
+    float4* __restrict__ brute_paths;
+    uint32_t* __restrict__ brute_queue;
+    uint32_t* __restrict__ brute_counts;
+    uint32_t brute_pass;
+    uint32_t brute_level;
     uint32_t texture_width;
     uint32_t texture_height;
     uint32_t env_map_width;

@@ -1009,10 +1009,14 @@ def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumul
     ("c4_mixed", dict(env_size=(256, 128)), 2, 3),
     ("c5_heightfield", dict(nx=60, nz=30), 2, 1),
 ])
-def test_gpu_brute_force_mode(gpu, oracle_lib, config, kw, batch, world):
+@pytest.mark.parametrize("wf", ["1", "0"])
+def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, world, wf):
     """rt_set_brute_force: the reference's own sphere and object -> sub-object ->
     triangle sweeps, sub-objects streamed through LDS tiles (BASELINE config 5's
-    stress mode) -- bit-identical to the oracle, in frame batches and tile splits."""
+    stress mode) -- bit-identical to the oracle, in frame batches and tile splits. Both
+    kernels: the wavefront over compacted queues of live paths (rt_brute_wf_kernel, the
+    default) and the lockstep workgroups (RT_BRUTE_WF=0, rt_brute_kernel)."""
+    monkeypatch.setenv("RT_BRUTE_WF", wf)
     scene, bounces = build_config(config, width=96, height=64, **kw)
     rays = scene.camera.recalculate_ray_directions()
     acc_o, out_o, n_o = oracle_frames(oracle_lib, scene, bounces, 4, rays)
@@ -1033,6 +1037,42 @@ def test_gpu_brute_force_mode(gpu, oracle_lib, config, kw, batch, world):
         n += k
     assert_same(acc, out, n, acc_o, out_o, n_o)
     assert (streamed > 0) == bool(scene.objects)
+
+
+@pytest.mark.parametrize("config,kw,spp,accumulate,batch,bounces", [
+    ("c2_rtiow", {}, 3, 1, 2, None),
+    ("c5_heightfield", dict(nx=40, nz=20), 2, 1, 3, None),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, None),
+    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 1, 0),
+    ("c1_four_spheres", {}, 1, 1, 2, 40),
+])
+def test_gpu_brute_force_samples_and_modes(gpu, oracle_lib, config, kw, spp, accumulate, batch, bounces):
+    """The brute-force wavefront's passes: several samples per frame (each pass = one (frame,
+    sample), summed in that order per pixel), accumulation off (the last frame's image), zero
+    bounces (no launch traces; the image is written from the empty paths), and a deep bounce
+    limit (the queue levels): the oracle's images and ray counts."""
+    scene, b0 = build_config(config, width=80, height=48, **kw)
+    bounces = b0 if bounces is None else bounces
+    rays = scene.camera.recalculate_ray_directions()
+    with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp, camera_rays=rays,
+                  frame_batch=batch) as r:
+        r.set_brute_force(True)
+        for _ in range(3):
+            r.compute_frame(bounces)
+        got = r.read_accumulation(), r.read_output(), r.ray_count()
+        assert r.last_launch_passes() == ["brute"]
+    o = oracle_lib.Oracle(scene, camera_rays=rays)
+    acc = np.zeros((48, 80, 4), np.float32)
+    out = np.zeros((48, 80), np.uint32)
+    n = 0
+    for i in range(3):
+        k = i + 1 if accumulate else 1
+        n += o.render_frame(scene.params(accumulate=accumulate, compute_per_frame=spp, accumulation_index=k),
+                            bounces, acc, out)
+    if accumulate:
+        assert_same(*got, acc, out, n)
+    else:
+        assert got[2] == n and np.array_equal(got[1], out)
 
 
 def _pcg_f32(seed):
