@@ -167,18 +167,11 @@ __device__ __forceinline__ bool ray_in_bounds(f3 o, f3 inv, const float* mn, con
     return near_t <= far_t && far_t >= 0.0f;
 }
 
-// ray_in_bounds on a 32-B record read as two float4 ({min, first}, {max, count}), with the
-// x/y subtractions and products as packed f32 pairs (v_pk_add_f32 / v_pk_mul_f32: the same
-// IEEE operations two lanes per instruction) and z's min/max pair as the third: the same
-// values, the same minNum/maxNum folds, the same result as ray_in_bounds.
-typedef float rt_v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ bool ray_in_box_pk(rt_v2f oxy, rt_v2f ozz, rt_v2f ixy, rt_v2f izz, float4 lo, float4 hi) {
-    const rt_v2f t1 = (rt_v2f{lo.x, lo.y} - oxy) * ixy;   // tminx, tminy
-    const rt_v2f t2 = (rt_v2f{hi.x, hi.y} - oxy) * ixy;   // tmaxx, tmaxy
-    const rt_v2f tz = (rt_v2f{lo.z, hi.z} - ozz) * izz;   // tminz, tmaxz
-    const float near_t = fmax_nn(fmax_nn(fmin_nn(t1.x, t2.x), fmin_nn(t1.y, t2.y)), fmin_nn(tz.x, tz.y));
-    const float far_t = fmin_nn(fmin_nn(fmax_nn(t1.x, t2.x), fmax_nn(t1.y, t2.y)), fmax_nn(tz.x, tz.y));
-    return near_t <= far_t && far_t >= 0.0f;
+// ray_in_bounds on a 32-B record read as two float4 ({min, first}, {max, count}): the same
+// operations (scalar f32: gfx950 issues v_pk_*_f32 at a third of the scalar rate, build.py).
+__device__ __forceinline__ bool ray_in_box4(f3 o, f3 inv, float4 lo, float4 hi) {
+    const float mn[3] = {lo.x, lo.y, lo.z}, mx[3] = {hi.x, hi.y, hi.z};
+    return ray_in_bounds(o, inv, mn, mx);
 }
 
 // Closest triangle found so far: distance, position in the reference's sweep
@@ -2492,7 +2485,6 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs k
                     if (more) load_tile(t + 1u);  // in flight during the tests
                     if (in_obj) {
                         const float4* tile = reinterpret_cast<const float4*>(l_tile + (size_t)(t & 1u) * 2u * kBruteWfTileSubs);
-                        const rt_v2f oxy = {o.x, o.y}, ozz = {o.z, o.z}, ixy = {inv.x, inv.y}, izz = {inv.z, inv.z};
                         // groups of kBruteGroup boxes: the box tests of a group issue together (their
                         // LDS reads in flight at once), then the hit sub-objects' triangles in order
                         uint32_t k = 0;
@@ -2501,11 +2493,11 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs k
                             bool any = false;
 #pragma unroll
                             for (uint32_t j = 0; j < kBruteGroup; ++j)  // broadcast reads
-                                any |= ray_in_box_pk(oxy, ozz, ixy, izz, tile[2u * (k + j)], tile[2u * (k + j) + 1u]);
+                                any |= ray_in_box4(o, inv, tile[2u * (k + j)], tile[2u * (k + j) + 1u]);
                             if (any) {  // (rare) the group's boxes again, one at a time, in order
                                 for (uint32_t j = 0; j < kBruteGroup; ++j) {
                                     const float4 lo = tile[2u * (k + j)], hi = tile[2u * (k + j) + 1u];
-                                    if (!ray_in_box_pk(oxy, ozz, ixy, izz, lo, hi)) continue;
+                                    if (!ray_in_box4(o, inv, lo, hi)) continue;
                                     brute_sub_triangles(ka, o, d, __float_as_uint(lo.w), __float_as_uint(hi.w), oi,
                                                         closest, ts.tri);
                                 }
@@ -2513,7 +2505,7 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs k
                         }
                         for (; k < nt; ++k) {
                             const float4 lo = tile[2u * k], hi = tile[2u * k + 1u];
-                            if (!ray_in_box_pk(oxy, ozz, ixy, izz, lo, hi)) continue;
+                            if (!ray_in_box4(o, inv, lo, hi)) continue;
                             brute_sub_triangles(ka, o, d, __float_as_uint(lo.w), __float_as_uint(hi.w), oi, closest, ts.tri);
                         }
                     }
