@@ -2376,9 +2376,63 @@ constexpr uint32_t kBruteGroup = RT_BRUTE_GROUP;  // boxes tested per group (see
 constexpr uint32_t kBruteWfTileSubs = RT_BRUTE_TILE;  // sub-object records per LDS tile (x2 buffers)
 constexpr uint32_t kBruteWfLoads = 2u * kBruteWfTileSubs / kBruteThreads;  // 16-B loads per thread and tile
 static_assert(kBruteWfLoads * kBruteThreads == 2u * kBruteWfTileSubs, "tile = whole 16-B loads per thread");
+static_assert(kBruteWfLoads == 4u, "the sweep's tile loads are written out for 4 per thread");
 
+// Rays per thread in a sweep: each broadcast LDS read of a box serves kBruteRays rays (one
+// ray per thread, the LDS data return -- 64 lanes x 12 B per read -- outran the box tests'
+// VALU work: VALU issue 38% at one ray per thread).
+#ifndef RT_BRUTE_RAYS
+#define RT_BRUTE_RAYS 1
+#endif
+constexpr uint32_t kBruteRays = RT_BRUTE_RAYS;
+constexpr uint32_t kBruteChunk = kBruteRays * kBruteThreads;  // queue entries per workgroup pass
+// Entries of a ray's list of entered boxes (tile-local u16 indices, LDS) before it is drained.
+#ifndef RT_BRUTE_HITS
+#define RT_BRUTE_HITS 8
+#endif
+constexpr uint32_t kBruteHits = RT_BRUTE_HITS;
+static_assert(kBruteHits >= kBruteGroup, "a group's hits fit a drained list");
+
+// One pixel slot of the wavefront: its pixel and whether it is inside the image.
+struct BruteSlot {
+    uint32_t s, index, x, y;
+    bool valid;
+};
+__device__ __forceinline__ BruteSlot brute_slot(const KernelArgs& ka, const uint32_t* q_in, uint32_t level,
+                                                uint32_t qi, uint32_t n_in) {
+    BruteSlot r;
+    const bool have = qi < n_in;
+    r.s = have ? (level == 0u ? qi : q_in[qi]) : 0u;
+    const uint32_t local_tile = r.s >> 6, lane_slot = r.s & 63u;
+    const uint32_t gt = local_tile * ka.world_size + ka.rank;
+    r.x = (gt % ka.tiles_x) * 8u + (lane_slot & 7u);
+    r.y = (gt / ka.tiles_x) * 8u + (lane_slot >> 3);
+    r.valid = have && local_tile < ka.owned_tiles && r.x < ka.width && r.y < ka.height;
+    r.index = r.valid ? r.y * ka.width + r.x : 0u;
+    return r;
+}
+
+__device__ __forceinline__ void brute_load_path(const float4* pl, uint32_t n_slots, uint32_t s, Path& p) {
+    const float4 a = pl[s], b = pl[n_slots + s], l = pl[2u * n_slots + s], k = pl[3u * n_slots + s];
+    p.o = mk(a.x, a.y, a.z);
+    p.seed = __float_as_uint(a.w);
+    p.d = mk(b.x, b.y, b.z);
+    p.bounce = __float_as_uint(b.w);
+    p.light = f4{l.x, l.y, l.z, l.w};
+    p.contrib = f4{k.x, k.y, k.z, k.w};
+}
+__device__ __forceinline__ void brute_store_path(float4* pl, uint32_t n_slots, uint32_t s, const Path& p) {
+    pl[s] = make_float4(p.o.x, p.o.y, p.o.z, __uint_as_float(p.seed));
+    pl[n_slots + s] = make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.bounce));
+    pl[2u * n_slots + s] = make_float4(p.light.x, p.light.y, p.light.z, p.light.w);
+    pl[3u * n_slots + s] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.contrib.w);
+}
+
+#ifndef RT_BRUTE_WAVES
+#define RT_BRUTE_WAVES 4
+#endif
 template <bool kTris>
-__global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs ka) {
+__global__ void __launch_bounds__(kBruteThreads, RT_BRUTE_WAVES) rt_brute_wf_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
     const uint32_t tid = threadIdx.x;
@@ -2387,13 +2441,14 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs k
     const uint32_t level = ka.brute_level;
     uint32_t* counts = ka.brute_counts + (size_t)ka.brute_pass * kBruteLevels;
     const uint32_t n_in = level == 0u ? n_slots : counts[level];
-    if (blockIdx.x * kBruteThreads >= n_in) {  // nothing for this workgroup (the queue shrank)
+    if (blockIdx.x * kBruteChunk >= n_in) {  // nothing for this workgroup (the queue shrank)
         if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
         return;
     }
     float* l_cam;
     const SceneView sv = brute_stage<kTris>(ka, lds, tid, l_cam);
     uint4* l_tile = reinterpret_cast<uint4*>(lds + ka.lds_stack_offset);  // 2 x kBruteWfTileSubs records
+    uint16_t* l_hits = reinterpret_cast<uint16_t*>(l_tile + 4u * kBruteWfTileSubs);  // per thread and ray kBruteHits
     if (tid == 0) block_rays = 0;
     __syncthreads();
 
@@ -2404,158 +2459,220 @@ __global__ void __launch_bounds__(kBruteThreads) rt_brute_wf_kernel(KernelArgs k
     const uint32_t random_index = ka.accumulation_index + (accumulate ? frame : 0u) + sample;
     const uint32_t* q_in = ka.brute_queue + (size_t)(level & 1u) * n_slots;
     uint32_t* q_out = ka.brute_queue + (size_t)((level + 1u) & 1u) * n_slots;
-    float4* pl0 = ka.brute_paths;
-    float4* pl1 = pl0 + n_slots;
-    float4* pl2 = pl1 + n_slots;
-    float4* pl3 = pl2 + n_slots;
+    float4* pl = ka.brute_paths;
     uint32_t rays = 0;
     uint64_t streamed = 0;
-    for (uint32_t c = blockIdx.x; c * kBruteThreads < n_in; c += gridDim.x) {
-        const uint32_t qi = c * kBruteThreads + tid;
-        const bool have = qi < n_in;
-        const uint32_t s = have ? (level == 0u ? qi : q_in[qi]) : 0u;
-        const uint32_t local_tile = s >> 6, lane_slot = s & 63u;
-        const uint32_t gt = local_tile * ka.world_size + ka.rank;
-        const uint32_t x = (gt % ka.tiles_x) * 8u + (lane_slot & 7u);
-        const uint32_t y = (gt / ka.tiles_x) * 8u + (lane_slot >> 3);
-        const bool valid = have && local_tile < ka.owned_tiles && x < ka.width && y < ka.height;
-        const uint32_t index = valid ? y * ka.width + x : 0u;
-        Path p;
-        if (level == 0u) {
-            if (valid) start_sample(ka, index, random_index, pixel_ray(ka, l_cam, index, x, y), p);
-        } else if (valid) {
-            const float4 a = pl0[s], b = pl1[s];
-            p.o = mk(a.x, a.y, a.z);
-            p.seed = __float_as_uint(a.w);
-            p.d = mk(b.x, b.y, b.z);
-            p.bounce = __float_as_uint(b.w);
-            const float4 l = pl2[s], k = pl3[s];
-            p.light = f4{l.x, l.y, l.z, l.w};
-            p.contrib = f4{k.x, k.y, k.z, k.w};
-        }
-        const bool alive = valid && p.bounce < ka.bounces;
-        // check_spheres (:355-404), every sphere
-        TraceState ts;
-        ts.sph = SphereHit{kF32Max, 0u, 0u};
-        ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
-        const f3 o = p.o, d = p.d;
-        if (alive) {
-            const float a = dot(d, d);
-            for (uint32_t i = 0; i < ka.sphere_slot_count; i += 4u) test_sphere_group(sv, i, o, d, 4.0f * a, 2.0f * a, ts.sph);
+    for (uint32_t c = blockIdx.x; c * kBruteChunk < n_in; c += gridDim.x) {
+        // the chunk's rays: ray k of this thread is queue entry c * chunk + k * threads + tid
+        f3 o[kBruteRays], d[kBruteRays], inv[kBruteRays];
+        bool alive[kBruteRays];
+        SphereHit sph[kBruteRays];
+        TriHit tri[kBruteRays];
+        float closest[kBruteRays];
+#pragma unroll
+        for (uint32_t k = 0; k < kBruteRays; ++k) {
+            const BruteSlot bs = brute_slot(ka, q_in, level, c * kBruteChunk + k * kBruteThreads + tid, n_in);
+            Path p;
+            if (level == 0u) {
+                if (bs.valid) {
+                    start_sample(ka, bs.index, random_index, pixel_ray(ka, l_cam, bs.index, bs.x, bs.y), p);
+                    brute_store_path(pl, n_slots, bs.s, p);  // the state the shading below reloads
+                }
+            } else if (bs.valid) {
+                brute_load_path(pl, n_slots, bs.s, p);
+            }
+            alive[k] = bs.valid && p.bounce < ka.bounces;
+            o[k] = alive[k] ? p.o : mk(0.f, 0.f, 0.f);
+            d[k] = alive[k] ? p.d : mk(0.f, 0.f, 1.f);
+            inv[k] = mk(1.0f / d[k].x, 1.0f / d[k].y, 1.0f / d[k].z);
+            sph[k] = SphereHit{kF32Max, 0u, 0u};
+            tri[k] = TriHit{kF32Max, 0u, 0u, 0u, false};
+            closest[k] = kF32Max;
+            // check_spheres (:355-404), every sphere
+            if (alive[k]) {
+                const float a = dot(d[k], d[k]);
+                for (uint32_t i = 0; i < ka.sphere_slot_count; i += 4u)
+                    test_sphere_group(sv, i, o[k], d[k], 4.0f * a, 2.0f * a, sph[k]);
+            }
         }
         // check_triangles (:422-517): objects in order, their sub-objects through the LDS tiles
         if constexpr (kTris) {
-            const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-            float closest = kF32Max;
             for (uint32_t oi = 0; oi < ka.object_count; ++oi) {
                 const RtObject& ob = sv.obj[oi];
-                const bool in_obj = alive && ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds);
-                if (!__syncthreads_or(in_obj)) continue;  // (a barrier: the tiles are free)
+                bool in_obj[kBruteRays];
+                bool any_in = false;
+#pragma unroll
+                for (uint32_t k = 0; k < kBruteRays; ++k) {
+                    in_obj[k] = alive[k] && ray_in_bounds(o[k], inv[k], ob.min_bounds, ob.max_bounds);
+                    any_in |= in_obj[k];
+                }
+                if (!__syncthreads_or(any_in)) continue;  // (a barrier: the tiles are free)
                 const uint32_t first = ob.first_sub_object_index, n_sub = ob.sub_object_count;
                 const uint32_t n_tiles = (n_sub + kBruteWfTileSubs - 1u) / kBruteWfTileSubs;
                 const uint4* src = reinterpret_cast<const uint4*>(ka.sub_objects);
                 const uint32_t last_sub = ka.sub_object_count - 1u;
-                uint4 r[kBruteWfLoads];
-                auto load_tile = [&](uint32_t t) {
-                    const uint32_t base = t * kBruteWfTileSubs, nt = min(kBruteWfTileSubs, n_sub - base);
-#pragma unroll
-                    for (uint32_t k = 0; k < kBruteWfLoads; ++k) {
-                        const uint32_t q = tid + k * kBruteThreads;
-                        if (q < 2u * nt) r[k] = src[2u * min(first + base + (q >> 1), last_sub) + (q & 1u)];
-                    }
-                };
-                auto store_tile = [&](uint32_t t) {
-                    uint4* dst = l_tile + (size_t)(t & 1u) * 2u * kBruteWfTileSubs;
-                    const uint32_t nt = min(kBruteWfTileSubs, n_sub - t * kBruteWfTileSubs);
-#pragma unroll
-                    for (uint32_t k = 0; k < kBruteWfLoads; ++k) {
-                        const uint32_t q = tid + k * kBruteThreads;
-                        if (q < 2u * nt) dst[q] = r[k];
-                    }
-                };
+                // the next tile, in flight: kBruteWfLoads (4) 16-B loads per thread, in named registers
+                uint4 r0, r1, r2, r3;
+#define RT_BRUTE_LOAD1(k_, rk)                                                                          \
+    {                                                                                                   \
+        const uint32_t q_ = tid + (k_) * kBruteThreads;                                                 \
+        rk = src[2u * min(first + base_ + (min(q_, 2u * nt_ - 1u) >> 1), last_sub) + (q_ & 1u)];       \
+    }
+#define RT_BRUTE_LOAD_TILE(t)                                                                           \
+    {                                                                                                   \
+        const uint32_t base_ = (t) * kBruteWfTileSubs, nt_ = min(kBruteWfTileSubs, n_sub - base_);     \
+        RT_BRUTE_LOAD1(0u, r0) RT_BRUTE_LOAD1(1u, r1) RT_BRUTE_LOAD1(2u, r2) RT_BRUTE_LOAD1(3u, r3)     \
+    }
+#define RT_BRUTE_STORE1(k_, rk)                                                                         \
+    {                                                                                                   \
+        const uint32_t q_ = tid + (k_) * kBruteThreads;                                                 \
+        if (q_ < 2u * nt_) dst_[q_] = rk;                                                               \
+    }
+#define RT_BRUTE_STORE_TILE(t)                                                                          \
+    {                                                                                                   \
+        uint4* dst_ = l_tile + (size_t)((t) & 1u) * 2u * kBruteWfTileSubs;                             \
+        const uint32_t nt_ = min(kBruteWfTileSubs, n_sub - (t) * kBruteWfTileSubs);                     \
+        RT_BRUTE_STORE1(0u, r0) RT_BRUTE_STORE1(1u, r1) RT_BRUTE_STORE1(2u, r2) RT_BRUTE_STORE1(3u, r3) \
+    }
                 if (n_tiles) {
-                    load_tile(0u);
-                    store_tile(0u);
+                    RT_BRUTE_LOAD_TILE(0u)
+                    RT_BRUTE_STORE_TILE(0u)
                 }
                 for (uint32_t t = 0; t < n_tiles; ++t) {
                     __syncthreads();  // tile t stored; every reader of tile t - 1's buffer done
                     const uint32_t nt = min(kBruteWfTileSubs, n_sub - t * kBruteWfTileSubs);
                     if (tid == 0) streamed += nt;
                     const bool more = t + 1u < n_tiles;
-                    if (more) load_tile(t + 1u);  // in flight during the tests
-                    if (in_obj) {
+                    if (more) RT_BRUTE_LOAD_TILE(t + 1u)  // in flight during the tests
+                    if (any_in) {
                         const float4* tile = reinterpret_cast<const float4*>(l_tile + (size_t)(t & 1u) * 2u * kBruteWfTileSubs);
-                        // groups of kBruteGroup boxes: the box tests of a group issue together (their
-                        // LDS reads in flight at once), then the hit sub-objects' triangles in order
-                        uint32_t k = 0;
-                        for (; k + kBruteGroup <= nt; k += kBruteGroup) {
-                            RT_ISA_MARK("brute_box");
-                            bool any = false;
+                        // A hit box's triangles are tested later, not in the box loop: their loads from
+                        // global memory would stall the wave once per hit group. Each ray appends the
+                        // tile-local indices of the boxes it enters to its list (LDS, in sweep order);
+                        // the lists are drained -- each lane its own entries in order, all lanes' loads
+                        // in flight together -- at the end of the tile, or when a list is full. A ray's
+                        // triangle tests keep their order, and the box tests do not read `closest`.
+                        uint32_t cnt[kBruteRays];
 #pragma unroll
-                            for (uint32_t j = 0; j < kBruteGroup; ++j)  // broadcast reads
-                                any |= ray_in_box4(o, inv, tile[2u * (k + j)], tile[2u * (k + j) + 1u]);
-                            if (any) {  // (rare) the group's boxes again, one at a time, in order
-                                for (uint32_t j = 0; j < kBruteGroup; ++j) {
-                                    const float4 lo = tile[2u * (k + j)], hi = tile[2u * (k + j) + 1u];
-                                    if (!ray_in_box4(o, inv, lo, hi)) continue;
-                                    brute_sub_triangles(ka, o, d, __float_as_uint(lo.w), __float_as_uint(hi.w), oi,
-                                                        closest, ts.tri);
+                        for (uint32_t k = 0; k < kBruteRays; ++k) cnt[k] = 0u;
+                        auto drain = [&]() {
+#pragma unroll
+                            for (uint32_t k = 0; k < kBruteRays; ++k) {
+                                for (uint32_t e = 0; __builtin_amdgcn_ballot_w64(e < cnt[k]) != 0ull; ++e) {
+                                    if (e < cnt[k]) {
+                                        const uint32_t j = l_hits[(k * kBruteHits + e) * kBruteThreads + tid];
+                                        const float4 lo = tile[2u * j], hi = tile[2u * j + 1u];
+                                        brute_sub_triangles(ka, o[k], d[k], __float_as_uint(lo.w), __float_as_uint(hi.w),
+                                                            oi, closest[k], tri[k]);
+                                    }
                                 }
+                                cnt[k] = 0u;
+                            }
+                        };
+                        // groups of kBruteGroup boxes: the group's LDS reads in flight at once
+                        uint32_t j0 = 0;
+                        for (; j0 + kBruteGroup <= nt; j0 += kBruteGroup) {
+                            RT_ISA_MARK("brute_box");
+                            uint32_t bits[kBruteRays];
+                            uint32_t any = 0u;
+#pragma unroll
+                            for (uint32_t k = 0; k < kBruteRays; ++k) bits[k] = 0u;
+#pragma unroll
+                            for (uint32_t j = 0; j < kBruteGroup; ++j) {  // broadcast reads
+                                const float4 lo = tile[2u * (j0 + j)], hi = tile[2u * (j0 + j) + 1u];
+#pragma unroll
+                                for (uint32_t k = 0; k < kBruteRays; ++k)
+                                    bits[k] |= (in_obj[k] & ray_in_box4(o[k], inv[k], lo, hi)) ? 1u << j : 0u;
+                            }
+#pragma unroll
+                            for (uint32_t k = 0; k < kBruteRays; ++k) any |= bits[k];
+                            if (any) {  // (rare) append the hit boxes, in order
+                                bool full = false;
+#pragma unroll
+                                for (uint32_t k = 0; k < kBruteRays; ++k) {
+                                    while (bits[k]) {
+                                        const uint32_t j = __builtin_ctz(bits[k]);
+                                        bits[k] &= bits[k] - 1u;
+                                        l_hits[(k * kBruteHits + cnt[k]) * kBruteThreads + tid] = (uint16_t)(j0 + j);
+                                        cnt[k] += 1u;
+                                    }
+                                    full |= cnt[k] + kBruteGroup > kBruteHits;  // the next group might not fit
+                                }
+                                if (__builtin_amdgcn_ballot_w64(full) != 0ull) drain();
                             }
                         }
-                        for (; k < nt; ++k) {
-                            const float4 lo = tile[2u * k], hi = tile[2u * k + 1u];
-                            if (!ray_in_box4(o, inv, lo, hi)) continue;
-                            brute_sub_triangles(ka, o, d, __float_as_uint(lo.w), __float_as_uint(hi.w), oi, closest, ts.tri);
+                        for (; j0 < nt; ++j0) {  // (a tile of fewer than kBruteGroup-aligned boxes)
+                            const float4 lo = tile[2u * j0], hi = tile[2u * j0 + 1u];
+#pragma unroll
+                            for (uint32_t k = 0; k < kBruteRays; ++k) {
+                                if (in_obj[k] && ray_in_box4(o[k], inv[k], lo, hi)) {
+                                    l_hits[(k * kBruteHits + cnt[k]) * kBruteThreads + tid] = (uint16_t)j0;
+                                    cnt[k] += 1u;
+                                }
+                            }
+                            bool full = false;
+#pragma unroll
+                            for (uint32_t k = 0; k < kBruteRays; ++k) full |= cnt[k] + 1u > kBruteHits;
+                            if (__builtin_amdgcn_ballot_w64(full) != 0ull) drain();
                         }
+                        drain();
                     }
-                    if (more) store_tile(t + 1u);
+                    if (more) RT_BRUTE_STORE_TILE(t + 1u)
                 }
+#undef RT_BRUTE_LOAD1
+#undef RT_BRUTE_LOAD_TILE
+#undef RT_BRUTE_STORE1
+#undef RT_BRUTE_STORE_TILE
             }
         }
-        bool done = valid && !alive;  // bounces == 0: the path ends untraced
-        if (alive) {
-            ++rays;
-            const Hit h = trace_end<kTris>(sv, ka, o, d, ts);
-            done = shade<true>(sv, ka, p, h);
-        }
-        const bool cont = alive && !done;
-        if (cont) {
-            pl0[s] = make_float4(p.o.x, p.o.y, p.o.z, __uint_as_float(p.seed));
-            pl1[s] = make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.bounce));
-            pl2[s] = make_float4(p.light.x, p.light.y, p.light.z, p.light.w);
-            pl3[s] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.contrib.w);
-        }
-        // the live slots to the next level's queue (wave-aggregated)
-        const uint64_t m = __ballot(cont);
-        if (m) {
-            const uint32_t lane = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            uint32_t base = 0u;
-            if ((tid & 63u) == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(counts + level + 1u, (uint32_t)__popcll(m));
-            base = __builtin_amdgcn_readlane(base, (uint32_t)__builtin_ctzll(m));
-            if (cont) q_out[base + lane] = s;
-        }
-        if (done) {  // the sample's light (:164-178), in pass order per pixel
-            float r, g, b, al;
-            if (accumulate) {
-                float4 pix = ka.accum[index];
-                pix.x = pix.x + p.light.x;
-                pix.y = pix.y + p.light.y;
-                pix.z = pix.z + p.light.z;
-                pix.w = pix.w + p.light.w;
-                ka.accum[index] = pix;
-                const float div = (float)((ka.accumulation_index + ka.frames - 1u) * ka.compute_per_frame);
-                r = clamp01(pix.x / div);
-                g = clamp01(pix.y / div);
-                b = clamp01(pix.z / div);
-                al = clamp01(pix.w / div);
-            } else {
-                r = clamp01(p.light.x);
-                g = clamp01(p.light.y);
-                b = clamp01(p.light.z);
-                al = clamp01(p.light.w);
+        // shading, ray by ray: the path state again from HBM
+#pragma unroll
+        for (uint32_t k = 0; k < kBruteRays; ++k) {
+            const BruteSlot bs = brute_slot(ka, q_in, level, c * kBruteChunk + k * kBruteThreads + tid, n_in);
+            Path p;
+            if (bs.valid) brute_load_path(pl, n_slots, bs.s, p);
+            bool done = bs.valid && !alive[k];  // bounces == 0: the path ends untraced
+            if (alive[k]) {
+                ++rays;
+                TraceState ts;
+                ts.sph = sph[k];
+                ts.tri = tri[k];
+                const Hit h = trace_end<kTris>(sv, ka, o[k], d[k], ts);
+                done = shade<true>(sv, ka, p, h);
             }
-            if (last_pass) ka.output[index] = pack_rgba8(r, g, b, al);
+            const bool cont = alive[k] && !done;
+            if (cont) brute_store_path(pl, n_slots, bs.s, p);
+            // the live slots to the next level's queue (wave-aggregated)
+            const uint64_t m = __ballot(cont);
+            if (m) {
+                const uint32_t lane = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                uint32_t base = 0u;
+                if ((tid & 63u) == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(counts + level + 1u, (uint32_t)__popcll(m));
+                base = __builtin_amdgcn_readlane(base, (uint32_t)__builtin_ctzll(m));
+                if (cont) q_out[base + lane] = bs.s;
+            }
+            if (done) {  // the sample's light (:164-178), in pass order per pixel
+                float r, g, b, al;
+                if (accumulate) {
+                    float4 pix = ka.accum[bs.index];
+                    pix.x = pix.x + p.light.x;
+                    pix.y = pix.y + p.light.y;
+                    pix.z = pix.z + p.light.z;
+                    pix.w = pix.w + p.light.w;
+                    ka.accum[bs.index] = pix;
+                    const float div = (float)((ka.accumulation_index + ka.frames - 1u) * ka.compute_per_frame);
+                    r = clamp01(pix.x / div);
+                    g = clamp01(pix.y / div);
+                    b = clamp01(pix.z / div);
+                    al = clamp01(pix.w / div);
+                } else {
+                    r = clamp01(p.light.x);
+                    g = clamp01(p.light.y);
+                    b = clamp01(p.light.z);
+                    al = clamp01(p.light.w);
+                }
+                if (last_pass) ka.output[bs.index] = pack_rgba8(r, g, b, al);
+            }
         }
     }
     atomicAdd(&block_rays, rays);
@@ -2900,7 +3017,11 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 
 size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
 
-size_t rt_brute_wf_tile_bytes() { return 2u * (size_t)kBruteWfTileSubs * sizeof(RtSubObject); }
+size_t rt_brute_wf_tile_bytes() {
+    return 2u * (size_t)kBruteWfTileSubs * sizeof(RtSubObject) + (size_t)kBruteThreads * kBruteRays * kBruteHits * 2u;
+}
+
+uint32_t rt_brute_wf_chunk() { return kBruteChunk; }
 
 // One (pass, bounce level) of the wavefront; `blocks` workgroups stride over the level's queue.
 hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, size_t lds_bytes, uint32_t blocks, hipStream_t stream) {

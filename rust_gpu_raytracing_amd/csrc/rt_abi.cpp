@@ -60,6 +60,7 @@ hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t l
 size_t rt_brute_tile_bytes();
 hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, size_t lds_bytes, uint32_t blocks, hipStream_t stream);
 size_t rt_brute_wf_tile_bytes();
+uint32_t rt_brute_wf_chunk();
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
                              uint32_t samples, uint32_t frames, unsigned long long* clock, hipStream_t stream);
@@ -1545,8 +1546,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ka.brute_paths = ctx->d_brute_paths;
             ka.brute_queue = ctx->d_brute_queue;
             ka.brute_counts = ctx->d_brute_counts;
-            // workgroups per launch: enough for every chunk of 256 slots, at most 16 per CU
-            const uint32_t chunks = (uint32_t)((n_slots + 255u) / 256u);
+            // workgroups per launch: enough for every chunk of queue entries, at most 16 per CU
+            const uint32_t chunks = (uint32_t)((n_slots + rt_brute_wf_chunk() - 1u) / rt_brute_wf_chunk());
             const uint32_t blocks = std::min<uint32_t>(chunks, 16u * (uint32_t)std::max<int>(1, (int)ctx->n_cu));
             for (uint64_t pass = 0; pass < passes; ++pass)
                 for (uint32_t level = 0; level < std::max(1u, bounces); ++level) {
