@@ -962,6 +962,18 @@ __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs&
 template <int kMode, bool kTris, bool kWide>
 constexpr bool kCoopLeaves = RT_COOP_LEAVES && kTris && !kWide && kMode <= 1;
 
+// Refill from a per-tile prologue: when a wave takes a tile, lane l computes slot l's pixel,
+// camera ray and the sample's start (start_sample: seed, jittered direction) with the whole wave
+// active, and a refilling lane fetches its slot's values with ds_bpermute instead of computing
+// them alone (RT_REFILL_PREP=1 builds; sphere-only instances). Measured slower, so off: C2
+// 0.2862 -> 0.3172 ms per frame, C1 0.0186 -> 0.0194 (profiles/r05/refill_prep_ab_*.json): the
+// refill's per-lane arithmetic is not what its share of the wave cycles pays for.
+#ifndef RT_REFILL_PREP
+#define RT_REFILL_PREP 0
+#endif
+template <bool kTris>
+constexpr bool kRefillPrep = RT_REFILL_PREP && !kTris;
+
 // LDS written by some lanes of a wave and read by others: the wave's LDS operations complete in
 // order, so only the compiler must not move them across this point.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1757,6 +1769,30 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // (advanced per frame by the host only when accumulating, src/renderer.rs:216-235)
     // plus the sample number.
     auto random_index = [&]() { return ka.accumulation_index + (accumulate ? frame : 0u) + sample; };
+    // kRefillPrep: slot (lane id) of the wave's current tile -- its pixel index (0xffffffff:
+    // outside the image), seed and jittered direction after start_sample
+    float prep_dx = 0.0f, prep_dy = 0.0f, prep_dz = 0.0f;
+    uint32_t prep_seed = 0u, prep_index = 0xffffffffu;
+    auto prep_tile = [&](uint32_t t, uint32_t t_frame) {  // whole wave
+        if constexpr (kRefillPrep<kTris>) {
+            const uint32_t slot = lane_id_here();
+            const uint32_t gt = t * ka.world_size + ka.rank;
+            const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);
+            const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
+            prep_index = 0xffffffffu;
+            if (t < ka.owned_tiles && x < ka.width && y < ka.height) {
+                const uint32_t idx = y * ka.width + x;
+                Path q;
+                start_sample(ka, idx, ka.accumulation_index + (accumulate ? t_frame : 0u),
+                             pixel_ray(ka, l_cam, idx, x, y), q);
+                prep_index = idx;
+                prep_seed = q.seed;
+                prep_dx = q.d.x;
+                prep_dy = q.d.y;
+                prep_dz = q.d.z;
+            }
+        }
+    };
     // A sample just started: with the primary pre-pass (rt_primary_kernel) its first
     // segment's trace result is read back and the lane goes straight to shading it;
     // else the trace starts at the next setup step.
@@ -1843,6 +1879,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     uint32_t tile_frame = 0;         // frame of the claimed unit (frame-parallel batches), wave-uniform
     uint32_t tile = unit_tile(ka, claim_tile(ka, queue), tile_frame);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
+    prep_tile(tile, tile_frame);
 #ifdef RT_DIAG
     unsigned long long iters = 0, trav_cyc = 0, steps = 0, step_lanes = 0, shade_cyc = 0, refill_cyc = 0,
                        setup_cyc = 0, leaf_cyc = 0, leaf_steps = 0;
@@ -1905,11 +1942,39 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 #endif
         // 2. Refill: idle lanes take the next pixels of the wave's tile, in slot
         // order (ballot + mbcnt = a wave-wide prefix sum over the idle lanes).
+        RT_ISA_MARK("refill");
         while (true) {
             const uint64_t need = __ballot(mode == kIdle);
             if (need == 0 || tile >= ka.owned_tiles) break;
             const uint32_t avail = 64u - next;
-            if (mode == kIdle) {
+            if constexpr (kRefillPrep<kTris>) {
+                // (the whole wave: ds_bpermute reads only from active lanes) each idle lane fetches
+                // the prologue's values of the slot it takes
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const int src = (int)(min(next + rank, 63u) * 4u);
+                const uint32_t g_index = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)prep_index);
+                const uint32_t g_seed = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)prep_seed);
+                const float g_dx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(prep_dx)));
+                const float g_dy = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(prep_dy)));
+                const float g_dz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(prep_dz)));
+                if (mode == kIdle && rank < avail && g_index != 0xffffffffu) {
+                    index = g_index;  // :148
+                    lane_tile = tile;
+                    lane_slot = next + rank;
+                    sample = 0;
+                    frame = tile_frame;
+                    if (accumulate && !frame_par) pix = ka.accum[index];  // :156
+                    // start_sample's state, computed in the tile's prologue (same operations)
+                    p.o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
+                    p.d = mk(g_dx, g_dy, g_dz);
+                    p.seed = g_seed;
+                    p.contrib = f4{1.0f, 1.0f, 1.0f, 1.0f};
+                    p.light = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                    p.bounce = 0;
+                    mode = primary_start();
+                }
+            } else if (mode == kIdle) {
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 if (rank < avail) {
@@ -1934,6 +1999,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             if (next == 64u) {
                 tile = unit_tile(ka, claim_tile(ka, queue), tile_frame);
                 next = 0;
+                prep_tile(tile, tile_frame);
 #ifdef RT_DIAG_TAIL
                 if (tile >= ka.owned_tiles && wave_dry == 0) wave_dry = realtime();
 #endif
@@ -1954,6 +2020,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             }
         }
 #endif
+        RT_ISA_MARK("setup");
         if (mode == kSetup) {
             while (mode == kSetup && p.bounce >= ka.bounces) finish_sample();
             if (mode == kSetup) {
