@@ -361,7 +361,7 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
     if (kTris && phase == 0) {  // the accelerator layout ordered for this ray's direction octant (global walks)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
                              ((__float_as_uint(ts.inv.z) >> 31) << 2);
-        ts.node = sv.tri_q4 ? 0u : oct * ka.tri_octant_stride;  // the 4-wide walk starts at its root
+        ts.node = (kQ4Built && sv.tri_q4) ? 0u : oct * ka.tri_octant_stride;  // the 4-wide walk starts at its root
         ts.sp = 0u;
     }
     if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
@@ -766,7 +766,7 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
     if (ts.pending != kNoLeaf) return;
     if (kTris && ts.phase == 0) {
         if (kWide ? (ts.node != kWideNone || ts.sp != 0u)
-                  : (sv.tri_q4 && ts.sp != kQ4Binary) ? (ts.node != kQ4None || ts.sp != 0u) : (ts.node < ka.tri_nodes))
+                  : (kQ4Built && sv.tri_q4 && ts.sp != kQ4Binary) ? (ts.node != kQ4None || ts.sp != 0u) : (ts.node < ka.tri_nodes))
             return;
 #ifdef RT_DIAG_TAIL
         if (ts.nan_hit) atomicAdd(ka.diag + 6, 1ull);
@@ -832,7 +832,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
         return;
     }
     if constexpr (kTris && !kWide) {
-        if (tri && sv.tri_q4 && ts.sp != kQ4Binary) {
+        if (kQ4Built && tri && sv.tri_q4 && ts.sp != kQ4Binary) {
             q4_node_step(sv, ka, d, ts);
             return;
         }
@@ -1650,7 +1650,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
                 sv.qsz = g1.z;
             }
         }
-        if (ka.tri_q4) {  // the 4-wide walk, on the same grid (both from the binary root, tri_qgrid)
+        if (kQ4Built && ka.tri_q4) {  // the 4-wide walk, on the same grid (both from the binary root, tri_qgrid)
             const float4 g0 = ka.tri_q4grid[0], g1 = ka.tri_q4grid[1];
             if (g0.w != 0.0f) {
                 sv.tri_q4 = ka.tri_q4;
@@ -2916,7 +2916,7 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
     // the 4-wide packet walk (global-memory accelerators): its grid, and this wave's stack
     uint32_t* q4_wstack = nullptr;
     if constexpr (kTris && kMode <= 1) {
-        if (ka.tri_q4 && ka.lds_q4packet_offset) {
+        if (kQ4Built && ka.tri_q4 && ka.lds_q4packet_offset) {
             const float4 g0 = ka.tri_q4grid[0], g1 = ka.tri_q4grid[1];
             if (g0.w != 0.0f) {
                 sv.tri_q4 = ka.tri_q4;
@@ -2963,7 +2963,7 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
         TraceState ts;
         trace_begin<kTris>(sv, ka, o, d, ts);  // brute-force spheres, slab constants, phase
         if constexpr (kTris) {
-            if (kMode <= 1 && ts.phase == 0 && sv.tri_q4) {
+            if (kQ4Built && kMode <= 1 && ts.phase == 0 && sv.tri_q4) {
                 q4_packet_walk(sv, ka, o, d, ts, valid, q4_wstack);
                 if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
                 ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;

@@ -1000,7 +1000,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         env = std::getenv("RT_TRI_LEAFCERT_LDS");
         if (env) ctx->use_leafcert_lds = env[0] == '1';
         env = std::getenv("RT_TRI_Q4");
-        if (env) ctx->use_q4 = env[0] != '0';
+        if (env) ctx->use_q4 = kQ4Built && env[0] != '0';
         env = std::getenv("RT_COOP_LEAVES");
         if (env) ctx->use_coop_leaves = env[0] != '0';
         env = std::getenv("RT_TRI_LDS_COMPACT");

@@ -41,6 +41,13 @@ struct TriQ4Node {
 };
 static_assert(sizeof(TriQ4Node) == 64, "4-wide node = 64 B");
 
+// Build switch: the 4-wide walk's code is compiled in only with -DRT_Q4=1 (its instructions and
+// registers slowed the default binary walk even when switched off at run time: DESIGN.md §5.3e).
+#ifndef RT_Q4
+#define RT_Q4 0
+#endif
+constexpr bool kQ4Built = RT_Q4 != 0;
+
 constexpr uint32_t kQ4Empty = 0xffffffffu;
 constexpr uint32_t kQ4Leaf = 0x80000000u;
 constexpr uint32_t kQ4MaxPrims = 1u << 20;  // leaf records a stack entry can name (larger scenes: binary walk)

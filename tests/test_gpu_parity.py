@@ -903,18 +903,31 @@ def test_gpu_triangle_accelerators(gpu, oracle_lib, monkeypatch, config, kw, wid
                                        ("c3_chess", dict(env_size=(512, 256)))])
 def test_gpu_global_walk_variants(gpu, oracle_lib, monkeypatch, config, kw, env):
     """The walks from global memory (scene not staged in LDS: RT_LDS_MODE=1): the 4-wide
-    quantized accelerator with its per-lane LDS stack (tri_q4.h, RT_TRI_Q4=1; with the primary
-    pre-pass's packet walk, without pruning, at 256 threads), and per-lane leaf tests instead of
-    the cooperative leaf batches (RT_COOP_LEAVES=0): the oracle's images and ray counts."""
+    quantized accelerator with its per-lane LDS stack (tri_q4.h, RT_TRI_Q4=1 in a -DRT_Q4=1
+    build -- skipped otherwise; with the primary pre-pass's packet walk, without pruning, at 256
+    threads), and per-lane leaf tests instead of the cooperative leaf batches
+    (RT_COOP_LEAVES=0): the oracle's images and ray counts."""
     monkeypatch.setenv("RT_LDS_MODE", "1")
+    scene, bounces = build_config(config, width=96, height=64, **kw)
+
+    def lds_bytes():
+        with Renderer(scene) as r:
+            r.compute_frame(bounces)
+            cfg = r.launch_config()
+            assert cfg["scene_in_lds"] <= 1
+            return cfg["lds_bytes"]
+
+    if env.get("RT_TRI_Q4") == "1":
+        # the 4-wide walk is a build switch (-DRT_Q4=1, off in the product build); its per-lane
+        # stacks add to the launch's LDS image when it runs
+        base = lds_bytes()
+        monkeypatch.setenv("RT_TRI_Q4", "1")
+        if lds_bytes() == base:
+            pytest.skip("library built without -DRT_Q4=1: no 4-wide walk to test")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    scene, bounces = build_config(config, width=96, height=64, **kw)
     acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
     assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
-    with Renderer(scene) as r:
-        r.compute_frame(bounces)
-        assert r.launch_config()["scene_in_lds"] <= 1
 
 
 def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
