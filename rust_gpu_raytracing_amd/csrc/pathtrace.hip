@@ -823,39 +823,35 @@ template <int kMode>
 constexpr bool kCertWalk = kMode <= 1 || RT_LEAFCERT_LDS == 1;
 
 
-// kCert: the walk reads leaf certificates (tri_leaf_skips) when ka.tri_leafcert is set.
-template <bool kTris, bool kWide = false, bool kCert = true>
-__device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
-    const bool tri = kTris && ts.phase == 0;
-    if (kWide && tri) {
-        wide_node_step(sv, ts);
-        return;
-    }
-    if constexpr (kTris && !kWide) {
-        if (kQ4Built && tri && sv.tri_q4 && ts.sp != kQ4Binary) {
-            q4_node_step(sv, ka, d, ts);
-            return;
-        }
-    }
-    if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
-        return;  // walk over, a leaf still deferred
-    float4 lo, hi;
-    if (kTris && !kWide && tri && sv.tri_q) {
-        // 16-B quantized node: the box decoded exactly (a superset of the 32-B node's box)
-        const uint4 q = sv.tri_q[ts.node];
-        lo = make_float4(fmaf((float)(q.x & 0xffffu), sv.qsx, sv.qox), fmaf((float)(q.x >> 16), sv.qsy, sv.qoy),
-                         fmaf((float)(q.y & 0xffffu), sv.qsz, sv.qoz), 0.0f);
-        hi = make_float4(fmaf((float)(q.y >> 16), sv.qsx, sv.qox), fmaf((float)(q.z & 0xffffu), sv.qsy, sv.qoy),
-                         fmaf((float)(q.z >> 16), sv.qsz, sv.qoz), 0.0f);
-        const bool is_leaf = (q.w & 0x80000000u) != 0u;
-        // a leaf's skip link is node + 1 (pre-order), or the end for a layout's last leaf
-        lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : ts.node + 1u) : q.w);
-        hi.w = __uint_as_float(is_leaf ? (q.w & 0xffffffu) : 0xffffffffu);
-    } else {
-        const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
-        lo = nodes[2u * ts.node];
-        hi = nodes[2u * ts.node + 1u];
-    }
+// Node pairs (walks from global memory over the 16-B quantized nodes): a step loads node n and
+// node n + 1 together (adjacent 16 B, one round trip) and, when the walk's next node is n + 1 --
+// after a leaf, hit or not (its skip link is n + 1), or after entering an internal node (its
+// first child) -- visits it in the same step with the data it already has. The visit order and
+// every test are unchanged; a descent takes one memory round trip per two nodes. Measured on C5
+// (one process): 15.63 ms per frame at the default 5 steps per check (the unrolled pairs cost
+// more than they save), 13.75 at 3, against 13.88 without pairs -- within noise, so off.
+#ifndef RT_NODE_PAIRS
+#define RT_NODE_PAIRS 0
+#endif
+
+// A 16-B quantized node decoded (tri_qnode.h): the box exactly (a superset of the 32-B node's
+// box), lo.w = the skip link (a leaf's: node + 1, or the end), hi.w = the leaf record or none.
+__device__ __forceinline__ void qnode_decode(const SceneView& sv, uint4 q, uint32_t node, float4& lo, float4& hi) {
+    lo = make_float4(fmaf((float)(q.x & 0xffffu), sv.qsx, sv.qox), fmaf((float)(q.x >> 16), sv.qsy, sv.qoy),
+                     fmaf((float)(q.y & 0xffffu), sv.qsz, sv.qoz), 0.0f);
+    hi = make_float4(fmaf((float)(q.y >> 16), sv.qsx, sv.qox), fmaf((float)(q.z & 0xffffu), sv.qsy, sv.qoy),
+                     fmaf((float)(q.z >> 16), sv.qsz, sv.qoz), 0.0f);
+    const bool is_leaf = (q.w & 0x80000000u) != 0u;
+    // a leaf's skip link is node + 1 (pre-order), or the end for a layout's last leaf
+    lo.w = __uint_as_float(is_leaf ? ((q.w & kTriQLastLeaf) ? kTriWalkEnd : node + 1u) : q.w);
+    hi.w = __uint_as_float(is_leaf ? (q.w & 0xffffffu) : 0xffffffffu);
+}
+
+// One node's visit, given its box and links: the box test, the deferred leaf or the sphere
+// group, the next node.
+template <bool kTris, bool kWide, bool kCert>
+__device__ __forceinline__ void node_visit(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
+                                           bool tri, float4 lo, float4 hi) {
     float near_t, far_t;
     if (!kTris && ka.sphere_boxes_ordered)  // (near, far) corners: no min/max per axis (6 VALU per node step)
         slab_hit_ordered(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
@@ -915,6 +911,43 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
         ts.pending = (leaf & 0xffffffu) | (skip << 24);
     }
     ts.node = (hit && !at_leaf) ? ts.node + 1u : __float_as_uint(lo.w);
+}
+
+// kCert: the walk reads leaf certificates (tri_leaf_skips) when ka.tri_leafcert is set.
+template <bool kTris, bool kWide = false, bool kCert = true>
+__device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
+    const bool tri = kTris && ts.phase == 0;
+    if (kWide && tri) {
+        wide_node_step(sv, ts);
+        return;
+    }
+    if constexpr (kTris && !kWide) {
+        if (kQ4Built && tri && sv.tri_q4 && ts.sp != kQ4Binary) {
+            q4_node_step(sv, ka, d, ts);
+            return;
+        }
+    }
+    if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
+        return;  // walk over, a leaf still deferred
+    float4 lo, hi;
+    if (kTris && !kWide && tri && sv.tri_q) {
+        const uint32_t n = ts.node;
+        const uint4 q = sv.tri_q[n];
+        if (RT_NODE_PAIRS && n + 1u < ka.tri_nodes) {
+            const uint4 q1 = sv.tri_q[n + 1u];  // with node n: the same round trip
+            qnode_decode(sv, q, n, lo, hi);
+            node_visit<kTris, kWide, kCert>(sv, ka, o, d, ts, tri, lo, hi);
+            if (ts.node != n + 1u) return;  // a skip (or blocked at a leaf): node n + 1 is not next
+            qnode_decode(sv, q1, n + 1u, lo, hi);
+        } else {
+            qnode_decode(sv, q, n, lo, hi);
+        }
+    } else {
+        const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
+        lo = nodes[2u * ts.node];
+        hi = nodes[2u * ts.node + 1u];
+    }
+    node_visit<kTris, kWide, kCert>(sv, ka, o, d, ts, tri, lo, hi);
 }
 
 template <bool kTris, bool kWide = false, bool kLazySub = false>
@@ -2459,6 +2492,12 @@ constexpr uint32_t kBruteChunk = kBruteRays * kBruteThreads;  // queue entries p
 #endif
 constexpr uint32_t kBruteHits = RT_BRUTE_HITS;
 static_assert(kBruteHits >= kBruteGroup, "a group's hits fit a drained list");
+// The sub-object records through the scalar cache instead of LDS tiles: each wave streams them
+// on its own (wave-uniform s_load), no tile barrier (RT_BRUTE_STREAM).
+#ifndef RT_BRUTE_STREAM
+#define RT_BRUTE_STREAM 0
+#endif
+constexpr bool kBruteStream = RT_BRUTE_STREAM != 0;
 
 // One pixel slot of the wavefront: its pixel and whether it is inside the image.
 struct BruteSlot {
@@ -2563,7 +2602,88 @@ __global__ void __launch_bounds__(kBruteThreads, RT_BRUTE_WAVES) rt_brute_wf_ker
             }
         }
         // check_triangles (:422-517): objects in order, their sub-objects through the LDS tiles
-        if constexpr (kTris) {
+        // (kBruteStream: through the scalar cache, wave by wave)
+        if constexpr (kTris && kBruteStream) {
+            static_assert(kBruteRays == 1, "the streamed sweep carries one ray per thread");
+            uint32_t* l_hits32 = reinterpret_cast<uint32_t*>(l_tile);  // kBruteHits entries per thread
+            typedef float rt_v4 __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(4))) const rt_v4 rt_cf4;  // scalar loads (wave-uniform)
+            auto ldc = [](rt_cf4* p_, uint32_t i_) {
+                const rt_v4 v_ = p_[i_];
+                return make_float4(v_.x, v_.y, v_.z, v_.w);
+            };
+            for (uint32_t oi = 0; oi < ka.object_count; ++oi) {
+                const RtObject& ob = sv.obj[oi];
+                const bool in_obj = alive[0] && ray_in_bounds(o[0], inv[0], ob.min_bounds, ob.max_bounds);
+                if (__ballot(in_obj) == 0ull) continue;  // no lane of the wave enters the object
+                const uint32_t first = ob.first_sub_object_index, n_sub = ob.sub_object_count;
+                const uint32_t last_sub = ka.sub_object_count - 1u;
+                rt_cf4* recs = (rt_cf4*)(const void*)ka.sub_objects;
+                if (tid == 0) streamed += n_sub;
+                uint32_t cnt = 0u;
+                // the entered boxes' triangles, each lane its own list in order (as the tiled sweep)
+                auto drain = [&]() {
+                    for (uint32_t e = 0; __builtin_amdgcn_ballot_w64(e < cnt) != 0ull; ++e) {
+                        if (e < cnt) {
+                            const uint32_t si = l_hits32[e * kBruteThreads + tid];
+                            const float4 lo = reinterpret_cast<const float4*>(ka.sub_objects)[2u * si];
+                            const float4 hi = reinterpret_cast<const float4*>(ka.sub_objects)[2u * si + 1u];
+                            brute_sub_triangles(ka, o[0], d[0], __float_as_uint(lo.w), __float_as_uint(hi.w), oi,
+                                                closest[0], tri[0]);
+                        }
+                    }
+                    cnt = 0u;
+                };
+                // groups of 4 records: the next group's scalar loads in flight while this one is tested
+                float4 l0, l1, l2, l3, h0, h1, h2, h3;
+#define RT_BRUTE_SLOAD(j_)                                                                              \
+    {                                                                                                   \
+        const uint32_t s0_ = 2u * min(first + (j_), last_sub), s1_ = 2u * min(first + (j_) + 1u, last_sub); \
+        const uint32_t s2_ = 2u * min(first + (j_) + 2u, last_sub), s3_ = 2u * min(first + (j_) + 3u, last_sub); \
+        n0 = ldc(recs, s0_); m0 = ldc(recs, s0_ + 1u); n1 = ldc(recs, s1_); m1 = ldc(recs, s1_ + 1u);   \
+        n2 = ldc(recs, s2_); m2 = ldc(recs, s2_ + 1u); n3 = ldc(recs, s3_); m3 = ldc(recs, s3_ + 1u);   \
+    }
+                {
+                    float4 n0, n1, n2, n3, m0, m1, m2, m3;
+                    RT_BRUTE_SLOAD(0u)
+                    l0 = n0; l1 = n1; l2 = n2; l3 = n3; h0 = m0; h1 = m1; h2 = m2; h3 = m3;
+                }
+                uint32_t j0 = 0;
+                for (; j0 + 4u <= n_sub; j0 += 4u) {
+                    RT_ISA_MARK("brute_box");
+                    float4 n0, n1, n2, n3, m0, m1, m2, m3;
+                    RT_BRUTE_SLOAD(j0 + 4u)  // (clamped: past the end it rereads the last record)
+                    uint32_t bits = 0u;
+                    if (in_obj) {
+                        bits |= ray_in_box4(o[0], inv[0], l0, h0) ? 1u : 0u;
+                        bits |= ray_in_box4(o[0], inv[0], l1, h1) ? 2u : 0u;
+                        bits |= ray_in_box4(o[0], inv[0], l2, h2) ? 4u : 0u;
+                        bits |= ray_in_box4(o[0], inv[0], l3, h3) ? 8u : 0u;
+                    }
+                    if (__ballot(bits != 0u) != 0ull) {  // (rare) queue the entered boxes, in order
+                        while (bits) {
+                            const uint32_t j = __builtin_ctz(bits);
+                            bits &= bits - 1u;
+                            l_hits32[cnt * kBruteThreads + tid] = first + j0 + j;
+                            cnt += 1u;
+                        }
+                        if (__ballot(cnt + 4u > kBruteHits) != 0ull) drain();
+                    }
+                    l0 = n0; l1 = n1; l2 = n2; l3 = n3; h0 = m0; h1 = m1; h2 = m2; h3 = m3;
+                }
+#undef RT_BRUTE_SLOAD
+                for (; j0 < n_sub; ++j0) {  // the last 1-3 records
+                    const uint32_t si = min(first + j0, last_sub);
+                    const float4 lo = ldc(recs, 2u * si), hi = ldc(recs, 2u * si + 1u);
+                    if (in_obj && ray_in_box4(o[0], inv[0], lo, hi)) {
+                        l_hits32[cnt * kBruteThreads + tid] = si;
+                        cnt += 1u;
+                    }
+                    if (__ballot(cnt + 1u > kBruteHits) != 0ull) drain();
+                }
+                drain();
+            }
+        } else if constexpr (kTris) {
             for (uint32_t oi = 0; oi < ka.object_count; ++oi) {
                 const RtObject& ob = sv.obj[oi];
                 bool in_obj[kBruteRays];
@@ -3085,6 +3205,7 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
 
 size_t rt_brute_wf_tile_bytes() {
+    if (kBruteStream) return (size_t)kBruteThreads * kBruteHits * 4u;  // the hit lists only (u32 entries)
     return 2u * (size_t)kBruteWfTileSubs * sizeof(RtSubObject) + (size_t)kBruteThreads * kBruteRays * kBruteHits * 2u;
 }
 
