@@ -894,19 +894,18 @@ def test_gpu_triangle_accelerators(gpu, oracle_lib, monkeypatch, config, kw, wid
 
 @pytest.mark.parametrize("env", [
     {"RT_TRI_Q4": "1"},
-    {"RT_TRI_Q4": "1", "RT_PRIMARY_PASS": "1"},
-    {"RT_TRI_Q4": "1", "RT_TRI_PRUNE": "0"},
     {"RT_COOP_LEAVES": "0"},
-    {"RT_TRI_Q4": "1", "RT_BLOCK_THREADS": "256"},
+    {"RT_BLOCK_THREADS": "256"},
+    {"RT_TRI_PRUNE": "0", "RT_PRIMARY_PASS": "0"},
 ])
 @pytest.mark.parametrize("config,kw", [("c4_mixed", dict(env_size=(256, 128))), ("c5_heightfield", dict(nx=60, nz=30)),
                                        ("c3_chess", dict(env_size=(512, 256)))])
 def test_gpu_global_walk_variants(gpu, oracle_lib, monkeypatch, config, kw, env):
-    """The walks from global memory (scene not staged in LDS: RT_LDS_MODE=1): the 4-wide
-    quantized accelerator with its per-lane LDS stack (tri_q4.h, RT_TRI_Q4=1 in a -DRT_Q4=1
-    build -- skipped otherwise; with the primary pre-pass's packet walk, without pruning, at 256
-    threads), and per-lane leaf tests instead of the cooperative leaf batches
-    (RT_COOP_LEAVES=0): the oracle's images and ray counts."""
+    """The walks from global memory (scene not staged in LDS: RT_LDS_MODE=1): per-lane leaf tests
+    instead of the cooperative leaf batches (RT_COOP_LEAVES=0), 256-thread workgroups, box
+    culling without the primary pre-pass, and the 4-wide quantized accelerator with its per-lane
+    LDS stack (tri_q4.h, RT_TRI_Q4=1 in a -DRT_Q4=1 build -- skipped otherwise): the oracle's
+    images and ray counts."""
     monkeypatch.setenv("RT_LDS_MODE", "1")
     scene, bounces = build_config(config, width=96, height=64, **kw)
 
