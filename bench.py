@@ -58,7 +58,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # 16 lanes x 2.4 GHz (a wave64 instruction issues over 4 cycles of a SIMD16)
 VALU_LANE_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 KERNEL_NAMES = {"path": "rt_pathtrace_kernel", "primary": "rt_primary_kernel", "resolve": "rt_resolve_frames_kernel",
-                "brute": "rt_brute_kernel"}
+                "brute": "rt_brute_wf_kernel"}
 # The reference computes a frame every >= 0.8 ms and displays every >= 5 ms
 # (src/main.rs:88-92, 365-375): about 6 computed frames per displayed image.
 DISPLAY_CADENCE_FRAMES = 6
@@ -201,9 +201,10 @@ def main() -> int:
                     help="N>1 route: torch = one process per GPU (torch.distributed.run, RCCL via ProcessGroupNCCL); "
                          "group = one process driving --gpus devices through the C ABI (rt_create_multi, "
                          "rt_gather_frame: RCCL send/recv), the Rust host's route")
-    ap.add_argument("--brute-force", action="store_true",
-                    help="the reference's own sweeps, LDS-tiled (rt_set_brute_force; BASELINE config 5's stress "
-                         "mode) instead of the acceleration structures")
+    ap.add_argument("--brute-force", nargs="?", const="tiled", default=None, choices=["tiled", "stream"],
+                    help="the reference's own sweeps (rt_set_brute_force; BASELINE config 5's stress mode) instead "
+                         "of the acceleration structures: the sub-object records LDS-tiled (default) or streamed "
+                         "through the scalar cache ('stream', rt_set_brute_force(ctx, 2))")
     ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
                     help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N, steps)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
@@ -270,7 +271,7 @@ def main() -> int:
             bpr = int(r._lib.rt_bytes_per_row(width, 256))
             display = (torch.zeros(height * bpr, dtype=torch.uint8, device=torch.device("cuda", device)), bpr)
         if args.brute_force:
-            r.set_brute_force(True)
+            r.set_brute_force(2 if args.brute_force == "stream" else 1)
 
         def barrier_sync():
             r.synchronize()
@@ -522,7 +523,8 @@ def main() -> int:
         eff_launch_s = m["t_render"] / max(n_timed, 1)  # wall time per launch: overlapped launches pipeline
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
         if args.brute_force:
-            workload += ", brute-force LDS-tiled sweeps"
+            workload += (", brute-force sweeps streamed through the scalar cache" if args.brute_force == "stream"
+                         else ", brute-force LDS-tiled sweeps")
         # a non-default triangle walk is another workload for the PMC table (its counters are
         # not the default walk's): RT_TRI_PRUNE 0 = box culling, 2 = the round-3 slack (not exact)
         prune = os.environ.get("RT_TRI_PRUNE", "1")

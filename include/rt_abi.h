@@ -304,15 +304,18 @@ RT_API int rt_ray_count(rt_ctx* ctx, uint64_t* out);
 RT_API int rt_reset_ray_count(rt_ctx* ctx);
 
 /* Brute-force mode (BASELINE.json config 5, "brute-force LDS-tiled intersect
- * stress"): with enable != 0 later launches run the reference's own sweeps --
+ * stress"): with enable = 1 later launches run the reference's own sweeps --
  * every sphere (check_spheres, compute_shader.wgsl:355-404), every object's and
  * sub-object's box and the triangles of those hit (check_triangles, :422-517) --
- * with no acceleration structure: one thread per pixel, each workgroup streaming
- * the sub-object records through LDS in tiles and testing them with broadcast
- * reads. Same results, bit for bit, as the accelerated default (0). The scene's
- * spheres, materials and objects must fit in LDS. rt_streamed_bytes: sub-object
- * bytes those launches streamed (the tile-streaming term of SURVEY §8d), since
- * creation or the last rt_reset_ray_count. Synchronous. */
+ * with no acceleration structure: a wavefront over the live paths, each
+ * workgroup streaming the sub-object records through LDS in tiles and testing
+ * them with broadcast reads. enable = 2 (ABI 11): the same sweeps with the
+ * records streamed through the scalar cache by each wave (no LDS tile). Same
+ * results, bit for bit, as the accelerated default (0); other values are
+ * RT_E_INVALID. The scene's spheres, materials and objects must fit in LDS.
+ * rt_streamed_bytes: sub-object bytes those launches streamed (the
+ * tile-streaming term of SURVEY §8d), since creation or the last
+ * rt_reset_ray_count. Synchronous. */
 RT_API int rt_set_brute_force(rt_ctx* ctx, int enable);
 RT_API int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out);
 

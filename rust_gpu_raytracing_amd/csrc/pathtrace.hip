@@ -2492,12 +2492,13 @@ constexpr uint32_t kBruteChunk = kBruteRays * kBruteThreads;  // queue entries p
 #endif
 constexpr uint32_t kBruteHits = RT_BRUTE_HITS;
 static_assert(kBruteHits >= kBruteGroup, "a group's hits fit a drained list");
-// The sub-object records through the scalar cache instead of LDS tiles: each wave streams them
-// on its own (wave-uniform s_load), no tile barrier (RT_BRUTE_STREAM).
-#ifndef RT_BRUTE_STREAM
-#define RT_BRUTE_STREAM 0
+// kStream instances (rt_set_brute_force(ctx, 2)): the sub-object records through the scalar
+// cache instead of LDS tiles -- each wave streams them on its own (wave-uniform s_load), no tile
+// barrier, no LDS but the hit lists, so the occupancy is set by registers (RT_BRUTE_STREAM_WAVES
+// waves per SIMD requested; the shading code spills a little at 8).
+#ifndef RT_BRUTE_STREAM_WAVES
+#define RT_BRUTE_STREAM_WAVES 8
 #endif
-constexpr bool kBruteStream = RT_BRUTE_STREAM != 0;
 
 // One pixel slot of the wavefront: its pixel and whether it is inside the image.
 struct BruteSlot {
@@ -2537,8 +2538,9 @@ __device__ __forceinline__ void brute_store_path(float4* pl, uint32_t n_slots, u
 #ifndef RT_BRUTE_WAVES
 #define RT_BRUTE_WAVES 4
 #endif
-template <bool kTris>
-__global__ void __launch_bounds__(kBruteThreads, RT_BRUTE_WAVES) rt_brute_wf_kernel(KernelArgs ka) {
+template <bool kTris, bool kStream>
+__global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES : RT_BRUTE_WAVES)
+    rt_brute_wf_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
     const uint32_t tid = threadIdx.x;
@@ -2603,7 +2605,7 @@ __global__ void __launch_bounds__(kBruteThreads, RT_BRUTE_WAVES) rt_brute_wf_ker
         }
         // check_triangles (:422-517): objects in order, their sub-objects through the LDS tiles
         // (kBruteStream: through the scalar cache, wave by wave)
-        if constexpr (kTris && kBruteStream) {
+        if constexpr (kTris && kStream) {
             static_assert(kBruteRays == 1, "the streamed sweep carries one ray per thread");
             uint32_t* l_hits32 = reinterpret_cast<uint32_t*>(l_tile);  // kBruteHits entries per thread
             typedef float rt_v4 __attribute__((ext_vector_type(4)));
@@ -3204,26 +3206,30 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 
 size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
 
-size_t rt_brute_wf_tile_bytes() {
-    if (kBruteStream) return (size_t)kBruteThreads * kBruteHits * 4u;  // the hit lists only (u32 entries)
+size_t rt_brute_wf_tile_bytes(bool stream) {
+    if (stream) return (size_t)kBruteThreads * kBruteHits * 4u;  // the hit lists only (u32 entries)
     return 2u * (size_t)kBruteWfTileSubs * sizeof(RtSubObject) + (size_t)kBruteThreads * kBruteRays * kBruteHits * 2u;
 }
 
 uint32_t rt_brute_wf_chunk() { return kBruteChunk; }
 
 // One (pass, bounce level) of the wavefront; `blocks` workgroups stride over the level's queue.
-hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, size_t lds_bytes, uint32_t blocks, hipStream_t stream) {
+hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, bool scalar_stream, size_t lds_bytes, uint32_t blocks,
+                              hipStream_t stream) {
     if (blocks == 0) return hipSuccess;
+    const void* fn = tris ? (scalar_stream ? reinterpret_cast<const void*>(&rt_brute_wf_kernel<true, true>)
+                                           : reinterpret_cast<const void*>(&rt_brute_wf_kernel<true, false>))
+                          : reinterpret_cast<const void*>(&rt_brute_wf_kernel<false, false>);
     if (lds_bytes > 64u * 1024u) {
-        const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_wf_kernel<true>)
-                              : reinterpret_cast<const void*>(&rt_brute_wf_kernel<false>);
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return hipErrorInvalidConfiguration;
     }
-    if (tris)
-        hipLaunchKernelGGL(rt_brute_wf_kernel<true>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+    if (tris && scalar_stream)
+        hipLaunchKernelGGL((rt_brute_wf_kernel<true, true>), dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+    else if (tris)
+        hipLaunchKernelGGL((rt_brute_wf_kernel<true, false>), dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
     else
-        hipLaunchKernelGGL(rt_brute_wf_kernel<false>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
+        hipLaunchKernelGGL((rt_brute_wf_kernel<false, false>), dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
     return hipGetLastError();
 }
 

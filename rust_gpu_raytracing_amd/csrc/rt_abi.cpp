@@ -58,8 +58,9 @@ hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hi
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
 size_t rt_brute_tile_bytes();
-hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, size_t lds_bytes, uint32_t blocks, hipStream_t stream);
-size_t rt_brute_wf_tile_bytes();
+hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, bool scalar_stream, size_t lds_bytes, uint32_t blocks,
+                              hipStream_t stream);
+size_t rt_brute_wf_tile_bytes(bool scalar_stream);
 uint32_t rt_brute_wf_chunk();
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
@@ -318,8 +319,9 @@ struct rt_ctx {
     uint32_t* d_vsrc = nullptr;
     size_t wide_cap = 0, leaves_cap = 0, verts_cap = 0, vsrc_cap = 0;
     uint32_t wide_leaves = 0, wide_verts = 0, wide_depth = 0, wide_compact_leaves = 0;
-    // rt_set_brute_force: the reference's own sweeps, LDS-tiled (rt_brute_kernel; BASELINE config 5)
-    bool brute = false;
+    // rt_set_brute_force: the reference's own sweeps (BASELINE config 5): 0 off, 1 LDS-tiled, 2
+    // through the scalar cache (rt_brute_wf_kernel<tris, stream>)
+    int brute = 0;
     // coherent primary rays (rt_primary_kernel): RT_PRIMARY_PASS 1 / 0 force on / off, -1 by scene
     int primary_pass = -1;
     // Workgroup size of the pre-pass where the accelerator is walked from global memory (modes
@@ -964,7 +966,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         if (env) ctx->primary_min_waves = env[0] == '8' ? 8u : 0u;
         if (ctx->primary_threads != 256u) ctx->primary_min_waves = 0;  // the 64-VGPR variant is built at 256
         env = std::getenv("RT_BRUTE_FORCE");
-        ctx->brute = env && env[0] == '1';
+        ctx->brute = !env ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : 0;
         env = std::getenv("RT_BRUTE_WF");
         if (env) ctx->brute_wf = env[0] != '0';
         env = std::getenv("RT_TRI_COMPACT");
@@ -1506,7 +1508,8 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         const uint64_t passes = (uint64_t)frames * samples;
         // the wavefront: every pass (frame, sample) in order, one launch per bounce level
         const bool wf = ctx->brute_wf && passes > 0 && passes <= (1u << 20) && bounces + 2u <= kBruteLevels;
-        const size_t lds = ka.lds_stack_offset + (wf ? rt_brute_wf_tile_bytes() : rt_brute_tile_bytes());
+        const bool scalar_stream = wf && tris && ctx->brute == 2;
+        const size_t lds = ka.lds_stack_offset + (wf ? rt_brute_wf_tile_bytes(scalar_stream) : rt_brute_tile_bytes());
         int dev = 0, max_optin = 0;
         RT_HIP(ctx, hipGetDevice(&dev));
         RT_HIP(ctx, hipDeviceGetAttribute(&max_optin, hipDeviceAttributeSharedMemPerBlockOptin, dev));
@@ -1553,7 +1556,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
                 for (uint32_t level = 0; level < std::max(1u, bounces); ++level) {
                     ka.brute_pass = (uint32_t)pass;
                     ka.brute_level = level;
-                    RT_HIP(ctx, rt_launch_brute_wf(ka, tris, lds, blocks, ctx->stream));
+                    RT_HIP(ctx, rt_launch_brute_wf(ka, tris, scalar_stream, lds, blocks, ctx->stream));
                 }
             ctx->last_blocks = blocks;
         } else {
@@ -2110,7 +2113,8 @@ int rt_ray_count(rt_ctx* ctx, uint64_t* out) {
 
 int rt_set_brute_force(rt_ctx* ctx, int enable) {
     RT_ENTER(ctx);
-    ctx->brute = enable != 0;
+    if (enable < 0 || enable > 2) return fail(ctx, RT_E_INVALID, "brute-force mode must be 0, 1 or 2");
+    ctx->brute = enable;
     return RT_OK;
 }
 

@@ -309,9 +309,10 @@ class Renderer:
         self._call("rt_dispatch_time_total", ctypes.byref(ms), ctypes.byref(n))
         return ms.value, n.value
 
-    def set_brute_force(self, enable: bool) -> None:
-        """rt_set_brute_force: the reference's own sphere and triangle sweeps, LDS-tiled
-        (BASELINE config 5's stress mode), instead of the acceleration structures."""
+    def set_brute_force(self, enable) -> None:
+        """rt_set_brute_force: the reference's own sphere and triangle sweeps (BASELINE config
+        5's stress mode) instead of the acceleration structures: True / 1 with the sub-object
+        records LDS-tiled, 2 streamed through the scalar cache, False / 0 off."""
         self._call("rt_set_brute_force", int(enable))
 
     def set_triangle_pruning(self, mode: int) -> None:

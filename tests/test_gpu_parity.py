@@ -149,15 +149,17 @@ def test_gpu_full_size_sampled_c5(gpu, oracle_lib):
     _check_c5_sample(smp, acc, out)
 
 
-def test_gpu_full_size_brute_force_c5(gpu, oracle_lib):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gpu_full_size_brute_force_c5(gpu, oracle_lib, mode):
     """BASELINE config 5 as named -- the 1,000,000-triangle mesh at 1920x1080x8 in the
-    brute-force LDS-tiled mode (rt_brute_kernel: the reference's own object -> sub-object
-    -> triangle sweep for every ray): the oracle's 20,000 sampled pixels, and every pixel
-    of both frames bit-identical to the accelerated default path."""
+    brute-force mode (rt_brute_wf_kernel: the reference's own object -> sub-object ->
+    triangle sweep for every ray; the records LDS-tiled, 1, or streamed through the scalar
+    cache, 2): the oracle's 20,000 sampled pixels, and every pixel of both frames
+    bit-identical to the accelerated default path."""
     smp = _c5_full_size_oracle_sample(oracle_lib)
     scene, bounces, rays = smp["scene"], smp["bounces"], smp["rays"]
     with Renderer(scene, camera_rays=rays, frame_batch=2) as r:
-        r.set_brute_force(True)
+        r.set_brute_force(mode)
         for _ in range(2):
             r.compute_frame(bounces)
         acc, out, n = r.read_accumulation(), r.read_output(), r.ray_count()
@@ -1021,13 +1023,14 @@ def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumul
     ("c4_mixed", dict(env_size=(256, 128)), 2, 3),
     ("c5_heightfield", dict(nx=60, nz=30), 2, 1),
 ])
-@pytest.mark.parametrize("wf", ["1", "0"])
-def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, world, wf):
+@pytest.mark.parametrize("wf,mode", [("1", 1), ("1", 2), ("0", 1)])
+def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, world, wf, mode):
     """rt_set_brute_force: the reference's own sphere and object -> sub-object ->
     triangle sweeps, sub-objects streamed through LDS tiles (BASELINE config 5's
     stress mode) -- bit-identical to the oracle, in frame batches and tile splits. Both
     kernels: the wavefront over compacted queues of live paths (rt_brute_wf_kernel, the
-    default) and the lockstep workgroups (RT_BRUTE_WF=0, rt_brute_kernel)."""
+    default; the sub-object records LDS-tiled, or streamed through the scalar cache with
+    rt_set_brute_force(ctx, 2)) and the lockstep workgroups (RT_BRUTE_WF=0, rt_brute_kernel)."""
     monkeypatch.setenv("RT_BRUTE_WF", wf)
     scene, bounces = build_config(config, width=96, height=64, **kw)
     rays = scene.camera.recalculate_ray_directions()
@@ -1038,7 +1041,7 @@ def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, w
     streamed = 0
     for rank in range(world):
         with Renderer(scene, camera_rays=rays, frame_batch=batch, rank=rank, world_size=world) as r:
-            r.set_brute_force(True)
+            r.set_brute_force(mode)
             for _ in range(4):
                 r.compute_frame(bounces)
             a, o, k = r.read_accumulation(), r.read_output(), r.ray_count()
@@ -1051,14 +1054,15 @@ def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, w
     assert (streamed > 0) == bool(scene.objects)
 
 
-@pytest.mark.parametrize("config,kw,spp,accumulate,batch,bounces", [
-    ("c2_rtiow", {}, 3, 1, 2, None),
-    ("c5_heightfield", dict(nx=40, nz=20), 2, 1, 3, None),
-    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, None),
-    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 1, 0),
-    ("c1_four_spheres", {}, 1, 1, 2, 40),
+@pytest.mark.parametrize("config,kw,spp,accumulate,batch,bounces,mode", [
+    ("c2_rtiow", {}, 3, 1, 2, None, 1),
+    ("c5_heightfield", dict(nx=40, nz=20), 2, 1, 3, None, 1),
+    ("c5_heightfield", dict(nx=40, nz=20), 2, 1, 3, None, 2),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, None, 2),
+    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 1, 0, 1),
+    ("c1_four_spheres", {}, 1, 1, 2, 40, 1),
 ])
-def test_gpu_brute_force_samples_and_modes(gpu, oracle_lib, config, kw, spp, accumulate, batch, bounces):
+def test_gpu_brute_force_samples_and_modes(gpu, oracle_lib, config, kw, spp, accumulate, batch, bounces, mode):
     """The brute-force wavefront's passes: several samples per frame (each pass = one (frame,
     sample), summed in that order per pixel), accumulation off (the last frame's image), zero
     bounces (no launch traces; the image is written from the empty paths), and a deep bounce
@@ -1068,7 +1072,9 @@ def test_gpu_brute_force_samples_and_modes(gpu, oracle_lib, config, kw, spp, acc
     rays = scene.camera.recalculate_ray_directions()
     with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp, camera_rays=rays,
                   frame_batch=batch) as r:
-        r.set_brute_force(True)
+        r.set_brute_force(mode)
+        with pytest.raises(Exception):
+            r.set_brute_force(3)  # RT_E_INVALID
         for _ in range(3):
             r.compute_frame(bounces)
         got = r.read_accumulation(), r.read_output(), r.ray_count()
