@@ -22,8 +22,19 @@ def main(prof_dir, dest):
     dest.mkdir(parents=True, exist_ok=True)
     bench_line = json.loads((prof_dir / "trace_bench.json").read_text().strip().splitlines()[-1])
     # the launch's dominant kernel: the brute-force sweep kernel, or the path kernel
-    kernel = "rt_brute_kernel" if "rt_brute_kernel" in bench_line["roofline"].get("kernel", "") else "rt_pathtrace_kernel"
+    kname = bench_line["roofline"].get("kernel", "")
+    kernel = "rt_brute_wf_kernel" if "rt_brute_wf_kernel" in kname else (
+        "rt_brute_kernel" if "rt_brute_kernel" in kname else "rt_pathtrace_kernel")
     summ = summarize_prof.main(prof_dir, kernel)
+    # bench.py prices a batch (rt_compute_frames' launch); the brute-force wavefront runs one
+    # dispatch per (frame, bounce level) of the batch: its per-dispatch counters times that
+    per_batch = 1
+    if kernel == "rt_brute_wf_kernel":
+        per_batch = int(bench_line["config"]["frame_batch"]) * max(1, int(bench_line["config"]["bounces"]))
+        for k in ("fetch_bytes_x2", "write_bytes", "avg_ns"):
+            if summ.get(k) is not None:
+                summ[k] = summ[k] * per_batch
+        summ["dispatches_per_batch"] = per_batch
     (dest / "summary.json").write_text(json.dumps(summ, indent=1) + "\n")
     ks = prof_dir / "trace" / "run_kernel_stats.csv"
     if ks.exists():
