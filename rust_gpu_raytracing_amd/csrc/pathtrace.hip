@@ -2621,7 +2621,7 @@ __global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES
                 const uint32_t first = ob.first_sub_object_index, n_sub = ob.sub_object_count;
                 const uint32_t last_sub = ka.sub_object_count - 1u;
                 rt_cf4* recs = (rt_cf4*)(const void*)ka.sub_objects;
-                if (tid == 0) streamed += n_sub;
+                if ((tid & 63u) == 0u) streamed += n_sub;  // every wave streams the records itself
                 uint32_t cnt = 0u;
                 // the entered boxes' triangles, each lane its own list in order (as the tiled sweep)
                 auto drain = [&]() {
@@ -2866,10 +2866,9 @@ __global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES
     }
     atomicAdd(&block_rays, rays);
     __syncthreads();
-    if (tid == 0) {
-        if (block_rays) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
-        if (streamed && ka.stream_bytes) atomicAdd(ka.stream_bytes, (unsigned long long)streamed * 32ull);
-    }
+    if (tid == 0 && block_rays) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
+    // the records this workgroup's LDS tiles (thread 0) or its waves (lane 0 of each, kStream) read
+    if (streamed && ka.stream_bytes) atomicAdd(ka.stream_bytes, (unsigned long long)streamed * 32ull);
     if (ka.launch_clock) {
         __syncthreads();
         if (tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
