@@ -6,7 +6,7 @@
 set -o pipefail
 case "$1" in
   r05h)
-    walk-variant and brute-force tests, q4 A/B, brute A/B
+    # walk-variant and brute-force tests, q4 A/B, brute A/B
     mkdir -p gpurun_out/r05h
     timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "global_walk_variants or lds_vertex or brute" > gpurun_out/r05h/tests.log 2>&1 || exit 1
     RT_BRUTE_WF=1 timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/r05h/brute_wf.json 2> gpurun_out/r05h/brute_wf.err || exit 1
@@ -16,19 +16,19 @@ case "$1" in
     RT_LIB=abvar/lib_diag.so RT_TRI_Q4=0 timeout -k 10 200 python3 tools/diag_split.py --frame-batch 20 c5_heightfield > gpurun_out/r05h/diag_bin.json 2>&1
     ;;
   r05i)
-    brute-force tests + bench, C5 layout A/B
+    # brute-force tests + bench, C5 layout A/B
     mkdir -p gpurun_out/r05i
     timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "brute" > gpurun_out/r05i/tests.log 2>&1 || exit 1
     timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/r05i/brute_wf.json 2> gpurun_out/r05i/brute_wf.err || exit 1
     timeout -k 10 400 python3 tools/ab_env.py "RT_TRI_OCTANTS=1" "RT_TRI_OCTANTS=0" "RT_TRI_OCTANTS=0 RT_TRI_QNODES=0" "RT_TRI_OCTANTS=1 RT_PRIMARY_PASS=0" "RT_TRI_OCTANTS=0 RT_PRIMARY_PASS=0" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05i/ab_oct.jsonl 2> gpurun_out/r05i/ab_oct.err
     ;;
   r05j)
-    PMC of the C5 walk (TCP/TA/TD) and of the brute-force wavefront
+    # PMC of the C5 walk (TCP/TA/TD) and of the brute-force wavefront
     bash tools/pmc_tcp.sh r05_c5tcp --config c5_heightfield || exit 1
     bash tools/profile.sh r05_c5b --config c5_heightfield --brute-force --steps 2 --warmup 2 || exit 1
     ;;
   r05k)
-    brute-force wavefront variants
+    # brute-force wavefront variants
     mkdir -p gpurun_out/r05k
     timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "brute" > gpurun_out/r05k/tests.log 2>&1 || exit 1
     for v in default abvar/lib_brh16.so abvar/lib_brg8.so abvar/lib_br2.so abvar/lib_brt1k.so; do
@@ -37,28 +37,28 @@ case "$1" in
     done
     ;;
   r05l)
-    all configs with the CPU baseline, strong probes C4/C2
+    # all configs with the CPU baseline, strong probes C4/C2
     mkdir -p gpurun_out/r05l
     timeout -k 10 900 python3 tools/bench_all.py --frames 20 --cpu-seconds 8 > gpurun_out/r05l/bench_all.jsonl 2> gpurun_out/r05l/bench_all.err || exit 1
     timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c4_mixed --gather accumulation > gpurun_out/r05l/strong_c4_acc.jsonl 2> gpurun_out/r05l/strong_c4_acc.err || exit 1
     timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c2_rtiow --gather accumulation > gpurun_out/r05l/strong_c2_acc.jsonl 2> gpurun_out/r05l/strong_c2_acc.err || exit 1
     ;;
   r05m)
-    refill prologue tests + A/B
+    # refill prologue tests + A/B
     mkdir -p gpurun_out/r05m
     timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -x -v --timeout 120 --timeout-method thread -m gpu -k "golden or frame_batch or group or full_frame or sphere or determinism or camera or device" > gpurun_out/r05m/tests.log 2>&1 || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_noprep.so --config c2_rtiow --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/r05m/ab_c2.json 2> gpurun_out/r05m/ab_c2.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_noprep.so --config c1_four_spheres --width 800 --height 600 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/r05m/ab_c1.json 2> gpurun_out/r05m/ab_c1.err || exit 1
     ;;
   r05n)
-    C5 regression check (ABI-11 commit build vs now, q4 compiled in/out)
+    # C5 regression check (ABI-11 commit build vs now, q4 compiled in/out)
     mkdir -p gpurun_out/r05n
     timeout -k 10 600 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_3e26.so abvar/lib_q4.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05n/ab_c5.json 2> gpurun_out/r05n/ab_c5.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_3e26.so --config c3_chess --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/r05n/ab_c3.json 2> gpurun_out/r05n/ab_c3.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_3e26.so --config c2_rtiow --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/r05n/ab_c2.json 2> gpurun_out/r05n/ab_c2.err || exit 1
     ;;
   r05o)
-    lazy triangle piece loads -- tests and A/B against the previous build
+    # lazy triangle piece loads -- tests and A/B against the previous build
     mkdir -p gpurun_out/r05o
     timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "triangle or chess or golden or pruning or walk" > gpurun_out/r05o/tests.log 2>&1 || exit 1
     for c in c3_chess c4_mixed c5_heightfield; do
@@ -66,32 +66,32 @@ case "$1" in
     done
     ;;
   r05p)
-    lazy triangle pieces on C5, three builds in one process
+    # lazy triangle pieces on C5, three builds in one process
     mkdir -p gpurun_out/r05p
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_nolazy.so abvar/lib_head.so --config c5_heightfield --rounds 4 --frames 40 --frame-batch 20 > gpurun_out/r05p/ab_c5.json 2> gpurun_out/r05p/ab_c5.err || exit 1
     ;;
   r05q)
-    streamed brute-force sweep variant
+    # streamed brute-force sweep variant
     mkdir -p gpurun_out/r05q
     RT_LIB=abvar/lib_bstream.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "brute" > gpurun_out/r05q/tests.log 2>&1 || exit 1
     timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/r05q/brute_default.json 2> gpurun_out/r05q/brute_default.err || exit 1
     RT_LIB=abvar/lib_bstream.so timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/r05q/brute_stream.json 2> gpurun_out/r05q/brute_stream.err || exit 1
     ;;
   r05r)
-    node pairs in the global-memory walk
+    # node pairs in the global-memory walk
     mkdir -p gpurun_out/r05r
     timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "heightfield or c5 or quantized or pruning or grazing or walk or certif or leaf or triangle_accel or device_scene" > gpurun_out/r05r/tests.log 2>&1 || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_nopairs.so abvar/lib_pairs_u3.so --config c5_heightfield --rounds 4 --frames 40 --frame-batch 20 > gpurun_out/r05r/ab_c5.json 2> gpurun_out/r05r/ab_c5.err || exit 1
     ;;
   r05s)
-    the whole GPU suite, smoke, headline bench
+    # the whole GPU suite, smoke, headline bench
     mkdir -p gpurun_out/r05s
     timeout -k 10 1100 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r05s/tests.log 2>&1 || exit 1
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05s/smoke.log 2>&1 || exit 1
     timeout -k 10 400 python3 bench.py > gpurun_out/r05s/bench.json 2> gpurun_out/r05s/bench.err || exit 1
     ;;
   r05t)
-    brute-force occupancy variants
+    # brute-force occupancy variants
     mkdir -p gpurun_out/r05t
     for v in default abvar/lib_bstream.so abvar/lib_bs_w6.so abvar/lib_bs_w8.so abvar/lib_bt_w6.so; do
       if [ "$v" = default ]; then L=""; else L="RT_LIB=$v"; fi
@@ -99,7 +99,7 @@ case "$1" in
     done
     ;;
   r05u)
-    brute-force modes (tiled / scalar-streamed)
+    # brute-force modes (tiled / scalar-streamed)
     mkdir -p gpurun_out/r05u
     timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "brute" > gpurun_out/r05u/tests.log 2>&1 || exit 1
     timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/r05u/brute_tiled.json 2> gpurun_out/r05u/brute_tiled.err || exit 1
@@ -115,13 +115,13 @@ case "$1" in
     bash tools/profile.sh r05_c5bs --config c5_heightfield --brute-force stream --steps 2 --warmup 2 > gpurun_out/prof_r05_c5bs.log 2>&1 || exit 1
     ;;
   r05w)
-    C5 knobs at the final build
+    # C5 knobs at the final build
     mkdir -p gpurun_out/r05w
     timeout -k 10 500 python3 tools/ab_env.py "RT_LEAF_BATCH=4" "RT_LEAF_BATCH=3" "RT_LEAF_BATCH=5" "RT_TRAV_THRESHOLD=48" "RT_TRAV_THRESHOLD=60" "RT_DRAIN_THRESHOLD=24" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05w/ab_knobs.jsonl 2> gpurun_out/r05w/ab_knobs.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_u4.so abvar/lib_u6.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05w/ab_unroll.json 2> gpurun_out/r05w/ab_unroll.err || exit 1
     ;;
   r05x)
-    scalar loads in the primary pre-pass -- tests, bench A/B
+    # scalar loads in the primary pre-pass -- tests, bench A/B
     mkdir -p gpurun_out/r05x
     timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "primary or heightfield or c5 or pruning or grazing or quantized or walk or full_size" > gpurun_out/r05x/tests.log 2>&1 || exit 1
     for i in 1 2; do
@@ -130,7 +130,7 @@ case "$1" in
     done
     ;;
   r05y)
-    sphere pair leaves (RT_SPHERE_PAIRS) -- parity and A/B
+    # sphere pair leaves (RT_SPHERE_PAIRS) -- parity and A/B
     mkdir -p gpurun_out/r05y
     RT_SPHERE_PAIRS=1 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -x -v --timeout 200 --timeout-method thread -m gpu -k "golden or full_frame or c2 or c1 or four_spheres or rtiow or sphere or brute or frame_batch" > gpurun_out/r05y/tests.log 2>&1 || exit 1
     timeout -k 10 500 python3 tools/ab_env.py "RT_SPHERE_PAIRS=0" "RT_SPHERE_PAIRS=1" "RT_SPHERE_PAIRS=1 RT_SPHERE_LEAF=1" --config c2_rtiow --frame-batch 20 --frames 40 --rounds 5 > gpurun_out/r05y/ab_c2.jsonl 2> gpurun_out/r05y/ab_c2.err || exit 1
@@ -151,18 +151,25 @@ case "$1" in
     bash tools/profile.sh r05f_c5bs --config c5_heightfield --brute-force stream --steps 2 --warmup 2 > gpurun_out/r05z/prof_c5bs.log 2>&1 || exit 1
     ;;
   r05aa)
-    C3/C4 in the global-memory walk (mode 1) vs LDS-resident (mode 2)
+    # C3/C4 in the global-memory walk (mode 1) vs LDS-resident (mode 2)
     mkdir -p gpurun_out/r05aa
     timeout -k 10 400 python3 tools/ab_env.py "RT_LDS_MODE=2" "RT_LDS_MODE=1" "RT_LDS_MODE=1 RT_PRIMARY_PASS=0" --config c3_chess --frame-batch 20 --frames 40 --rounds 4 > gpurun_out/r05aa/ab_c3.jsonl 2> gpurun_out/r05aa/ab_c3.err || exit 1
     timeout -k 10 600 python3 tools/ab_env.py "RT_LDS_MODE=2" "RT_LDS_MODE=1" --config c4_mixed --width 3840 --height 2160 --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05aa/ab_c4.jsonl 2> gpurun_out/r05aa/ab_c4.err || exit 1
     ;;
   r05ab)
-    cooperative leaf batches in the LDS-resident walk (RT_COOP_LDS build)
+    # cooperative leaf batches in the LDS-resident walk (RT_COOP_LDS build)
     mkdir -p gpurun_out/r05ab
     RT_LIB=abvar/lib_cooplds.so timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "chess or c3 or c4 or mixed or golden or lds or full_frame" > gpurun_out/r05ab/tests.log 2>&1 || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_cooplds.so --config c3_chess --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/r05ab/ab_c3.json 2> gpurun_out/r05ab/ab_c3.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_cooplds.so --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 20 --frame-batch 20 > gpurun_out/r05ab/ab_c4.json 2> gpurun_out/r05ab/ab_c4.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_cooplds.so --config c2_rtiow --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05ab/ab_c2.json 2> gpurun_out/r05ab/ab_c2.err || exit 1
+    ;;
+  r05ad)
+    # strong-scaling probes at the final build: C2 with both payloads, C4 with the accumulation
+    mkdir -p gpurun_out/r05ad
+    timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c2_rtiow --gather accumulation > gpurun_out/r05ad/strong_c2_accumulation.jsonl 2> gpurun_out/r05ad/strong_c2_accumulation.err || exit 1
+    timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c2_rtiow --gather image > gpurun_out/r05ad/strong_c2_image.jsonl 2> gpurun_out/r05ad/strong_c2_image.err || exit 1
+    timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c4_mixed --gather accumulation > gpurun_out/r05ad/strong_c4_accumulation.jsonl 2> gpurun_out/r05ad/strong_c4_accumulation.err || exit 1
     ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
