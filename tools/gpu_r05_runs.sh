@@ -171,5 +171,25 @@ case "$1" in
     timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c2_rtiow --gather image > gpurun_out/r05ad/strong_c2_image.jsonl 2> gpurun_out/r05ad/strong_c2_image.err || exit 1
     timeout -k 10 600 python3 tools/strong_probe.py --steps 20 --config c4_mixed --gather accumulation > gpurun_out/r05ad/strong_c4_accumulation.jsonl 2> gpurun_out/r05ad/strong_c4_accumulation.err || exit 1
     ;;
+  r05ae)
+    # small-subtree certificates (RT_TRI_SUBTREE) -- parity on the walks from global memory, C5 A/B
+    mkdir -p gpurun_out/r05ae
+    timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "heightfield or c5 or pruning or grazing or quantized or walk or certif" > gpurun_out/r05ae/tests.log 2>&1 || exit 1
+    timeout -k 10 600 python3 tools/ab_env.py "RT_TRI_SUBTREE=0" "RT_TRI_SUBTREE=2" "RT_TRI_SUBTREE=3" "RT_TRI_SUBTREE=4" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ae/ab_subtree.jsonl 2> gpurun_out/r05ae/ab_subtree.err || exit 1
+    ;;
+  r05af)
+    # the same with the subtree tests deferred to the leaf batches (r05ae tested them on the spot)
+    mkdir -p gpurun_out/r05af
+    timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "heightfield or c5 or pruning or grazing or quantized or walk or certif" > gpurun_out/r05af/tests.log 2>&1 || exit 1
+    timeout -k 10 600 python3 tools/ab_env.py "RT_TRI_SUBTREE=0" "RT_TRI_SUBTREE=2" "RT_TRI_SUBTREE=3" "RT_TRI_SUBTREE=4" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05af/ab_subtree.jsonl 2> gpurun_out/r05af/ab_subtree.err || exit 1
+    ;;
+  r05ag)
+    # subtree tests deferred, the waiting lane marked through its node index -- parity, A/B against the
+    # round's final build (abvar/lib_head.so) in one process, and the subtree sizes
+    mkdir -p gpurun_out/r05ag
+    timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "heightfield or c5 or pruning or grazing or quantized or walk or certif" > gpurun_out/r05ag/tests.log 2>&1 || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_head.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05ag/ab_head.json 2> gpurun_out/r05ag/ab_head.err || exit 1
+    timeout -k 10 600 python3 tools/ab_env.py "RT_TRI_SUBTREE=0" "RT_TRI_SUBTREE=2" "RT_TRI_SUBTREE=4" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ag/ab_subtree.jsonl 2> gpurun_out/r05ag/ab_subtree.err || exit 1
+    ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
