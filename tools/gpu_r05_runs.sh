@@ -191,5 +191,20 @@ case "$1" in
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_head.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05ag/ab_head.json 2> gpurun_out/r05ag/ab_head.err || exit 1
     timeout -k 10 600 python3 tools/ab_env.py "RT_TRI_SUBTREE=0" "RT_TRI_SUBTREE=2" "RT_TRI_SUBTREE=4" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ag/ab_subtree.jsonl 2> gpurun_out/r05ag/ab_subtree.err || exit 1
     ;;
+  r05ah)
+    # workgroup size at the final build: 1024 threads (4 waves per SIMD, 128 VGPRs with spills) against
+    # 512 / 256 (3 waves per SIMD, no spills), on the triangle scenes
+    mkdir -p gpurun_out/r05ah
+    for c in c5_heightfield c3_chess c4_mixed; do
+    timeout -k 10 400 python3 tools/ab_env.py "RT_BLOCK_THREADS=1024" "RT_BLOCK_THREADS=512" "RT_BLOCK_THREADS=256" --config $c --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ah/ab_threads_$c.jsonl 2> gpurun_out/r05ah/ab_threads_$c.err || exit 1
+    done
+    ;;
+  r05ai)
+    # traversal knobs re-checked at the final build: C2, C3, C4 (at its 4K size)
+    mkdir -p gpurun_out/r05ai
+    timeout -k 10 300 python3 tools/ab_env.py "RT_TRAV_THRESHOLD=8" "RT_TRAV_THRESHOLD=6" "RT_TRAV_THRESHOLD=10" "RT_TRAV_THRESHOLD=12" --config c2_rtiow --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ai/ab_c2.jsonl 2> gpurun_out/r05ai/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_env.py "RT_TRAV_THRESHOLD=24" "RT_TRAV_THRESHOLD=16" "RT_TRAV_THRESHOLD=32" "RT_LEAF_BATCH=5" "RT_LEAF_BATCH=7" --config c3_chess --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ai/ab_c3.jsonl 2> gpurun_out/r05ai/ab_c3.err || exit 1
+    timeout -k 10 400 python3 tools/ab_env.py "RT_TRAV_THRESHOLD=24" "RT_TRAV_THRESHOLD=16" "RT_TRAV_THRESHOLD=32" "RT_LEAF_BATCH=5" "RT_LEAF_BATCH=7" --config c4_mixed --width 3840 --height 2160 --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ai/ab_c4.jsonl 2> gpurun_out/r05ai/ab_c4.err || exit 1
+    ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
