@@ -206,5 +206,11 @@ case "$1" in
     timeout -k 10 300 python3 tools/ab_env.py "RT_TRAV_THRESHOLD=24" "RT_TRAV_THRESHOLD=16" "RT_TRAV_THRESHOLD=32" "RT_LEAF_BATCH=5" "RT_LEAF_BATCH=7" --config c3_chess --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ai/ab_c3.jsonl 2> gpurun_out/r05ai/ab_c3.err || exit 1
     timeout -k 10 400 python3 tools/ab_env.py "RT_TRAV_THRESHOLD=24" "RT_TRAV_THRESHOLD=16" "RT_TRAV_THRESHOLD=32" "RT_LEAF_BATCH=5" "RT_LEAF_BATCH=7" --config c4_mixed --width 3840 --height 2160 --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05ai/ab_c4.jsonl 2> gpurun_out/r05ai/ab_c4.err || exit 1
     ;;
+  r05ak)
+    # the leaf batch's certificate and triangle-block loads non-temporal (abvar/lib_nt.so, -DRT_NT_LEAF=1):
+    # do the node lines stay in the L1 longer?
+    mkdir -p gpurun_out/r05ak
+    timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_nt.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05ak/ab_nt.json 2> gpurun_out/r05ak/ab_nt.err || exit 1
+    ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
