@@ -212,5 +212,14 @@ case "$1" in
     mkdir -p gpurun_out/r05ak
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_nt.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05ak/ab_nt.json 2> gpurun_out/r05ak/ab_nt.err || exit 1
     ;;
+  r05al)
+    # multi-frame packets in the primary pre-pass (RT_PRIMARY_FRAMES=2 / 4) -- parity, C5 A/B, F=1 against
+    # the final build in one process
+    mkdir -p gpurun_out/r05al
+    RT_PRIMARY_FRAMES=4 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "primary or heightfield or c5 or pruning or grazing or quantized or walk or frame_batch" > gpurun_out/r05al/tests_f4.log 2>&1 || exit 1
+    RT_PRIMARY_FRAMES=2 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -m gpu -k "primary or heightfield or c5 or pruning or grazing" > gpurun_out/r05al/tests_f2.log 2>&1 || exit 1
+    timeout -k 10 600 python3 tools/ab_env.py "RT_PRIMARY_FRAMES=1" "RT_PRIMARY_FRAMES=2" "RT_PRIMARY_FRAMES=4" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05al/ab_frames.jsonl 2> gpurun_out/r05al/ab_frames.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_head.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05al/ab_head.json 2> gpurun_out/r05al/ab_head.err || exit 1
+    ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
