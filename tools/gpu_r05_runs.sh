@@ -221,5 +221,12 @@ case "$1" in
     timeout -k 10 600 python3 tools/ab_env.py "RT_PRIMARY_FRAMES=1" "RT_PRIMARY_FRAMES=2" "RT_PRIMARY_FRAMES=4" --config c5_heightfield --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05al/ab_frames.jsonl 2> gpurun_out/r05al/ab_frames.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/lib_head.so --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/r05al/ab_head.json 2> gpurun_out/r05al/ab_head.err || exit 1
     ;;
+  r05am)
+    # C3 / C4 scene-side knobs at the final build (sphere leaves and layouts, sub-object staging, claim order)
+    mkdir -p gpurun_out/r05am
+    K='"RT_SPHERE_LEAF=0" "RT_SPHERE_LEAF=2" "RT_SPHERE_LEAF=8" "RT_SPHERE_OCTANTS=0" "RT_SPHERE_BOX_ORDER=0" "RT_STAGE_SUBS=0" "RT_STAGE_SUBS=1" "RT_TILE_SCHEDULE=0" "RT_UNIT_TILE_MAJOR=0" "RT_UNIT_TILE_MAJOR=1" "RT_BATCH_SCHEDULE=1"'
+    eval timeout -k 10 400 python3 tools/ab_env.py $K --config c4_mixed --width 3840 --height 2160 --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05am/ab_c4.jsonl 2> gpurun_out/r05am/ab_c4.err || exit 1
+    eval timeout -k 10 300 python3 tools/ab_env.py $K --config c3_chess --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05am/ab_c3.jsonl 2> gpurun_out/r05am/ab_c3.err || exit 1
+    ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
