@@ -228,5 +228,15 @@ case "$1" in
     eval timeout -k 10 400 python3 tools/ab_env.py $K --config c4_mixed --width 3840 --height 2160 --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05am/ab_c4.jsonl 2> gpurun_out/r05am/ab_c4.err || exit 1
     eval timeout -k 10 300 python3 tools/ab_env.py $K --config c3_chess --frame-batch 20 --frames 20 --rounds 3 > gpurun_out/r05am/ab_c3.jsonl 2> gpurun_out/r05am/ab_c3.err || exit 1
     ;;
+  r05aj)
+    # the TD-rate microbenchmark with its L1-hit and coalesced-line variants (build it first:
+    # hipcc --offload-arch=gfx950 -O3 tools/microbench/td_rate.hip -o tools/microbench/td_rate)
+    mkdir -p gpurun_out/r05aj
+    timeout -k 10 120 ./tools/microbench/td_rate > gpurun_out/r05aj/td_rate.txt 2>&1 || exit 1
+    ;;
+  r05_verify)
+    # end-of-session check of the committed tree: every GPU test, smoke, the headline bench
+    bash tools/gpu_check.sh r05_verify tests smoke bench || exit 1
+    ;;
   *) echo "unknown run $1"; exit 2 ;;
 esac
