@@ -58,7 +58,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # 16 lanes x 2.4 GHz (a wave64 instruction issues over 4 cycles of a SIMD16)
 VALU_LANE_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 KERNEL_NAMES = {"path": "rt_pathtrace_kernel", "primary": "rt_primary_kernel", "resolve": "rt_resolve_frames_kernel",
-                "brute": "rt_brute_wf_kernel"}
+                "brute": "rt_brute_wf_kernel", "brute_stream": "(its records through the scalar cache)"}
 # The reference computes a frame every >= 0.8 ms and displays every >= 5 ms
 # (src/main.rs:88-92, 365-375): about 6 computed frames per displayed image.
 DISPLAY_CADENCE_FRAMES = 6
@@ -205,8 +205,14 @@ def main() -> int:
                     help="the reference's own sweeps (rt_set_brute_force; BASELINE config 5's stress mode) instead "
                          "of the acceleration structures: the sub-object records LDS-tiled (default) or streamed "
                          "through the scalar cache ('stream', rt_set_brute_force(ctx, 2))")
-    ap.add_argument("--frame-batch", type=int, default=int(os.environ.get("RT_FRAME_BATCH", "0")),
+    ap.add_argument("--frame-batch", type=int, default=0,
                     help="frames one launch may render (rt_set_frame_batch); 0 = default_frame_batch(N, steps)")
+    ap.add_argument("--triangle-pruning", type=int, choices=[0, 1, 2], default=1,
+                    help="rt_set_triangle_pruning: 1 certified (default, exact), 0 box culling, 2 the round-3 "
+                         "relative slack (not exact)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="rt_set_tuning: an exact variant of the schedule or acceleration structures (A/B runs; "
+                         "include/rt_abi.h lists the keys); repeatable")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="N>1: strong = the 1920x1080 frame split N ways (the metric's config, `value`); "
                          "weak = N x the pixels (per-GPU work fixed)")
@@ -263,7 +269,10 @@ def main() -> int:
         width, height = size_for(scaling)
         scene, default_bounces = build_config(args.config, width=width, height=height)
         bounces = args.bounces or default_bounces
-        r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=frame_batch)
+        r = Renderer(scene, device=device, rank=rank, world_size=world, frame_batch=frame_batch,
+                     tuning={k: int(v) for k, v in (t.split("=", 1) for t in args.tune)})
+        if args.triangle_pruning != 1:
+            r.set_triangle_pruning(args.triangle_pruning)
         if frame_batch is None:
             frame_batch = r.frame_batch()[0]
         display = None
@@ -378,7 +387,7 @@ def main() -> int:
         t_render = t_total - t_gather_in_region
         assert 0.0 < t_render <= t_total, (t_render, t_total, t_gather_in_region)
         res = dict(r=r, scene=scene, bounces=bounces, width=width, height=height, rays=r.ray_count(),
-                   streamed=r.streamed_bytes(),
+                   streamed=r.streamed_bytes(), streamed_l2=r.streamed_bytes_l2(),
                    settle_frames=settle_frames,
                    t_render=t_render, t_gather=t_gather, gathered=gathered, launch=r.launch_config(),
                    passes=r.last_launch_passes(),
@@ -515,9 +524,12 @@ def main() -> int:
         frames_per_launch = args.steps / max(n_timed, 1)
         rays_per_launch = m["rays"] / max(n_timed, 1)
         b_launch = algorithmic_bytes(m["owned_px"], rays_per_launch, scene_bytes(scene), frames_per_launch)
-        # brute-force launches also stream the sub-object records through LDS once per
-        # workgroup and bounce: SURVEY §8d's tile-streaming term, counted by the kernel
+        # brute-force launches also stream the sub-object records: SURVEY §8d's tile-streaming
+        # term with its fixed convention (32 B x the sub-objects per started 256 rays of each
+        # bounce level), counted by the kernel; what the sweeps actually read from L2 (per LDS
+        # tile and workgroup, or per wave in the scalar-cache mode) is reported beside it
         stream_launch = m.get("streamed", 0) / max(n_timed, 1)
+        stream_l2_launch = m.get("streamed_l2", 0) / max(n_timed, 1)
         b_launch += stream_launch
         achieved = b_launch / avg_kernel_s / 1e9
         eff_launch_s = m["t_render"] / max(n_timed, 1)  # wall time per launch: overlapped launches pipeline
@@ -526,10 +538,11 @@ def main() -> int:
             workload += (", brute-force sweeps streamed through the scalar cache" if args.brute_force == "stream"
                          else ", brute-force LDS-tiled sweeps")
         # a non-default triangle walk is another workload for the PMC table (its counters are
-        # not the default walk's): RT_TRI_PRUNE 0 = box culling, 2 = the round-3 slack (not exact)
-        prune = os.environ.get("RT_TRI_PRUNE", "1")
-        if prune != "1" and int(scene.flatten()[2].shape[0]) > 0:
-            workload += f", triangle pruning mode {prune}"
+        # not the default walk's): --triangle-pruning 0 = box culling, 2 = the round-3 slack (not exact)
+        if args.triangle_pruning != 1 and int(scene.flatten()[2].shape[0]) > 0:
+            workload += f", triangle pruning mode {args.triangle_pruning}"
+        if args.tune:
+            workload += ", tuning " + " ".join(sorted(args.tune))
         build_hash = native_build.source_hash()
         pmc, pmc_why = pmc_entry(f"{workload} | frame_batch {fb}", build_hash) if world == 1 else (None, "N>1")
         result = {
@@ -584,6 +597,7 @@ def main() -> int:
                 "launch": m["launch"],
                 "bytes_per_launch": b_launch,
                 "tile_stream_bytes_per_launch": stream_launch,
+                "l2_stream_bytes_per_launch": stream_l2_launch,
                 "note": ("the reference's sweeps: VALU-bound on sub-object box tests (DESIGN §5.5)"
                          if args.brute_force else
                          "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction"),
@@ -608,12 +622,14 @@ def main() -> int:
             result["reference_pattern_vs_headline"] = cadences["ms_per_step_reference_pattern"] / result["ms_per_step"]
         if args.driver == "group":
             result["driver"] = "c-abi group (rt_create_multi + rt_gather_frame, one process)"
+        # the gather's payload in `value` (the default moved from the RGBA8 image to
+        # the accumulation in round 5; None when no gather is timed, N = 1)
+        result["gather_payload"] = args.gather if (dist_run and m["gathered"]) else None
         if dist_run:
             result["render_ms_per_step"] = m["t_render_max"] / args.steps * 1e3
             result["gather_ms"] = m["t_gather_max"] * 1e3
             result["gather_in_value"] = m["gathered"]
             if m["gathered"]:
-                result["gather_payload"] = args.gather
                 result["gather_image_ms"] = m["t_gather_image_max"] * 1e3
                 result["gather_accum_ms"] = m["t_gather_accum_max"] * 1e3
                 # the same run priced with the other payload's gather in place of the --gather

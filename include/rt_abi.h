@@ -43,7 +43,7 @@ extern "C" {
 #define RT_API
 #endif
 
-#define RT_ABI_VERSION 11
+#define RT_ABI_VERSION 12
 
 /* ---- error codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -219,7 +219,10 @@ RT_API int rt_dispatch(rt_ctx* ctx, uint32_t bounces);
 
 /* Renderer::compute_frame (src/renderer.rs:201-252): if Params.accumulate
  * is 1, write Params with accumulation_index = k and then k += 1; then
- * rt_dispatch. Asynchronous. */
+ * rt_dispatch. Asynchronous. With frame batching (below) the frame may only be
+ * queued: an error of its launch (a failed allocation or launch) is then returned
+ * by the call that launches the batch -- the rt_compute_frame that fills it, or
+ * the next other entry point on the context. */
 RT_API int rt_compute_frame(rt_ctx* ctx, uint32_t bounces);
 
 /* `frames` consecutive rt_compute_frame calls fused into one launch: each
@@ -228,7 +231,10 @@ RT_API int rt_compute_frame(rt_ctx* ctx, uint32_t bounces);
  * sequence of calls (the per-frame outputs in between are never observable:
  * the reference only reads output_data after a frame, src/renderer.rs:254).
  * Used by the multi-GPU bench, where each rank advances its tiles by N frames
- * per step. frames >= 1. Asynchronous. */
+ * per step. frames >= 1. A batch whose per-frame buffers (32 B per owned pixel,
+ * frame and sample) would exceed the batch budget -- an eighth of the device's
+ * memory, tuning "batch_memory_mb" -- runs as consecutive launches of as many
+ * frames as fit, with the same results. Asynchronous. */
 RT_API int rt_compute_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
 
 /* `count` consecutive rt_compute_frame calls made in one call (new, ABI 10): the loop a
@@ -257,7 +263,7 @@ RT_API int rt_submit_frames(rt_ctx* ctx, uint32_t bounces, uint32_t count);
  * host that mirrors the reference's event loop -- one rt_compute_frame per frame and
  * a display copy every few frames (src/renderer.rs:201-283, src/main.rs:88-92,
  * 365-375) -- gets launches of the frames between two displays without calling
- * this. 1 launches each frame at once (env RT_FRAME_BATCH overrides the default).
+ * this. 1 launches each frame at once.
  * max_frames in [1, 64]. rt_frame_batch reports the setting and the frames
  * queued; rt_flush launches them now. */
 #define RT_DEFAULT_FRAME_BATCH 16
@@ -290,7 +296,9 @@ RT_API int rt_read_output_pitched(rt_ctx* ctx, uint8_t* dst, uint32_t bytes_per_
  * rows `bytes_per_row` bytes apart (>= 4*width; padding untouched). Stream-ordered
  * after the frames submitted so far (queued frames are launched first), asynchronous:
  * the display observation point of a render loop, with no PCIe transfer and no host
- * wait, as in the reference (which never reads the frame back to the host). */
+ * wait, as in the reference (which never reads the frame back to the host).
+ * RT_E_INVALID (ABI 12) when `dst_device` is not device memory of the context's device,
+ * or on a rank context (world_size > 1), whose output holds only its own tiles. */
 RT_API int rt_copy_output_to_device(rt_ctx* ctx, void* dst_device, uint32_t bytes_per_row);
 
 /* calculate_bytes_per_row (src/renderer.rs:285-295): 4*width rounded up to
@@ -310,14 +318,18 @@ RT_API int rt_reset_ray_count(rt_ctx* ctx);
  * with no acceleration structure: a wavefront over the live paths, each
  * workgroup streaming the sub-object records through LDS in tiles and testing
  * them with broadcast reads. enable = 2 (ABI 11): the same sweeps with the
- * records streamed through the scalar cache by each wave (no LDS tile). Same
- * results, bit for bit, as the accelerated default (0); other values are
- * RT_E_INVALID. The scene's spheres, materials and objects must fit in LDS.
- * rt_streamed_bytes: sub-object bytes those launches streamed (the
- * tile-streaming term of SURVEY §8d), since creation or the last
- * rt_reset_ray_count. Synchronous. */
+ * records streamed through the scalar cache by each wave (no LDS tile; a scene
+ * without triangles has none to stream and runs mode 1's kernel: rt_last_launch_passes
+ * says which ran). Same results, bit for bit, as the accelerated default (0); other
+ * values are RT_E_INVALID. The scene's spheres, materials and objects must fit in LDS.
+ * rt_streamed_bytes: the tile-streaming term of SURVEY §8d for those launches --
+ * 32 B x the swept sub-objects per started 256 rays of each bounce level, its fixed
+ * convention -- since creation or the last rt_reset_ray_count. rt_streamed_bytes_l2
+ * (ABI 12): the sub-object bytes the sweeps actually read from L2 (per LDS tile and
+ * workgroup in mode 1, per wave in mode 2). Synchronous. */
 RT_API int rt_set_brute_force(rt_ctx* ctx, int enable);
 RT_API int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out);
+RT_API int rt_streamed_bytes_l2(rt_ctx* ctx, uint64_t* out);
 
 /* Distance pruning of the triangle walk (new; ABI 8, modes since ABI 9). The
  * reference sweeps every object -> sub-object -> triangle
@@ -333,8 +345,26 @@ RT_API int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out);
  * faster on scenes without coherent normals, NOT exact -- rays nearly in a
  * triangle's plane near their origin can get another triangle than the sweep's
  * (tests/test_tri_accel_cpu.py builds such rays). Walks of the octant-ordered
- * layouts visit near boxes first in every mode. Synchronous. */
+ * layouts visit near boxes first in every mode. This call is the only way to select
+ * mode 2 (the library reads no environment). Synchronous. */
 RT_API int rt_set_triangle_pruning(rt_ctx* ctx, int mode);
+
+/* Exact variants of the launch schedule and of the acceleration structures (new, ABI 12;
+ * they were environment variables read at rt_create up to ABI 11), for A/B measurements:
+ * every setting renders the same bits as the default. Takes effect from the next launch.
+ * Keys and values (default first):
+ *   "scene_in_lds" 1|0, "lds_mode" 2|1|0 (highest LDS staging mode), "block_threads"
+ *   0|256|512|1024 (0: by occupancy), "waves_per_cu" 0..32 (0: 16), "trav_threshold" 0..63
+ *   (0: by scene), "drain_threshold" 0..63 (32), "drain_min_steps" (64), "leaf_batch" 0..8
+ *   (0: by scene), "queue_stripes" 1..64 (32), "tile_schedule" 1|0, "frame_parallel" 1|0,
+ *   "batch_overlap" 1|0, "batch_schedule" 0|1, "unit_tile_major" 1|0, "batch_memory_mb"
+ *   (an eighth of device memory), "sphere_bvh" 1|0, "sphere_leaf" 0..64 (0: default),
+ *   "sphere_octants" 1|0, "sphere_box_order" 1|0, "tri_bvh" 1|0 (0: the reference's sweep),
+ *   "tri_octants" 1|0, "tri_qnodes" 1|0, "coop_leaves" 1|0, "stage_subs" 1|0,
+ *   "primary_pass" -1|0|1 (-1: by scene), "primary_threads" 256|64|128|512|1024,
+ *   "primary_waves" 8|0, "primary_tile_major" 1|0.
+ * RT_E_INVALID for an unknown key or a value out of range. */
+RT_API int rt_set_tuning(rt_ctx* ctx, const char* key, int32_t value);
 
 /* Tile claim order (new; the reference dispatches a plain grid,
  * src/renderer.rs:238-249). 0 = tile index order. 1 = cost-ordered (the
@@ -412,11 +442,13 @@ RT_API int rt_launch_config(rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, ui
 
 /* The kernels the last rt_dispatch ran (diagnostics, ABI 7), a mask of RT_PASS_*:
  * the path kernel, the coherent primary-ray pre-pass, the batch resolve pass, or the
- * brute-force sweep kernel instead of the path kernel. */
+ * brute-force sweep kernel instead of the path kernel (with RT_PASS_BRUTE_STREAM, ABI 12:
+ * its scalar-cache variant, rt_set_brute_force mode 2). */
 #define RT_PASS_PATH 1u
 #define RT_PASS_PRIMARY 2u
 #define RT_PASS_RESOLVE 4u
 #define RT_PASS_BRUTE 8u
+#define RT_PASS_BRUTE_STREAM 16u
 RT_API int rt_last_launch_passes(rt_ctx* ctx, uint32_t* passes);
 
 /* Diagnostic counters (filled only by builds compiled with -DRT_DIAG or

@@ -121,6 +121,8 @@ SIGNATURES = {
     "rt_set_brute_force": (ctypes.c_int, [_P, ctypes.c_int]),
     "rt_set_triangle_pruning": (ctypes.c_int, [_P, ctypes.c_int]),
     "rt_streamed_bytes": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_streamed_bytes_l2": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_set_tuning": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int32]),
     "rt_set_tile_schedule": (ctypes.c_int, [_P, _U32]),
     "rt_tile_schedule_state": (ctypes.c_int, [_P, _P, _P]),
     "rt_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
@@ -186,6 +188,7 @@ SIGNATURES = {
 }
 
 RT_DEFAULT_FRAME_BATCH = 16  # include/rt_abi.h (ABI 11)
+RT_PASS_PATH, RT_PASS_PRIMARY, RT_PASS_RESOLVE, RT_PASS_BRUTE, RT_PASS_BRUTE_STREAM = 1, 2, 4, 8, 16
 RT_GROUP_COPY_TRANSPORT = 1  # rt_create_multi_ex flags
 RT_GATHER_IMAGE = 0
 RT_GATHER_ACCUMULATION = 1

@@ -65,22 +65,10 @@ struct SceneView {
     const float4* tri_nodes;  // triangle accelerator nodes (LDS in mode 2, else global)
     const uint4* tri_prims;   // triangle accelerator leaves: object, sub-object, sweep position
     float tri_extent;         // triangle margin scale (device memory: a device refit updates it)
-    // the 4-wide accelerator (kWide instances, tri_wide.h)
-    const float4* tri_wide;   // nodes (LDS in mode 2, else global)
-    uint32_t* stk;            // this lane's walk stack in LDS: entry e at stk[e * stk_stride]
-    uint32_t stk_stride;
     const RtSubObject* sub;   // sub-object records (LDS in mode 2 when they fit, else global)
     // the quantized triangle nodes (modes 0/1; null: the 32-B nodes) and their grid
     const uint4* tri_q;
     float qox, qoy, qoz, qsx, qsy, qsz;
-    // mode 2: the vertex-indexed triangles in LDS (null: the 64-B records), and whether the
-    // leaves then test their sub-object lazily (the records not staged)
-    const float4* cverts;
-    const uint16_t* cidx;
-    bool lazy_sub;
-    // the 4-wide quantized accelerator (tri_q4.h; null: the binary walk), decoded on the grid above;
-    // its per-lane stack is `stk` (entry e at stk[e * stk_stride])
-    const uint4* tri_q4;
 };
 
 __device__ __forceinline__ f3 ld3(const float4& v) { return mk(v.x, v.y, v.z); }
@@ -192,37 +180,12 @@ __device__ __forceinline__ TriGeom load_tri(const RtTriangleHot* __restrict__ t,
     return TriGeom{mk(p0.x, p0.y, p0.z), mk(p0.w, p1.x, p1.y), mk(p1.z, p1.w, p2.x), mk(p2.y, p2.z, p2.w)};
 }
 
-// Leaf certificates in the walks (certified pruning, tri_leaf_skips): walks from global memory
-// always carry the test; walks of the LDS-resident accelerator (mode 2) only when built with
-// RT_LEAFCERT_LDS=1. Off by default: the code costs the LDS-resident instances registers, more
-// than the triangle tests it skips save (C3 0.304 ms per frame without it, 0.335 compiled in
-// and off, 0.362 on; a variant testing at the leaf with the certificates staged in LDS measured
-// 0.297 compiled in and off, 0.312 on, against 0.269). Mode 2 then walks with
-// box culling, exact without any bound.
-#ifndef RT_LEAFCERT_LDS
-#define RT_LEAFCERT_LDS 0
-#endif
-// Walks from global memory: the certificate test made in the leaf batch (node_step records the
-// leaf box's gap beyond the best hit, one more VGPR) instead of in node_step, where every wave
-// step paid for the seven normals of whichever lane met a certified leaf (C5 11.08 -> 10.81 ms
-// per frame, 10.71 with leaf batches at 4/8; profiles/r04/r04_k). RT_LEAFCERT_DEFER=0: in node_step.
-#ifndef RT_LEAFCERT_DEFER
-#define RT_LEAFCERT_DEFER 1
-#endif
-// RT_LDS_COMPACT (the LDS vertex table's build switch) is defined in rt_kernel_args.h, where the
-// host sees it too.
-// A triangle from the LDS vertex table (mode 2): edge_ab, edge_ac and calc_normal recomputed
-// with SceneTriangle::new's f32 operations (src/buffers.rs:66-95; tri_wide.h
-// wide_tri_from_vertices) -- the record's own bits, checked for every triangle when the table
-// was built (rt_abi.cpp build_compact_triangles), so the test sees exactly the stored values.
-__device__ __forceinline__ TriGeom compact_tri(const SceneView& sv, uint32_t ti) {
-    const uint16_t* ix = sv.cidx + 3u * ti;
-    const float4 va = sv.cverts[ix[0]], vb = sv.cverts[ix[1]], vc = sv.cverts[ix[2]];
-    const f3 ab = mk(vb.x - va.x, vb.y - va.y, vb.z - va.z);
-    const f3 ac = mk(vc.x - va.x, vc.y - va.y, vc.z - va.z);
-    const f3 cn = mk(ab.y * ac.z - ab.z * ac.y, ab.z * ac.x - ab.x * ac.z, ab.x * ac.y - ab.y * ac.x);
-    return TriGeom{mk(va.x, va.y, va.z), ab, ac, cn};
-}
+// Leaf certificates (certified pruning) are read by the walks from global memory
+// only: node_step records the gap of a leaf box entered beyond the best hit, and the leaf batch
+// tests the leaf's certificate with it (C5 11.08 -> 10.81 ms per frame against testing in
+// node_step, profiles/r04/r04_k). The LDS-resident walk (mode 2) culls by box alone, exact
+// without any bound: the certificate code cost its instances more registers than the triangle
+// tests it skipped (C3 0.304 -> 0.335 ms per frame compiled in and off).
 
 // check_triangles, compute_shader.wgsl:422-517: the reference's own sweep over
 // objects -> sub-objects -> triangles (first wins on equal distance, `>=`
@@ -291,12 +254,8 @@ struct TraceState {
     float limit;      // pruning distance: min(best sphere, triangle hit) * 1.00001 + slack (inf: none)
     uint32_t node;
     uint32_t phase;
-    uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf;
-                       // wide walk: leaf_base << 4 | mask of the node's leaves still to test
-    uint32_t sp;       // wide walk: stack entries in use
-#if RT_LEAFCERT_DEFER
+    uint32_t pending;  // postponed leaf (sphere group slot / triangle prim), or kNoLeaf
     float cert_gap;    // deferred leaf certificate test (pending bit 24): the leaf box's gap beyond the best hit
-#endif
     bool nan_hit;
     SphereHit sph;
     TriHit tri;
@@ -329,7 +288,8 @@ __device__ __forceinline__ float tri_limit(const SceneView& sv, const KernelArgs
 // triangle, that the reference's test (:449-481) cannot accept it at a distance <= tb; those
 // triangles are skipped without being loaded, and the whole leaf when all are. Returns the mask
 // of skipped triangles (kLeafCertAll: the leaf). The per-axis entries are the culling slab
-// test's own (rt_bvh_slab.h) on the box as the walk decoded it.
+// test's own (rt_bvh_slab.h) on the box as the walk decoded it. (The path kernel's walk defers
+// this test to its leaf batch, tri_leafcert_skips_gap; the primary pre-pass tests on the spot.)
 __device__ __forceinline__ uint32_t tri_leaf_skips(const KernelArgs& ka, uint32_t prim, const SlabRay& sr, f3 o, f3 d,
                                                    float tb, float4 lo, float4 hi) {
     const uint4* rec = reinterpret_cast<const uint4*>(ka.tri_leafcert + prim);
@@ -361,8 +321,7 @@ __device__ __forceinline__ void phase_setup(const SceneView& sv, const KernelArg
     if (kTris && phase == 0) {  // the accelerator layout ordered for this ray's direction octant (global walks)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
                              ((__float_as_uint(ts.inv.z) >> 31) << 2);
-        ts.node = (kQ4Built && sv.tri_q4) ? 0u : oct * ka.tri_octant_stride;  // the 4-wide walk starts at its root
-        ts.sp = 0u;
+        ts.node = oct * ka.tri_octant_stride;
     }
     if (phase == 1) {  // the sphere BVH layout ordered for this ray's direction octant (sphere_bvh.h)
         const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
@@ -395,7 +354,6 @@ __device__ __forceinline__ void trace_begin(const SceneView& sv, const KernelArg
     ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
     ts.nan_hit = false;
     ts.node = 0;
-    ts.sp = 0;
     ts.pending = kNoLeaf;
     // brute-force sphere set: wave-uniform sweep over groups of 4, then the rest
     // one by one (a sphere's own test is exact, so the visiting order is free)
@@ -437,7 +395,6 @@ template <bool kLazySub = false>
 __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
                                          uint32_t pending) {
     const uint32_t prim = pending & 0xffffffu;
-#if RT_LEAFCERT_DEFER
     uint32_t skip = 0u;
     if ((pending >> 24) & 1u) {  // the certificate test deferred by node_step
         const uint4* rec = reinterpret_cast<const uint4*>(ka.tri_leafcert + prim);
@@ -446,15 +403,12 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         skip = tri_leafcert_skips_gap(w, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), ts.tri.t, ts.cert_gap);
         if (skip == kLeafCertAll) return;
     }
-#else
-    const uint32_t skip = pending >> 24;
-#endif
     const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base, range
     const RtObject& ob = sv.obj[pr.x];
     if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) return;
     uint32_t first, count;
     int sub_state;  // 1: passed, 0: not tested yet
-    if ((kLazySub || (RT_LDS_COMPACT && sv.lazy_sub)) && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
+    if (kLazySub && pr.w != 0xffffffffu) {  // kPrimRangeNone (sphere_bvh.h)
         first = pr.w & ((1u << 27) - 1u);
         count = pr.w >> 27;
         sub_state = 0;
@@ -469,7 +423,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         if ((skip >> j) & 1u) continue;
         const uint32_t ti = min(first + j, ka.triangle_count - 1u);
         const uint32_t seq = pr.z + j;
-        const TriGeom g = (RT_LDS_COMPACT && sv.cidx) ? compact_tri(sv, ti) : load_tri(ka.triangles, ti);
+        const TriGeom g = load_tri(ka.triangles, ti);
         const float det = -dot(d, g.cn);
         const float inv_det = 1.0f / det;
         const f3 ao = o - g.a;
@@ -484,7 +438,7 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
         if (u < 0.0f) continue;
         const float w = 1.0f - u - v;
         if (w < 0.0f) continue;
-        if ((kLazySub || (RT_LDS_COMPACT && sv.lazy_sub)) && sub_state == 0) {
+        if (kLazySub && sub_state == 0) {
             const RtSubObject sub = sv.sub[pr.y];
             if (!ray_in_bounds(o, ts.inv, sub.min_bounds, sub.max_bounds)) return;
             sub_state = 1;
@@ -497,73 +451,6 @@ __device__ __forceinline__ void tri_leaf(const SceneView& sv, const KernelArgs& 
     }
 }
 
-// A leaf of the 4-wide accelerator (tri_wide.h): the reference's object and
-// sub-object ray_in_bounds tests (:431, :441) and its triangle tests (:445-500)
-// for one record of a sub-object's triangles. Compact records recompute each
-// triangle's a, edge_ab, edge_ac and calc_normal from their vertex block with
-// SceneTriangle::new's f32 operations (src/buffers.rs:66-95) -- the record's own
-// bits, verified when the block was built -- so the tests below see exactly the
-// values the triangle buffer holds.
-__device__ __forceinline__ void tri_leaf_wide(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
-                                              uint32_t leaf) {
-    const uint4* lf = ka.tri_leaves + 4u * leaf;
-    const uint4 q0 = lf[0], q1 = lf[1], q2 = lf[2], q3 = lf[3];  // mn first | mx seq | obj count vbase sub | idx
-    const RtObject& ob = sv.obj[q2.x];
-    const float mn[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-    const float mx[3] = {__uint_as_float(q1.x), __uint_as_float(q1.y), __uint_as_float(q1.z)};
-    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds) || !ray_in_bounds(o, ts.inv, mn, mx)) return;
-    const uint32_t count = q2.y & 0xffu;
-    const bool compact = (q2.y & kWideLeafCompact) != 0u;
-    uint64_t iw0 = (uint64_t)q3.x | ((uint64_t)q3.y << 32), iw1 = (uint64_t)q3.z | ((uint64_t)q3.w << 32);
-    for (uint32_t j = 0; j < count; ++j) {
-        TriGeom g;
-        if (compact) {
-            const TriVertex* vb = ka.tri_verts + q2.z;
-            const TriVertex va = vb[iw0 & 0xfu], vv = vb[(iw0 >> 4) & 0xfu], vc = vb[(iw0 >> 8) & 0xfu];
-            iw0 = (iw0 >> 12) | (iw1 << 52);
-            iw1 >>= 12;
-            float ab[3], ac[3], cn[3];
-            wide_tri_from_vertices(va, vv, vc, ab, ac, cn);
-            g = TriGeom{mk(va.x, va.y, va.z), mk(ab[0], ab[1], ab[2]), mk(ac[0], ac[1], ac[2]), mk(cn[0], cn[1], cn[2])};
-        } else {
-            g = load_tri(ka.triangles, min(q0.w + j, ka.triangle_count - 1u));
-        }
-        const uint32_t seq = q1.w + j;
-        const float det = -dot(d, g.cn);
-        const float inv_det = 1.0f / det;
-        const f3 ao = o - g.a;
-        const float dist = dot(ao, g.cn) * inv_det;
-        const bool nan_dist = dist != dist;
-        if (dist < 0.0f) continue;
-        if (!nan_dist && !(dist < ts.tri.t || (dist == ts.tri.t && seq < ts.tri.seq))) continue;
-        const f3 dao = cross(ao, d);
-        const float v = -dot(g.ab, dao) * inv_det;
-        if (v < 0.0f) continue;
-        const float u = dot(g.ac, dao) * inv_det;
-        if (u < 0.0f) continue;
-        const float w = 1.0f - u - v;
-        if (w < 0.0f) continue;
-        if (nan_dist) {
-            ts.nan_hit = true;
-            continue;
-        }
-        ts.tri = TriHit{dist, seq, min(q0.w + j, ka.triangle_count - 1u), q2.x, det > 0.0f};
-    }
-}
-
-// ---- the 4-wide quantized walk (tri_q4.h) --------------------------------
-// One 64-B node per step: its four child boxes decoded on the grid and tested with the ray's
-// culling slab (rt_bvh_slab.h, the binary walk's margin), the hit children ordered by entry
-// distance (a 5-exchange sorting network), the nearest taken next and the others pushed on the
-// lane's LDS stack, farthest first. A hit leaf is deferred to the wave's leaf batch
-// (ts.pending) with its certified gap beyond the best hit measured now, from the child's box
-// (node_step's test: the leaf batch runs tri_leafcert_skips_gap); a leaf waiting on the stack
-// carries that gap in 11 bits (tri_q4.h q4_gap_code, a lower bound). A lane whose leaf is still
-// deferred when it pops another leaf waits until the batch. A push beyond kQ4StackEntries
-// restarts the lane on the binary walk (ts.sp = kQ4Binary), which is complete and merges into
-// the same lexicographic minimum.
-constexpr uint32_t kQ4Binary = 0x80000000u;  // TraceState::sp: this walk fell back to the binary tree
-
 // The lane's index in its wave, computed where it is used: an opaque value, so that the compiler
 // does not hoist it (and what is derived from it) out of the traversal loop into a register
 // held across every node step.
@@ -573,201 +460,12 @@ __device__ __forceinline__ uint32_t lane_id_here() {
     return l;
 }
 
-// The dynamic LDS of the kernel (the same block as the kernels' own extern declaration).
-extern __shared__ __attribute__((aligned(16))) unsigned char rt_dyn_lds[];
-
-// Entry `e` of this lane's 4-wide walk stack (lane-interleaved: entry e of thread t at
-// [e * threads + t]), addressed from the thread index where it is used rather than a pointer held
-// in a register across the walk (the walk's instances are at their VGPR limit).
-__device__ __forceinline__ uint32_t* q4_stack_entry(const KernelArgs& ka, uint32_t e) {
-    const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u) + lane_id_here();
-    return reinterpret_cast<uint32_t*>(rt_dyn_lds + ka.lds_q4stack_offset) + e * blockDim.x + t;
-}
-
-__device__ __forceinline__ void q4_child(const SceneView& sv, const KernelArgs& ka, f3 d, const TraceState& ts,
-                                         uint32_t w0, uint32_t w1, uint32_t w2, uint32_t ref, float& key,
-                                         uint32_t& ent) {
-    const float lx = fmaf((float)(w0 & 0xffffu), sv.qsx, sv.qox), ly = fmaf((float)(w0 >> 16), sv.qsy, sv.qoy);
-    const float lz = fmaf((float)(w1 & 0xffffu), sv.qsz, sv.qoz), hx = fmaf((float)(w1 >> 16), sv.qsx, sv.qox);
-    const float hy = fmaf((float)(w2 & 0xffffu), sv.qsy, sv.qoy), hz = fmaf((float)(w2 >> 16), sv.qsz, sv.qoz);
-    float t1x, t1y, t1z, far_t;
-    slab_hit_axes(ts.slab, lx, ly, lz, hx, hy, hz, t1x, t1y, t1z, far_t);
-    const float near_t = fmaxf(fmaxf(t1x, t1y), t1z);  // slab_hit's near_t
-    const bool hit = ref != kQ4Empty && near_t <= far_t && far_t >= 0.0f;
-    key = hit ? near_t : __builtin_inff();
-    ent = ref;
-    if (hit && (ref & kQ4Leaf) && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max) {
-        // the leaf box's gap beyond the best hit (node_step's, pathtrace.hip RT_LEAFCERT_DEFER)
-        const float tbs = ts.tri.t * (1.0f + 0x1p-20f);
-        const float gx = (t1x - tbs) * fabsf(d.x), gy = (t1y - tbs) * fabsf(d.y), gz = (t1z - tbs) * fabsf(d.z);
-        ent = ref | (q4_gap_code(fmaxf(fmaxf(gx, gy), gz) * (1.0f - 0x1p-20f)) << 20);
-    }
-}
-
-// A leaf entry into the deferred slot (the caller checked it is free).
-__device__ __forceinline__ void q4_defer_leaf(TraceState& ts, uint32_t e) {
-#if RT_LEAFCERT_DEFER
-    const uint32_t code = (e >> 20) & 0x7ffu;
-    ts.pending = (e & 0xfffffu) | (code != 0u ? (1u << 24) : 0u);  // bit 24: test the certificate in the batch
-    ts.cert_gap = q4_gap_decode(code);
-#else
-    ts.pending = e & 0xfffffu;  // (bits 24-30 would be a skip mask in this build: no certificate test)
-#endif
-}
-
-__device__ __forceinline__ void q4_fallback(const KernelArgs& ka, TraceState& ts) {
-    // the binary walk from the start of the ray's octant layout (phase_setup's)
-    const uint32_t oct = (__float_as_uint(ts.inv.x) >> 31) | ((__float_as_uint(ts.inv.y) >> 31) << 1) |
-                         ((__float_as_uint(ts.inv.z) >> 31) << 2);
-    ts.node = oct * ka.tri_octant_stride;
-    ts.sp = kQ4Binary;
-}
-
-__device__ __forceinline__ void q4_node_step(const SceneView& sv, const KernelArgs& ka, f3 d, TraceState& ts) {
-    uint32_t n = ts.node;
-    if (n == kQ4None) {
-        if (ts.sp == 0u) return;  // walk over (phase_end)
-        const uint32_t e = *q4_stack_entry(ka, ts.sp - 1u);
-        if (e & kQ4Leaf) {
-            if (ts.pending != kNoLeaf) return;  // blocked until the batch tests the deferred leaf
-            q4_defer_leaf(ts, e);
-            ts.sp -= 1u;
-            return;
-        }
-        n = e;
-        ts.sp -= 1u;
-    }
-    const uint4* nd = sv.tri_q4 + 4u * n;
-    const uint4 b0 = nd[0], b1 = nd[1], b2 = nd[2], rf = nd[3];
-    float k0, k1, k2, k3;
-    uint32_t e0, e1, e2, e3;
-    q4_child(sv, ka, d, ts, b0.x, b0.y, b0.z, rf.x, k0, e0);
-    q4_child(sv, ka, d, ts, b0.w, b1.x, b1.y, rf.y, k1, e1);
-    q4_child(sv, ka, d, ts, b1.z, b1.w, b2.x, rf.z, k2, e2);
-    q4_child(sv, ka, d, ts, b2.y, b2.z, b2.w, rf.w, k3, e3);
-    // nearest first: misses (inf) sort last
-#define RT_Q4_CX(ka_, ea_, kb_, eb_)               \
-    {                                               \
-        const bool sw = kb_ < ka_;                  \
-        const float tk = sw ? kb_ : ka_;            \
-        kb_ = sw ? ka_ : kb_;                       \
-        ka_ = tk;                                   \
-        const uint32_t te = sw ? eb_ : ea_;         \
-        eb_ = sw ? ea_ : eb_;                       \
-        ea_ = te;                                   \
-    }
-    RT_Q4_CX(k0, e0, k1, e1)
-    RT_Q4_CX(k2, e2, k3, e3)
-    RT_Q4_CX(k0, e0, k2, e2)
-    RT_Q4_CX(k1, e1, k3, e3)
-    RT_Q4_CX(k1, e1, k2, e2)
-#undef RT_Q4_CX
-    ts.node = kQ4None;
-    if (k0 == __builtin_inff()) return;  // no child hit
-    const uint32_t n_push = (k1 != __builtin_inff() ? 1u : 0u) + (k2 != __builtin_inff() ? 1u : 0u) +
-                            (k3 != __builtin_inff() ? 1u : 0u);
-    // the nearest child: a leaf that cannot be deferred now waits on the stack too
-    const bool e0_waits = (e0 & kQ4Leaf) && ts.pending != kNoLeaf;
-    if (ts.sp + n_push + (e0_waits ? 1u : 0u) > kQ4StackEntries) {
-        q4_fallback(ka, ts);
-        return;
-    }
-    uint32_t* st = q4_stack_entry(ka, ts.sp);
-    const uint32_t stride = blockDim.x;
-    if (n_push == 3u) {
-        st[0] = e3;
-        st += stride;
-    }
-    if (n_push >= 2u) {
-        st[0] = e2;
-        st += stride;
-    }
-    if (n_push >= 1u) {
-        st[0] = e1;
-        st += stride;
-    }
-    ts.sp += n_push;
-    if (!(e0 & kQ4Leaf)) {
-        ts.node = e0;
-    } else if (e0_waits) {
-        st[0] = e0;
-        ts.sp += 1u;
-    } else {
-        q4_defer_leaf(ts, e0);
-    }
-}
-
-// One node of the 4-wide walk (tri_wide.h): the four child boxes, inflated by the
-// ray's margin, tested together (rt_bvh_slab.h). Hit leaves are deferred to the
-// wave's leaf batches (ts.pending: the node's leaf records still to test); the
-// first hit internal child is visited next and the others wait on the lane's LDS
-// stack as one entry (first child, mask). A lane whose leaves are still pending
-// when it reaches another node with hit leaves stays on that node (marked
-// kWideBlocked, so it is not reloaded) until the batch has tested them.
-constexpr uint32_t kWideNone = 0xffffffffu;
-constexpr uint32_t kWideBlocked = 0x80000000u;
-
-__device__ __forceinline__ void wide_node_step(const SceneView& sv, TraceState& ts) {
-    uint32_t n = ts.node;
-    if (n != kWideNone && (n & kWideBlocked)) {
-        if (ts.pending != kNoLeaf) return;
-        n &= ~kWideBlocked;
-    }
-    if (n == kWideNone) {
-        if (ts.sp == 0u) return;  // walk over (phase_end)
-        const uint32_t at = (ts.sp - 1u) * sv.stk_stride;
-        uint32_t e = sv.stk[at];
-        n = (e >> 4) + (uint32_t)__builtin_ctz(e & 0xfu);
-        e &= e - 1u;  // the lowest set bit is the mask's
-        if ((e & 0xfu) == 0u)
-            ts.sp -= 1u;
-        else
-            sv.stk[at] = e;
-    }
-    const float4* nd = sv.tri_wide + 8u * n;
-    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-    const uint4 meta = reinterpret_cast<const uint4*>(nd)[6];  // child_base, leaf_base, slots
-    const uint32_t n_int = meta.z & 0xfu, n_slots = n_int + ((meta.z >> 4) & 0xfu);
-    uint32_t hit = 0;
-    float nt, ft;
-    slab_hit(ts.slab, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, nt, ft);
-    hit |= (nt <= ft && ft >= 0.0f) ? 1u : 0u;
-    slab_hit(ts.slab, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, nt, ft);
-    hit |= (nt <= ft && ft >= 0.0f) ? 2u : 0u;
-    slab_hit(ts.slab, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, nt, ft);
-    hit |= (nt <= ft && ft >= 0.0f) ? 4u : 0u;
-    slab_hit(ts.slab, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, nt, ft);
-    hit |= (nt <= ft && ft >= 0.0f) ? 8u : 0u;
-    hit &= (1u << n_slots) - 1u;
-    const uint32_t hl = hit >> n_int;                   // leaf ranks
-    const uint32_t hi = hit & ((1u << n_int) - 1u);     // internal ranks
-    if (hl != 0u) {
-        if (ts.pending != kNoLeaf) {
-            ts.node = n | kWideBlocked;
-            return;
-        }
-        ts.pending = (meta.y << 4) | hl;
-    }
-    if (hi != 0u) {
-        ts.node = meta.x + (uint32_t)__builtin_ctz(hi);
-        const uint32_t rest = hi & (hi - 1u);
-        if (rest != 0u) {
-            sv.stk[ts.sp * sv.stk_stride] = (meta.x << 4) | rest;
-            ts.sp += 1u;
-        }
-    } else {
-        ts.node = kWideNone;
-    }
-}
-
 // Ends the current BVH walk once its nodes are exhausted and no leaf is pending.
-template <bool kTris, bool kWide = false>
+template <bool kTris>
 __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     if (ts.pending != kNoLeaf) return;
     if (kTris && ts.phase == 0) {
-        if (kWide ? (ts.node != kWideNone || ts.sp != 0u)
-                  : (kQ4Built && sv.tri_q4 && ts.sp != kQ4Binary) ? (ts.node != kQ4None || ts.sp != 0u) : (ts.node < ka.tri_nodes))
-            return;
+        if (ts.node < ka.tri_nodes) return;
 #ifdef RT_DIAG_TAIL
         if (ts.nan_hit) atomicAdd(ka.diag + 6, 1ull);
 #endif
@@ -790,49 +488,25 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
 // is the lexicographic minimum over the tested primitives either way.
 // Sphere-only scenes test a group on the spot (kDeferLeaves false): deferring
 // measured slower there.
-#ifndef RT_SPHERE_DEFER
-#define RT_SPHERE_DEFER 0
-#endif
 template <bool kTris>
-constexpr bool kDeferLeaves = kTris || RT_SPHERE_DEFER;
+constexpr bool kDeferLeaves = kTris;
 // Node steps per wave-wide check of the traversal loop (the ballots of the
 // threshold and leaf-batch tests, exec-mask updates). Lanes that finish inside
 // the group idle for its remaining steps; the visit order is unchanged.
-// Measured (RT_TRAV_UNROLL / _TRI = 1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%. Round 4, per
-// accelerator placement (profiles/r04/r04_z): global-memory walks 3 -> 4 / 5 / 6: C5 -4.0% /
-// -4.3% / -1.6%; LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%; sphere walks 2 or 4: C2
-// +1.5% / +0.8%.
-#ifndef RT_TRAV_UNROLL
-#define RT_TRAV_UNROLL 3
-#endif
-#ifndef RT_TRAV_UNROLL_TRI  // triangle scenes, accelerator in global memory (modes 0, 1)
-#define RT_TRAV_UNROLL_TRI 5
-#endif
-#ifndef RT_TRAV_UNROLL_LDS  // triangle scenes, accelerator in LDS (mode 2)
-#define RT_TRAV_UNROLL_LDS 2
-#endif
+// Measured (1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%. Round 4, per accelerator placement
+// (profiles/r04/r04_z): global-memory walks 3 -> 4 / 5 / 6: C5 -4.0% / -4.3% / -1.6%;
+// LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%; sphere walks 2 or 4: C2 +1.5% / +0.8%.
 template <int kMode, bool kTris>
-constexpr int kTravUnroll = !kTris ? RT_TRAV_UNROLL : kMode <= 1 ? RT_TRAV_UNROLL_TRI : RT_TRAV_UNROLL_LDS;
+constexpr int kTravUnroll = !kTris ? 3 : kMode <= 1 ? 5 : 2;
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
 template <int kMode, bool kTris>
 constexpr bool kDrainDecouple = kTris && kMode < 2;
 
+// Walks that read leaf certificates: from global memory only (see tri_leaf).
 template <int kMode>
-constexpr bool kCertWalk = kMode <= 1 || RT_LEAFCERT_LDS == 1;
-
-
-// Node pairs (walks from global memory over the 16-B quantized nodes): a step loads node n and
-// node n + 1 together (adjacent 16 B, one round trip) and, when the walk's next node is n + 1 --
-// after a leaf, hit or not (its skip link is n + 1), or after entering an internal node (its
-// first child) -- visits it in the same step with the data it already has. The visit order and
-// every test are unchanged; a descent takes one memory round trip per two nodes. Measured on C5
-// (one process): 15.63 ms per frame at the default 5 steps per check (the unrolled pairs cost
-// more than they save), 13.75 at 3, against 13.88 without pairs -- within noise, so off.
-#ifndef RT_NODE_PAIRS
-#define RT_NODE_PAIRS 0
-#endif
+constexpr bool kCertWalk = kMode <= 1;
 
 // A 16-B quantized node decoded (tri_qnode.h): the box exactly (a superset of the 32-B node's
 // box), lo.w = the skip link (a leaf's: node + 1, or the end), hi.w = the leaf record or none.
@@ -849,7 +523,7 @@ __device__ __forceinline__ void qnode_decode(const SceneView& sv, uint4 q, uint3
 
 // One node's visit, given its box and links: the box test, the deferred leaf or the sphere
 // group, the next node.
-template <bool kTris, bool kWide, bool kCert>
+template <bool kTris, bool kCert>
 __device__ __forceinline__ void node_visit(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
                                            bool tri, float4 lo, float4 hi) {
     float near_t, far_t;
@@ -861,32 +535,21 @@ __device__ __forceinline__ void node_visit(const SceneView& sv, const KernelArgs
     // side also not beyond the best sphere or the triangle hit (a sphere wins
     // only when strictly closer, :347); ts.slack / ts.limit are 0 / inf on the
     // triangle side
-    bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
+    const bool hit = near_t <= far_t && far_t >= -ts.slack && near_t <= ts.limit;
     const uint32_t leaf = __float_as_uint(hi.w);
     uint32_t skip = 0u;
-    if constexpr (kTris && !kWide && kCert) {
-        // certified pruning: a leaf whose box is entered beyond the best triangle hit
-        if (tri && hit && leaf != 0xffffffffu && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max) {
-#if RT_LEAFCERT_DEFER
-            // the gap of the leaf box beyond the best hit, for the leaf batch's certificate test
-            if (ts.pending == kNoLeaf) {
-                const float tbs = ts.tri.t * (1.0f + 0x1p-20f);
-                const SlabRay& sr = ts.slab;
-                const float gx = (fminf(fmaf(lo.x, sr.ix, sr.lx), fmaf(hi.x, sr.ix, sr.hx)) - tbs) * fabsf(d.x);
-                const float gy = (fminf(fmaf(lo.y, sr.iy, sr.ly), fmaf(hi.y, sr.iy, sr.hy)) - tbs) * fabsf(d.y);
-                const float gz = (fminf(fmaf(lo.z, sr.iz, sr.lz), fmaf(hi.z, sr.iz, sr.hz)) - tbs) * fabsf(d.z);
-                ts.cert_gap = fmaxf(fmaxf(gx, gy), gz) * (1.0f - 0x1p-20f);
-                skip = ts.cert_gap > 0.0f ? 1u : 0u;  // (bit 24 of pending: test deferred)
-            }
-#else
-            skip = tri_leaf_skips(ka, leaf & 0xffffffu, ts.slab, o, d, ts.tri.t, lo, hi);
-            if (skip == kLeafCertAll) hit = false;
-#endif
-#ifdef RT_DIAG
-            atomicAdd(ka.diag + 19, 1ull);  // certificate checks, leaves skipped, triangles skipped
-            if (skip == kLeafCertAll) atomicAdd(ka.diag + 20, 1ull);
-            atomicAdd(ka.diag + 21, (unsigned long long)__popc(skip));
-#endif
+    if constexpr (kTris && kCert) {
+        // certified pruning: a leaf whose box is entered beyond the best triangle hit records
+        // the gap of its box beyond that hit, for the leaf batch's certificate test
+        if (tri && hit && leaf != 0xffffffffu && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max &&
+            ts.pending == kNoLeaf) {
+            const float tbs = ts.tri.t * (1.0f + 0x1p-20f);
+            const SlabRay& sr = ts.slab;
+            const float gx = (fminf(fmaf(lo.x, sr.ix, sr.lx), fmaf(hi.x, sr.ix, sr.hx)) - tbs) * fabsf(d.x);
+            const float gy = (fminf(fmaf(lo.y, sr.iy, sr.ly), fmaf(hi.y, sr.iy, sr.hy)) - tbs) * fabsf(d.y);
+            const float gz = (fminf(fmaf(lo.z, sr.iz, sr.lz), fmaf(hi.z, sr.iz, sr.hz)) - tbs) * fabsf(d.z);
+            ts.cert_gap = fmaxf(fmaxf(gx, gy), gz) * (1.0f - 0x1p-20f);
+            skip = ts.cert_gap > 0.0f ? 1u : 0u;  // (bit 24 of pending: test deferred)
         }
     }
     const bool at_leaf = hit && leaf != 0xffffffffu;
@@ -913,59 +576,29 @@ __device__ __forceinline__ void node_visit(const SceneView& sv, const KernelArgs
     ts.node = (hit && !at_leaf) ? ts.node + 1u : __float_as_uint(lo.w);
 }
 
-// kCert: the walk reads leaf certificates (tri_leaf_skips) when ka.tri_leafcert is set.
-template <bool kTris, bool kWide = false, bool kCert = true>
+// kCert: the walk records leaf-certificate gaps (node_visit) when ka.tri_leafcert is set.
+template <bool kTris, bool kCert = true>
 __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
     const bool tri = kTris && ts.phase == 0;
-    if (kWide && tri) {
-        wide_node_step(sv, ts);
-        return;
-    }
-    if constexpr (kTris && !kWide) {
-        if (kQ4Built && tri && sv.tri_q4 && ts.sp != kQ4Binary) {
-            q4_node_step(sv, ka, d, ts);
-            return;
-        }
-    }
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
     float4 lo, hi;
-    if (kTris && !kWide && tri && sv.tri_q) {
-        const uint32_t n = ts.node;
-        const uint4 q = sv.tri_q[n];
-        if (RT_NODE_PAIRS && n + 1u < ka.tri_nodes) {
-            const uint4 q1 = sv.tri_q[n + 1u];  // with node n: the same round trip
-            qnode_decode(sv, q, n, lo, hi);
-            node_visit<kTris, kWide, kCert>(sv, ka, o, d, ts, tri, lo, hi);
-            if (ts.node != n + 1u) return;  // a skip (or blocked at a leaf): node n + 1 is not next
-            qnode_decode(sv, q1, n + 1u, lo, hi);
-        } else {
-            qnode_decode(sv, q, n, lo, hi);
-        }
+    if (kTris && tri && sv.tri_q) {
+        qnode_decode(sv, sv.tri_q[ts.node], ts.node, lo, hi);
     } else {
         const float4* nodes = tri ? sv.tri_nodes : sv.nodes;
         lo = nodes[2u * ts.node];
         hi = nodes[2u * ts.node + 1u];
     }
-    node_visit<kTris, kWide, kCert>(sv, ka, o, d, ts, tri, lo, hi);
+    node_visit<kTris, kCert>(sv, ka, o, d, ts, tri, lo, hi);
 }
 
-template <bool kTris, bool kWide = false, bool kLazySub = false>
+template <bool kTris, bool kLazySub = false>
 __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts) {
-    if (kWide && kTris && ts.phase == 0) {
-        // one of the node's pending leaf records per batch
-        const uint32_t m = ts.pending & 0xfu;
-        const uint32_t leaf = (ts.pending >> 4) + (uint32_t)__builtin_ctz(m);
-        const uint32_t rest = m & (m - 1u);
-        ts.pending = rest ? ((ts.pending & ~0xfu) | rest) : kNoLeaf;
-        tri_leaf_wide(sv, ka, o, d, ts, leaf);
-        return;
-    }
     if (kTris && ts.phase == 0) {
         tri_leaf<kLazySub>(sv, ka, o, d, ts, ts.pending);
         ts.limit = tri_limit(sv, ka, o, ts);
-    } else
-    {
+    } else {
         test_sphere_group(sv, ts.pending, o, d, ts.a4, ts.a2, ts.sph);
         ts.limit = prune_limit(ts);
     }
@@ -989,23 +622,8 @@ __device__ __forceinline__ void leaf_step(const SceneView& sv, const KernelArgs&
 // counts; else the NaN flag and the best candidate are taken. (Within a leaf the sequential
 // loop's result is that minimum: a candidate's test does not depend on the running best other
 // than through "distance < best", which is the minimum's own comparison.)
-#ifndef RT_COOP_LEAVES
-#define RT_COOP_LEAVES 1
-#endif
-template <int kMode, bool kTris, bool kWide>
-constexpr bool kCoopLeaves = RT_COOP_LEAVES && kTris && !kWide && kMode <= 1;
-
-// Refill from a per-tile prologue: when a wave takes a tile, lane l computes slot l's pixel,
-// camera ray and the sample's start (start_sample: seed, jittered direction) with the whole wave
-// active, and a refilling lane fetches its slot's values with ds_bpermute instead of computing
-// them alone (RT_REFILL_PREP=1 builds; sphere-only instances). Measured slower, so off: C2
-// 0.2862 -> 0.3172 ms per frame, C1 0.0186 -> 0.0194 (profiles/r05/refill_prep_ab_*.json): the
-// refill's per-lane arithmetic is not what its share of the wave cycles pays for.
-#ifndef RT_REFILL_PREP
-#define RT_REFILL_PREP 0
-#endif
-template <bool kTris>
-constexpr bool kRefillPrep = RT_REFILL_PREP && !kTris;
+template <int kMode, bool kTris>
+constexpr bool kCoopLeaves = kTris && kMode <= 1;
 
 // LDS written by some lanes of a wave and read by others: the wave's LDS operations complete in
 // order, so only the compiler must not move them across this point.
@@ -1037,14 +655,12 @@ __device__ __forceinline__ void coop_leaf_batch(const SceneView& sv, const Kerne
         if (ts.phase == 0) {
             prim = ts.pending & 0xffffffu;
             uint32_t skip = 0u;
-#if RT_LEAFCERT_DEFER
             if ((ts.pending >> 24) & 1u) {  // the certificate test deferred by node_step
                 const uint4* rec = reinterpret_cast<const uint4*>(ka.tri_leafcert + prim);
                 const uint4 c0 = rec[0], c1 = rec[1];
                 const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
                 skip = tri_leafcert_skips_gap(w, tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z), ts.tri.t, ts.cert_gap);
             }
-#endif
             if (skip != kLeafCertAll) {
                 const uint4 pr = sv.tri_prims[prim];  // object, sub, seq_base, range
                 const RtObject& ob = sv.obj[pr.x];
@@ -1208,11 +824,7 @@ __device__ __forceinline__ uint32_t fetch_texture(const KernelArgs& ka, uint32_t
     const int y = texel_coord(v * (float)(int32_t)ka.texture_height, ka.tex_h);
     const uint32_t l = min(layer, ka.tex_layers - 1u);
     const size_t off = ((size_t)l * ka.tex_h + (size_t)y) * ka.tex_w + (size_t)x;
-#ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
-    return 0xff8040c0u ^ (uint32_t)off;
-#else
     return ka.textures[off];
-#endif
 }
 
 __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb, f3 d) {
@@ -1228,11 +840,7 @@ __device__ __forceinline__ f4 sample_env(const KernelArgs& ka, const float* srgb
         const float v = 0.5f + div_const(asinf_c(d.y), kWgslPi, kInvWgslPi);
         y = texel_coord(v * (float)(int32_t)ka.env_map_height, ka.env_h);
     }
-#ifdef RT_EXP_NO_TEX  // timing experiment only: results are wrong
-    return decode_texel(0xffc0a080u ^ (uint32_t)(y * ka.env_w + x), srgb);
-#else
     return decode_texel(ka.env[(size_t)y * ka.env_w + (size_t)x], srgb);
-#endif
 }
 
 // State of one path of per_pixel (compute_shader.wgsl:210-314) between bounces.
@@ -1654,11 +1262,8 @@ __device__ __forceinline__ unsigned long long stamp() {
 // wave never idles behind one long path while work remains. A pixel's samples
 // (compute_per_frame) run back to back on one lane, so the accumulation is
 // summed in the reference's order (:160-163) and results are bit-identical.
-#ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 1
-#endif
-template <int kMode, uint32_t kThreads, bool kTris, bool kWide>
-__global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel(KernelArgs ka) {
+template <int kMode, uint32_t kThreads, bool kTris>
+__global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
 
@@ -1667,26 +1272,12 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     float* l_srgb = reinterpret_cast<float*>(lds + ka.lds_srgb_offset);
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
                  ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
-                 ka.tri_wide,     nullptr,        kThreads,       ka.sub_objects};
-    if constexpr (kWide) sv.stk = reinterpret_cast<uint32_t*>(lds + ka.lds_stack_offset) + tid;
-    sv.tri_q4 = nullptr;
-    if constexpr (kTris && !kWide && kMode <= 1) {
+                 ka.sub_objects};
+    if constexpr (kTris && kMode <= 1) {
         if (ka.tri_qnodes) {
             const float4 g0 = ka.tri_qgrid[0], g1 = ka.tri_qgrid[1];
             if (g0.w != 0.0f) {
                 sv.tri_q = ka.tri_qnodes;
-                sv.qox = g0.x;
-                sv.qoy = g0.y;
-                sv.qoz = g0.z;
-                sv.qsx = g1.x;
-                sv.qsy = g1.y;
-                sv.qsz = g1.z;
-            }
-        }
-        if (kQ4Built && ka.tri_q4) {  // the 4-wide walk, on the same grid (both from the binary root, tri_qgrid)
-            const float4 g0 = ka.tri_q4grid[0], g1 = ka.tri_q4grid[1];
-            if (g0.w != 0.0f) {
-                sv.tri_q4 = ka.tri_q4;
                 sv.qox = g0.x;
                 sv.qoy = g0.y;
                 sv.qoz = g0.z;
@@ -1735,11 +1326,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
         sv.mat = l_mat;
         sv.obj = l_obj;
     }
-    if constexpr (kMode == 2 && kWide) {  // the wide nodes (leaf records stay in global memory)
-        float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
-        for (uint32_t i = tid; i < 8u * ka.tri_nodes; i += kThreads) l_tn[i] = ka.tri_wide[i];
-        sv.tri_wide = l_tn;
-    } else if constexpr (kMode == 2) {
+    if constexpr (kMode == 2) {
         float4* l_tn = reinterpret_cast<float4*>(lds + ka.lds_tri_nodes_offset);
         uint4* l_tp = reinterpret_cast<uint4*>(lds + ka.lds_tri_prims_offset);
         for (uint32_t i = tid; i < 2u * ka.tri_nodes; i += kThreads) l_tn[i] = ka.tri_bvh[i];
@@ -1751,18 +1338,6 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             for (uint32_t i = tid; i < ka.sub_object_count; i += kThreads) l_sub[i] = ka.sub_objects[i];
             sv.sub = l_sub;
         }
-#if RT_LDS_COMPACT
-        if (ka.lds_cidx_offset) {  // the vertex-indexed triangles, when they fit
-            float4* l_cv = reinterpret_cast<float4*>(lds + ka.lds_cvert_offset);
-            uint32_t* l_ci = reinterpret_cast<uint32_t*>(lds + ka.lds_cidx_offset);
-            const uint32_t* g_ci = reinterpret_cast<const uint32_t*>(ka.tri_cidx);
-            for (uint32_t i = tid; i < ka.tri_cvert_count; i += kThreads) l_cv[i] = ka.tri_cverts[i];
-            for (uint32_t i = tid; i < (3u * ka.triangle_count + 1u) / 2u; i += kThreads) l_ci[i] = g_ci[i];
-            sv.cverts = l_cv;
-            sv.cidx = reinterpret_cast<const uint16_t*>(l_ci);
-            sv.lazy_sub = ka.lds_sub_offset == 0;  // records in global memory: test them lazily
-        }
-#endif
     }
     for (uint32_t i = tid; i < 256u; i += kThreads) l_srgb[i] = ka.srgb[i];
     float* l_cam = l_srgb + 256;  // camera block for device-side primary rays
@@ -1802,30 +1377,6 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     // (advanced per frame by the host only when accumulating, src/renderer.rs:216-235)
     // plus the sample number.
     auto random_index = [&]() { return ka.accumulation_index + (accumulate ? frame : 0u) + sample; };
-    // kRefillPrep: slot (lane id) of the wave's current tile -- its pixel index (0xffffffff:
-    // outside the image), seed and jittered direction after start_sample
-    float prep_dx = 0.0f, prep_dy = 0.0f, prep_dz = 0.0f;
-    uint32_t prep_seed = 0u, prep_index = 0xffffffffu;
-    auto prep_tile = [&](uint32_t t, uint32_t t_frame) {  // whole wave
-        if constexpr (kRefillPrep<kTris>) {
-            const uint32_t slot = lane_id_here();
-            const uint32_t gt = t * ka.world_size + ka.rank;
-            const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);
-            const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
-            prep_index = 0xffffffffu;
-            if (t < ka.owned_tiles && x < ka.width && y < ka.height) {
-                const uint32_t idx = y * ka.width + x;
-                Path q;
-                start_sample(ka, idx, ka.accumulation_index + (accumulate ? t_frame : 0u),
-                             pixel_ray(ka, l_cam, idx, x, y), q);
-                prep_index = idx;
-                prep_seed = q.seed;
-                prep_dx = q.d.x;
-                prep_dy = q.d.y;
-                prep_dz = q.d.z;
-            }
-        }
-    };
     // A sample just started: with the primary pre-pass (rt_primary_kernel) its first
     // segment's trace result is read back and the lane goes straight to shading it;
     // else the trace starts at the next setup step.
@@ -1912,7 +1463,6 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
     uint32_t tile_frame = 0;         // frame of the claimed unit (frame-parallel batches), wave-uniform
     uint32_t tile = unit_tile(ka, claim_tile(ka, queue), tile_frame);  // wave-uniform
     uint32_t next = 0;               // next pixel slot of `tile`, wave-uniform
-    prep_tile(tile, tile_frame);
 #ifdef RT_DIAG
     unsigned long long iters = 0, trav_cyc = 0, steps = 0, step_lanes = 0, shade_cyc = 0, refill_cyc = 0,
                        setup_cyc = 0, leaf_cyc = 0, leaf_steps = 0;
@@ -1980,34 +1530,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             const uint64_t need = __ballot(mode == kIdle);
             if (need == 0 || tile >= ka.owned_tiles) break;
             const uint32_t avail = 64u - next;
-            if constexpr (kRefillPrep<kTris>) {
-                // (the whole wave: ds_bpermute reads only from active lanes) each idle lane fetches
-                // the prologue's values of the slot it takes
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                const int src = (int)(min(next + rank, 63u) * 4u);
-                const uint32_t g_index = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)prep_index);
-                const uint32_t g_seed = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)prep_seed);
-                const float g_dx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(prep_dx)));
-                const float g_dy = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(prep_dy)));
-                const float g_dz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(prep_dz)));
-                if (mode == kIdle && rank < avail && g_index != 0xffffffffu) {
-                    index = g_index;  // :148
-                    lane_tile = tile;
-                    lane_slot = next + rank;
-                    sample = 0;
-                    frame = tile_frame;
-                    if (accumulate && !frame_par) pix = ka.accum[index];  // :156
-                    // start_sample's state, computed in the tile's prologue (same operations)
-                    p.o = mk(ka.camera_origin[0], ka.camera_origin[1], ka.camera_origin[2]);
-                    p.d = mk(g_dx, g_dy, g_dz);
-                    p.seed = g_seed;
-                    p.contrib = f4{1.0f, 1.0f, 1.0f, 1.0f};
-                    p.light = f4{0.0f, 0.0f, 0.0f, 0.0f};
-                    p.bounce = 0;
-                    mode = primary_start();
-                }
-            } else if (mode == kIdle) {
+            if (mode == kIdle) {
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 if (rank < avail) {
@@ -2032,8 +1555,7 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             if (next == 64u) {
                 tile = unit_tile(ka, claim_tile(ka, queue), tile_frame);
                 next = 0;
-                prep_tile(tile, tile_frame);
-#ifdef RT_DIAG_TAIL
+            #ifdef RT_DIAG_TAIL
                 if (tile >= ka.owned_tiles && wave_dry == 0) wave_dry = realtime();
 #endif
             }
@@ -2116,13 +1638,13 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             const unsigned long long tl0 = stamp();
 #endif
             bool batched = false;
-            if constexpr (kCoopLeaves<kMode, kTris, kWide>) {
+            if constexpr (kCoopLeaves<kMode, kTris>) {
                 if (leaves && ka.tri_leaftris) {  // the wave's deferred leaves, cooperatively
                     RT_ISA_MARK("coop_leaf_batch");
                     const bool act = mode == kTrav && ts.pending != kNoLeaf;
                     coop_leaf_batch(sv, ka, p.o, p.d, ts, act, lds);
                     if (act) {
-                        phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                        phase_end<kTris>(sv, ka, p.o, p.d, ts);
                         if (ts.phase == 2) mode = kDone;
                     }
                     batched = true;
@@ -2131,20 +1653,20 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
             if (!batched && mode == kTrav && (!leaves || ts.pending != kNoLeaf)) {
                 if (kDeferLeaves<kTris> && leaves) {
                     RT_ISA_MARK("leaf_batch");
-                    leaf_step<kTris, kWide, (kMode <= 1)>(sv, ka, p.o, p.d, ts);
+                    leaf_step<kTris, (kMode <= 1)>(sv, ka, p.o, p.d, ts);
                 } else {
                     RT_ISA_MARK("node_step");
-                    node_step<kTris, kWide, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
+                    node_step<kTris, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
                 }
-                phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                phase_end<kTris>(sv, ka, p.o, p.d, ts);
                 if (ts.phase == 2) mode = kDone;
                 if (!(kDeferLeaves<kTris> && leaves)) {
-                    // further node steps before the next wave-wide check (RT_TRAV_UNROLL)
+                    // further node steps before the next wave-wide check (kTravUnroll)
 #pragma unroll
                     for (int k = 1; k < kTravUnroll<kMode, kTris>; ++k) {
                         if (mode == kTrav) {
-                            node_step<kTris, kWide, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
-                            phase_end<kTris, kWide>(sv, ka, p.o, p.d, ts);
+                            node_step<kTris, kCertWalk<kMode>>(sv, ka, p.o, p.d, ts);
+                            phase_end<kTris>(sv, ka, p.o, p.d, ts);
                             if (ts.phase == 2) mode = kDone;
                         }
                     }
@@ -2231,40 +1753,36 @@ __global__ void __launch_bounds__(kThreads, RT_WAVES_PER_EU) rt_pathtrace_kernel
 // the size with the most resident waves up to a cap (rt_pathtrace_pick_config).
 // Sphere-only scenes get kernels without the triangle side (fewer live scalar
 // registers: the kernel arguments of the triangle path no longer spill).
-#ifndef RT_EXTRA_CONFIGS  // experiment builds add instances here, e.g. -DRT_EXTRA_CONFIGS(X)="X(1, 640, false, false)"
-#define RT_EXTRA_CONFIGS(X)
-#endif
-// (mode, threads, triangles, 4-wide triangle accelerator)
+// (mode, threads, triangles)
 #define RT_FOR_EACH_CONFIG(X)                                                                                   \
-    X(0, 256, true, false) X(0, 512, true, false) X(0, 1024, true, false) X(1, 256, true, false)               \
-    X(1, 512, true, false) X(1, 1024, true, false) X(2, 256, true, false) X(2, 512, true, false)               \
-    X(2, 1024, true, false) X(0, 256, true, true) X(0, 512, true, true) X(0, 1024, true, true)                 \
-    X(1, 256, true, true) X(1, 512, true, true) X(1, 1024, true, true) X(2, 256, true, true)                   \
-    X(2, 512, true, true) X(2, 1024, true, true) X(0, 256, false, false) X(0, 512, false, false)               \
-    X(0, 1024, false, false) X(1, 256, false, false) X(1, 512, false, false) X(1, 1024, false, false)          \
-    RT_EXTRA_CONFIGS(X)
+    X(0, 256, true) X(0, 512, true) X(0, 1024, true) X(1, 256, true) X(1, 512, true) X(1, 1024, true)          \
+    X(2, 256, true) X(2, 512, true) X(2, 1024, true) X(0, 256, false) X(0, 512, false) X(0, 1024, false)       \
+    X(1, 256, false) X(1, 512, false) X(1, 1024, false)
 
-// ---- the reference's brute-force sweep, LDS-tiled (BASELINE.json config 5) -----
+// ---- the reference's brute-force sweep as a wavefront (BASELINE.json config 5) -------------
 //
-// rt_brute_kernel renders a batch of frames the way compute_shader.wgsl does --
-// one invocation per pixel (:146-189), every sphere tested (:355-404), every
-// object's box and every sub-object's box tested in order and the triangles of
-// the sub-objects hit (:422-517) -- with no acceleration structure. What is
-// MI355X-specific is how the sub-object array reaches the lanes: a workgroup of
-// 256 pixels steps through its paths one bounce at a time, and for each bounce
-// streams the object's sub-object records through LDS in tiles of
-// kBruteTileSubs (coalesced 16-B loads, one pass per workgroup and bounce instead
-// of one per pixel); every lane then tests the tile's boxes with LDS broadcast
-// reads (all lanes read the same record), and a sub-object's triangles are loaded
-// only for the lanes whose box test passed (the wave's exec mask is the ballot of
-// the per-lane hits). Same arithmetic and order as the reference's sweep: the
-// first of equal distances wins (`>=` rejects, :457), a NaN distance is accepted
-// and makes later candidates accepted (:449-481), spheres by (t, index).
-// HBM traffic: the framebuffer (SURVEY §8d, 52 B/px/frame), texels, and the
-// tile-streaming term -- 32 B x sub-objects per workgroup and bounce, counted in
-// KernelArgs::stream_bytes.
-constexpr uint32_t kBruteThreads = 256;     // 4 8x8 tiles per workgroup
-constexpr uint32_t kBruteTileSubs = 1024;   // sub-object records per LDS tile (32 KB)
+// rt_brute_wf_kernel renders frames the way compute_shader.wgsl does -- every sphere tested
+// (:355-404), every object's box and every sub-object's box tested in order and the triangles of
+// the sub-objects hit (:422-517) -- with no acceleration structure. What is MI355X-specific is
+// how the work reaches the lanes. The paths live in HBM (KernelArgs::brute_paths, 64 B per
+// pixel slot) and each launch advances one bounce level of one pass (frame, sample) over a
+// compacted queue of the slots still alive, so every lane of a sweep carries a live ray (a
+// workgroup in lockstep over its 256 pixels idles half its lanes once paths end at different
+// bounces: C5 535.7 ms per frame that way). The sub-object records reach the
+// lanes either through two LDS tiles per workgroup, the next tile's coalesced loads in flight
+// while the current one is tested with broadcast reads, one barrier per tile (mode 1), or
+// through the scalar cache, each wave streaming them on its own (mode 2). A sub-object's
+// triangles are loaded only by the lanes whose box test passed. Same arithmetic and order as
+// the reference's sweep per ray: the first of equal distances wins (`>=` rejects, :457), a NaN
+// distance is accepted and makes later candidates accepted (:449-481), spheres by (t, index).
+// Per pixel the passes run in order and a finished path adds its light to the accumulation
+// then, the reference's sum order (:164-178).
+//
+// HBM traffic: the framebuffer (52 B/px/frame), texels, and the tile-streaming term
+// with its fixed convention of one 256-ray tile -- 32 B x N_sub per started 256 rays of each
+// bounce level -- counted in KernelArgs::stream_bytes; the bytes the sweeps actually stream
+// from L2 (per LDS tile and workgroup, or per wave in mode 2) in KernelArgs::l2_stream_bytes.
+constexpr uint32_t kBruteThreads = 256;  // 4 8x8 tiles per workgroup
 
 // The brute-force kernels' LDS scene image (the persistent kernel's mode 1: spheres in slot
 // order, materials + glass constants, objects, sRGB table and camera block); the caller
@@ -2307,7 +1825,7 @@ __device__ __forceinline__ SceneView brute_stage(const KernelArgs& ka, unsigned 
     }
     if (tid == 0) l_cam[32] = ka.aspect;
     return SceneView{l_sph, l_orig, l_smat, nullptr, l_mat, l_aux, l_obj, l_srgb, nullptr, nullptr, 0.0f,
-                     nullptr, nullptr, 0u,     ka.sub_objects};
+                     ka.sub_objects};
 }
 
 // The triangles of one sub-object whose box the ray entered, in the sweep's order (:449-481):
@@ -2334,171 +1852,21 @@ __device__ __forceinline__ void brute_sub_triangles(const KernelArgs& ka, f3 o, 
     }
 }
 
-template <bool kTris>
-__global__ void __launch_bounds__(kBruteThreads) rt_brute_kernel(KernelArgs ka) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint32_t block_rays;
-    const uint32_t tid = threadIdx.x;
-    if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
-    float* l_cam;
-    const SceneView sv = brute_stage<kTris>(ka, lds, tid, l_cam);
-    RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_stack_offset);
-    const RtObject* l_obj = sv.obj;
-    if (tid == 0) block_rays = 0;
-    __syncthreads();
-
-    // this thread's pixel: local tile blockIdx * 4 + tid / 64 (global tile local * world + rank)
-    const uint32_t local_tile = blockIdx.x * (kBruteThreads / 64u) + (tid >> 6);
-    const uint32_t slot = tid & 63u;
-    const uint32_t gt = local_tile * ka.world_size + ka.rank;
-    const uint32_t x = (gt % ka.tiles_x) * 8u + (slot & 7u);
-    const uint32_t y = (gt / ka.tiles_x) * 8u + (slot >> 3);
-    const bool valid = local_tile < ka.owned_tiles && x < ka.width && y < ka.height;
-    const uint32_t index = valid ? y * ka.width + x : 0u;
-    const bool accumulate = ka.accumulate == 1u;
-    const uint32_t samples = accumulate ? ka.compute_per_frame : 1u;
-    uint32_t rays = 0;
-    uint64_t streamed = 0;  // sub-object records this workgroup loaded (tid 0 counts)
-    float4 pix = valid && accumulate ? ka.accum[index] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const f3 cam = valid ? pixel_ray(ka, l_cam, index, x, y) : mk(0.f, 0.f, 1.f);
-    Path p;
-    for (uint32_t frame = 0; frame < ka.frames; ++frame) {
-        for (uint32_t sample = 0; sample < samples; ++sample) {
-            const uint32_t random_index = ka.accumulation_index + (accumulate ? frame : 0u) + sample;
-            start_sample(ka, index, random_index, cam, p);
-            bool alive = valid && p.bounce < ka.bounces;
-            while (true) {
-                // the workgroup traces together while any of its paths is alive
-                if (!__syncthreads_or(alive)) break;
-                // check_spheres (:355-404), every sphere (the (t, index) rule makes slot order free)
-                TraceState ts;
-                ts.sph = SphereHit{kF32Max, 0u, 0u};
-                ts.tri = TriHit{kF32Max, 0u, 0u, 0u, false};
-                const f3 o = p.o, d = p.d;
-                const float a = dot(d, d);
-                if (alive) {
-                    for (uint32_t i = 0; i < ka.sphere_slot_count; i += 4u)
-                        test_sphere_group(sv, i, o, d, 4.0f * a, 2.0f * a, ts.sph);
-                }
-                // check_triangles (:422-517): objects, then their sub-objects through LDS tiles
-                if constexpr (kTris) {
-                    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-                    float closest = kF32Max;
-                    for (uint32_t oi = 0; oi < ka.object_count; ++oi) {
-                        const RtObject& ob = l_obj[oi];
-                        const bool in_obj = alive && ray_in_bounds(o, inv, ob.min_bounds, ob.max_bounds);
-                        if (!__syncthreads_or(in_obj)) continue;  // no lane of the workgroup enters the object
-                        const uint32_t first = ob.first_sub_object_index, n_sub = ob.sub_object_count;
-                        for (uint32_t t0 = 0; t0 < n_sub; t0 += kBruteTileSubs) {
-                            const uint32_t nt = min(kBruteTileSubs, n_sub - t0);
-                            __syncthreads();  // the previous tile's readers are done
-                            const uint4* src = reinterpret_cast<const uint4*>(ka.sub_objects);
-                            uint4* dst = reinterpret_cast<uint4*>(l_sub);
-                            for (uint32_t q = tid; q < 2u * nt; q += kBruteThreads) {
-                                const uint32_t si = min(first + t0 + (q >> 1), ka.sub_object_count - 1u);
-                                dst[q] = src[2u * si + (q & 1u)];
-                            }
-                            if (tid == 0) streamed += nt;
-                            __syncthreads();
-                            if (!in_obj) continue;
-                            for (uint32_t k = 0; k < nt; ++k) {
-                                const RtSubObject& sub = l_sub[k];  // broadcast read
-                                if (!ray_in_bounds(o, inv, sub.min_bounds, sub.max_bounds)) continue;
-                                brute_sub_triangles(ka, o, d, sub.first_triangle_index, sub.triangle_count, oi,
-                                                    closest, ts.tri);
-                            }
-                        }
-                    }
-                }
-                if (alive) {
-                    ++rays;
-                    const Hit h = trace_end<kTris>(sv, ka, o, d, ts);
-                    if (shade<true>(sv, ka, p, h)) alive = false;
-                }
-            }
-            if (accumulate && valid) {
-                pix.x = pix.x + p.light.x;
-                pix.y = pix.y + p.light.y;
-                pix.z = pix.z + p.light.z;
-                pix.w = pix.w + p.light.w;
-            }
-        }
-    }
-    if (valid) {  // the last frame's accumulation and output (:164-178)
-        float r, g, b, al;
-        if (accumulate) {
-            const float div = (float)((ka.accumulation_index + ka.frames - 1u) * ka.compute_per_frame);
-            r = clamp01(pix.x / div);
-            g = clamp01(pix.y / div);
-            b = clamp01(pix.z / div);
-            al = clamp01(pix.w / div);
-            ka.accum[index] = pix;
-        } else {
-            r = clamp01(p.light.x);
-            g = clamp01(p.light.y);
-            b = clamp01(p.light.z);
-            al = clamp01(p.light.w);
-        }
-        ka.output[index] = pack_rgba8(r, g, b, al);
-    }
-    atomicAdd(&block_rays, rays);
-    __syncthreads();
-    if (tid == 0) {
-        if (block_rays) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
-        if (streamed && ka.stream_bytes) atomicAdd(ka.stream_bytes, (unsigned long long)streamed * 32ull);
-    }
-    if (ka.launch_clock) {
-        __syncthreads();
-        if (tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
-    }
-}
-
-// ---- the brute-force sweep as a wavefront (rt_brute_wf_kernel) ---------------------------
-//
-// rt_brute_kernel keeps a workgroup's 256 paths in lockstep: it sweeps the sub-object array
-// for every bounce while any of its paths is alive, so most of its lanes idle once paths end at
-// different bounces (C5: ~2 segments per path on average, but a workgroup runs until its
-// longest path ends; PMC: half the lanes of each VALU instruction masked off). Here the paths
-// live in HBM (KernelArgs::brute_paths, 64 B per pixel slot) and each launch advances one
-// bounce level of one pass (frame, sample) over a compacted queue of the slots still alive:
-// every lane of a sweep carries a live ray. The sweep itself is the reference's (:422-517, the
-// same tests in the same order per ray, brute_sub_triangles); the sub-object records stream
-// through two LDS tiles, the next tile's loads in flight while the current one is tested, one
-// barrier per tile. Per pixel the passes run in order and a finished path adds its light to the
-// accumulation then, the reference's sum order (:164-178).
-#ifndef RT_BRUTE_TILE
-#define RT_BRUTE_TILE 512
-#endif
-#ifndef RT_BRUTE_GROUP
-#define RT_BRUTE_GROUP 4
-#endif
-constexpr uint32_t kBruteGroup = RT_BRUTE_GROUP;  // boxes tested per group (see the sweep)
-constexpr uint32_t kBruteWfTileSubs = RT_BRUTE_TILE;  // sub-object records per LDS tile (x2 buffers)
+constexpr uint32_t kBruteGroup = 4;          // boxes tested per group (see the sweep)
+constexpr uint32_t kBruteWfTileSubs = 512;    // sub-object records per LDS tile (x2 buffers)
 constexpr uint32_t kBruteWfLoads = 2u * kBruteWfTileSubs / kBruteThreads;  // 16-B loads per thread and tile
 static_assert(kBruteWfLoads * kBruteThreads == 2u * kBruteWfTileSubs, "tile = whole 16-B loads per thread");
 static_assert(kBruteWfLoads == 4u, "the sweep's tile loads are written out for 4 per thread");
-
-// Rays per thread in a sweep: each broadcast LDS read of a box serves kBruteRays rays (one
-// ray per thread, the LDS data return -- 64 lanes x 12 B per read -- outran the box tests'
-// VALU work: VALU issue 38% at one ray per thread).
-#ifndef RT_BRUTE_RAYS
-#define RT_BRUTE_RAYS 1
-#endif
-constexpr uint32_t kBruteRays = RT_BRUTE_RAYS;
+// Rays per thread in a sweep (the LDS-tiled sweep is written for several: each broadcast read of
+// a box would serve them all; measured no faster than one, round 5).
+constexpr uint32_t kBruteRays = 1;
 constexpr uint32_t kBruteChunk = kBruteRays * kBruteThreads;  // queue entries per workgroup pass
 // Entries of a ray's list of entered boxes (tile-local u16 indices, LDS) before it is drained.
-#ifndef RT_BRUTE_HITS
-#define RT_BRUTE_HITS 8
-#endif
-constexpr uint32_t kBruteHits = RT_BRUTE_HITS;
+constexpr uint32_t kBruteHits = 8;
 static_assert(kBruteHits >= kBruteGroup, "a group's hits fit a drained list");
-// kStream instances (rt_set_brute_force(ctx, 2)): the sub-object records through the scalar
-// cache instead of LDS tiles -- each wave streams them on its own (wave-uniform s_load), no tile
-// barrier, no LDS but the hit lists, so the occupancy is set by registers (RT_BRUTE_STREAM_WAVES
-// waves per SIMD requested; the shading code spills a little at 8).
-#ifndef RT_BRUTE_STREAM_WAVES
-#define RT_BRUTE_STREAM_WAVES 8
-#endif
+// Waves per SIMD requested: the LDS-tiled sweep 4 (its tiles), the streamed sweep 8 (no LDS but
+// the hit lists, so the occupancy is set by registers; the shading code spills a little at 8).
+constexpr int kBruteWaves = 4, kBruteStreamWaves = 8;
 
 // One pixel slot of the wavefront: its pixel and whether it is inside the image.
 struct BruteSlot {
@@ -2535,11 +1903,8 @@ __device__ __forceinline__ void brute_store_path(float4* pl, uint32_t n_slots, u
     pl[3u * n_slots + s] = make_float4(p.contrib.x, p.contrib.y, p.contrib.z, p.contrib.w);
 }
 
-#ifndef RT_BRUTE_WAVES
-#define RT_BRUTE_WAVES 4
-#endif
 template <bool kTris, bool kStream>
-__global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES : RT_BRUTE_WAVES)
+__global__ void __launch_bounds__(kBruteThreads, kStream ? kBruteStreamWaves : kBruteWaves)
     rt_brute_wf_kernel(KernelArgs ka) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t block_rays;
@@ -2547,7 +1912,7 @@ __global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES
     if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock, ~(unsigned long long)wall_clock64());
     const uint32_t n_slots = ka.owned_tiles * 64u;
     const uint32_t level = ka.brute_level;
-    uint32_t* counts = ka.brute_counts + (size_t)ka.brute_pass * kBruteLevels;
+    uint32_t* counts = ka.brute_counts + (size_t)ka.brute_pass * ka.brute_levels;
     const uint32_t n_in = level == 0u ? n_slots : counts[level];
     if (blockIdx.x * kBruteChunk >= n_in) {  // nothing for this workgroup (the queue shrank)
         if (ka.launch_clock && tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
@@ -2569,8 +1934,10 @@ __global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES
     uint32_t* q_out = ka.brute_queue + (size_t)((level + 1u) & 1u) * n_slots;
     float4* pl = ka.brute_paths;
     uint32_t rays = 0;
-    uint64_t streamed = 0;
+    uint64_t streamed = 0;  // sub-object records this workgroup's tiles (tid 0) or waves (lane 0 of each) read
+    uint32_t chunks = 0;    // 256-ray chunks this workgroup swept (SURVEY §8d's tile convention)
     for (uint32_t c = blockIdx.x; c * kBruteChunk < n_in; c += gridDim.x) {
+        ++chunks;
         // the chunk's rays: ray k of this thread is queue entry c * chunk + k * threads + tid
         f3 o[kBruteRays], d[kBruteRays], inv[kBruteRays];
         bool alive[kBruteRays];
@@ -2867,111 +2234,17 @@ __global__ void __launch_bounds__(kBruteThreads, kStream ? RT_BRUTE_STREAM_WAVES
     atomicAdd(&block_rays, rays);
     __syncthreads();
     if (tid == 0 && block_rays) atomicAdd(ka.ray_counter, (unsigned long long)block_rays);
-    // the records this workgroup's LDS tiles (thread 0) or its waves (lane 0 of each, kStream) read
-    if (streamed && ka.stream_bytes) atomicAdd(ka.stream_bytes, (unsigned long long)streamed * 32ull);
+    // the tile-streaming term of SURVEY §8d -- 32 B x the sweep's sub-objects per 256 rays of the
+    // level -- and the records the sweeps actually read from L2
+    if (tid == 0 && ka.stream_bytes && kTris && chunks) {
+        uint64_t n_sub = 0;
+        for (uint32_t oi = 0; oi < ka.object_count; ++oi) n_sub += sv.obj[oi].sub_object_count;
+        atomicAdd(ka.stream_bytes, (unsigned long long)(chunks * n_sub * 32ull));
+    }
+    if (streamed && ka.l2_stream_bytes) atomicAdd(ka.l2_stream_bytes, (unsigned long long)streamed * 32ull);
     if (ka.launch_clock) {
         __syncthreads();
         if (tid == 0) atomicMax(ka.launch_clock + 1, (unsigned long long)wall_clock64());
-    }
-}
-
-// ---- the 4-wide accelerator as a packet (rt_primary_kernel, tri_q4.h) --------------------
-// The wave walks one node at a time (wave-uniform address: one load serves the packet); each
-// lane tests the four child boxes with its own culling slab, and a child is entered when any
-// lane's ray enters it, by exactly those lanes. The node's hit leaves are tested at once by the
-// lanes that reached them (certificate first, as the binary packet walk does: tri_leaf_skips on
-// the child's box), in the order of the first hitting lane's entry distances; of the internal
-// children the nearest is walked next and the others wait on the wave's LDS stack with the mask
-// of their lanes (kQ4PacketStack entries of {node, mask}: enough for 3 per level of a tree of
-// depth <= 21, which the host checks). Every lane still gets the lexicographic minimum over a
-// superset of its own candidates -- its own result.
-__device__ __forceinline__ void q4_packet_walk(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
-                                               bool valid, uint32_t* wst) {
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    uint32_t node = 0u, sp = 0u;  // wave-uniform
-    bool act = valid;
-    while (true) {
-        if (node == kQ4None) {
-            if (sp == 0u) break;
-            sp -= 1u;
-            wave_lds_sync();
-            node = __builtin_amdgcn_readfirstlane(wst[3u * sp]);
-            const uint64_t m = (uint64_t)wst[3u * sp + 1u] | ((uint64_t)wst[3u * sp + 2u] << 32);
-            act = ((m >> lane) & 1ull) != 0ull;
-        }
-        const uint4* nd = sv.tri_q4 + 4u * node;
-        const uint4 b0 = nd[0], b1 = nd[1], b2 = nd[2], rf = nd[3];
-        const uint32_t w[12] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w};
-        const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
-        bool hit[4];
-        uint64_t mask[4];
-        float key[4];
-        uint32_t slot[4] = {0u, 1u, 2u, 3u};
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; k++) {
-            const uint32_t w0 = w[3u * k], w1 = w[3u * k + 1u], w2 = w[3u * k + 2u];
-            const float4 lo = make_float4(fmaf((float)(w0 & 0xffffu), sv.qsx, sv.qox),
-                                          fmaf((float)(w0 >> 16), sv.qsy, sv.qoy),
-                                          fmaf((float)(w1 & 0xffffu), sv.qsz, sv.qoz), 0.0f);
-            const float4 hi = make_float4(fmaf((float)(w1 >> 16), sv.qsx, sv.qox),
-                                          fmaf((float)(w2 & 0xffffu), sv.qsy, sv.qoy),
-                                          fmaf((float)(w2 >> 16), sv.qsz, sv.qoz), 0.0f);
-            float near_t, far_t;
-            slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
-            bool h = act && ref[k] != kQ4Empty && near_t <= far_t && far_t >= 0.0f;
-            if (h && (ref[k] & kQ4Leaf) && ka.tri_leafcert && near_t > ts.tri.t && ts.tri.t != kF32Max &&
-                tri_leaf_skips(ka, ref[k] & 0xfffffu, ts.slab, o, d, ts.tri.t, lo, hi) == kLeafCertAll)
-                h = false;  // certified: no triangle of the leaf can win
-            hit[k] = h;
-            mask[k] = __ballot(h);
-            float kk = __builtin_inff();
-            if (mask[k])
-                kk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(near_t), (uint32_t)__builtin_ctzll(mask[k])));
-            key[k] = kk;
-        }
-        // the order of the first hitting lanes' entry distances (wave-uniform)
-#define RT_Q4_SX(a, b)                                           \
-        if (key[b] < key[a]) {                                    \
-            const float tk = key[a];                              \
-            key[a] = key[b];                                      \
-            key[b] = tk;                                          \
-            const uint32_t ts_ = slot[a];                         \
-            slot[a] = slot[b];                                    \
-            slot[b] = ts_;                                        \
-        }
-        RT_Q4_SX(0, 1) RT_Q4_SX(2, 3) RT_Q4_SX(0, 2) RT_Q4_SX(1, 3) RT_Q4_SX(1, 2)
-#undef RT_Q4_SX
-        // the hit leaves, nearest first
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; j++) {
-            const uint32_t k = slot[j];
-            if (mask[k] == 0ull || !(ref[k] & kQ4Leaf)) continue;
-            if (hit[k]) {
-                tri_leaf<true>(sv, ka, o, d, ts, ref[k] & 0xfffffu);
-                ts.limit = tri_limit(sv, ka, o, ts);
-            }
-        }
-        // the nearest internal child next, the others on the stack (farthest first)
-        node = kQ4None;
-        uint32_t first = 4u;
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; j++) {
-            const uint32_t k = slot[3u - j];
-            if (mask[k] == 0ull || (ref[k] & kQ4Leaf)) continue;
-            if (first != 4u) {  // the previously found (farther) one waits
-                if (lane == 0u) {
-                    wst[3u * sp] = ref[first];
-                    wst[3u * sp + 1u] = (uint32_t)mask[first];
-                    wst[3u * sp + 2u] = (uint32_t)(mask[first] >> 32);
-                }
-                sp += 1u;
-            }
-            first = k;
-        }
-        if (first != 4u) {
-            node = ref[first];
-            act = hit[first];
-        }
     }
 }
 
@@ -3003,7 +2276,7 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
     float* l_cam = l_srgb + 256;
     SceneView sv{ka.sphere_slots, ka.sphere_orig, ka.sphere_material, ka.sphere_bvh, ka.materials, nullptr,
                  ka.objects,      l_srgb,         ka.tri_bvh,     ka.tri_prims, kTris ? *ka.tri_extent : 0.0f,
-                 nullptr,         nullptr,        0u,             ka.sub_objects};
+                 ka.sub_objects};
     if constexpr (kMode >= 1) {  // what the walks read (the path kernel's mode 1 / 2 image)
         float4* l_sph = reinterpret_cast<float4*>(lds);
         RtObject* l_obj = reinterpret_cast<RtObject*>(lds + ka.lds_obj_offset);
@@ -3032,23 +2305,6 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
             RtSubObject* l_sub = reinterpret_cast<RtSubObject*>(lds + ka.lds_sub_offset);
             for (uint32_t i = tid; i < ka.sub_object_count; i += kThreads) l_sub[i] = ka.sub_objects[i];
             sv.sub = l_sub;
-        }
-    }
-    // the 4-wide packet walk (global-memory accelerators): its grid, and this wave's stack
-    uint32_t* q4_wstack = nullptr;
-    if constexpr (kTris && kMode <= 1) {
-        if (kQ4Built && ka.tri_q4 && ka.lds_q4packet_offset) {
-            const float4 g0 = ka.tri_q4grid[0], g1 = ka.tri_q4grid[1];
-            if (g0.w != 0.0f) {
-                sv.tri_q4 = ka.tri_q4;
-                sv.qox = g0.x;
-                sv.qoy = g0.y;
-                sv.qoz = g0.z;
-                sv.qsx = g1.x;
-                sv.qsy = g1.y;
-                sv.qsz = g1.z;
-                q4_wstack = reinterpret_cast<uint32_t*>(lds + ka.lds_q4packet_offset) + (tid >> 6) * (3u * kQ4PacketStack);
-            }
         }
     }
     if (tid < 16u) {
@@ -3084,13 +2340,6 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
         TraceState ts;
         trace_begin<kTris>(sv, ka, o, d, ts);  // brute-force spheres, slab constants, phase
         if constexpr (kTris) {
-            if (kQ4Built && kMode <= 1 && ts.phase == 0 && sv.tri_q4) {
-                q4_packet_walk(sv, ka, o, d, ts, valid, q4_wstack);
-                if (ts.nan_hit) ts.tri = sweep_triangles(sv, ka, o, d);  // measure-zero case: the sweep decides
-                ts.phase = ka.sphere_nodes != 0 ? 1u : 2u;
-                ts.node = 0;
-                if (ts.phase == 1) phase_setup<kTris>(sv, ka, o, ts.a2 * 0.5f, 1, ts);
-            }
             if (ts.phase == 0) {
                 // the triangle accelerator as a packet: wave-uniform node (the layout of the
                 // first lane's direction octant), per-lane culling and pruning
@@ -3109,11 +2358,8 @@ __global__ void __launch_bounds__(kThreads, kMinWaves) rt_primary_kernel(KernelA
                     }
                     const bool any = __ballot(hit) != 0;
                     if (any && leaf != 0xffffffffu && hit) {
-#if RT_LEAFCERT_DEFER
-                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);  // (bit 24 means "deferred" there)
-#else
-                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, (leaf & 0xffffffu) | (skip << 24));
-#endif
+                        // (its certificate tested above: bit 24 of the argument would mean "deferred")
+                        tri_leaf<(kMode <= 1)>(sv, ka, o, d, ts, leaf & 0xffffffu);
                         ts.limit = tri_limit(sv, ka, o, ts);
                     }
                     node = (any && leaf == 0xffffffffu) ? node + 1u : __float_as_uint(lo.w);
@@ -3175,35 +2421,17 @@ hipError_t allow_big_lds(const void* fn) {
 }
 }  // namespace
 
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool wide, uint32_t threads,
-                               size_t lds_bytes, uint32_t blocks, hipStream_t stream) {
-#define RT_LAUNCH(M, T, TR, W)                                                                                   \
-    if (mode == M && threads == T && tris == TR && wide == W) {                                                 \
-        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T, TR, W>), dim3(blocks), dim3(T), lds_bytes, stream, ka);   \
-        return hipGetLastError();                                                                               \
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes,
+                               uint32_t blocks, hipStream_t stream) {
+#define RT_LAUNCH(M, T, TR)                                                                                    \
+    if (mode == M && threads == T && tris == TR) {                                                            \
+        hipLaunchKernelGGL((rt_pathtrace_kernel<M, T, TR>), dim3(blocks), dim3(T), lds_bytes, stream, ka);    \
+        return hipGetLastError();                                                                             \
     }
     RT_FOR_EACH_CONFIG(RT_LAUNCH)
 #undef RT_LAUNCH
     return hipErrorInvalidValue;
 }
-
-hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream) {
-    const uint32_t blocks = (ka.owned_tiles + kBruteThreads / 64u - 1u) / (kBruteThreads / 64u);
-    if (blocks == 0) return hipSuccess;
-    if (lds_bytes > 64u * 1024u) {  // dynamic LDS above 64 KiB must be opted into (exactly what is used)
-        const void* fn = tris ? reinterpret_cast<const void*>(&rt_brute_kernel<true>)
-                              : reinterpret_cast<const void*>(&rt_brute_kernel<false>);
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-        if (e != hipSuccess) return hipErrorInvalidConfiguration;  // (distinguishes the opt-in from the launch)
-    }
-    if (tris)
-        hipLaunchKernelGGL(rt_brute_kernel<true>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
-    else
-        hipLaunchKernelGGL(rt_brute_kernel<false>, dim3(blocks), dim3(kBruteThreads), lds_bytes, stream, ka);
-    return hipGetLastError();
-}
-
-size_t rt_brute_tile_bytes() { return (size_t)kBruteTileSubs * sizeof(RtSubObject); }
 
 size_t rt_brute_wf_tile_bytes(bool stream) {
     if (stream) return (size_t)kBruteThreads * kBruteHits * 4u;  // the hit lists only (u32 entries)
@@ -3260,18 +2488,18 @@ hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t l
 // add contention), ties to the smaller workgroup.
 constexpr int kDefaultWavesPerCu = 16;
 
-hipError_t rt_pathtrace_pick_config(int mode, bool tris, bool wide, size_t lds_bytes,
-                                    size_t lds_bytes_per_thread, uint32_t force_threads, uint32_t waves_cap,
-                                    uint32_t* threads, int* blocks_per_cu) {
+hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, size_t lds_bytes_per_thread,
+                                    uint32_t force_threads, uint32_t waves_cap, uint32_t* threads,
+                                    int* blocks_per_cu) {
     const int kTargetWavesPerCu = waves_cap ? (int)waves_cap : kDefaultWavesPerCu;
     int best_waves = -1;
-    // lds_bytes_per_thread: the wide walk's stack (grows with the workgroup size)
-#define RT_OCC(M, T, TR, W)                                                                               \
-    if (mode == M && tris == TR && wide == W) {                                                           \
+    // lds_bytes_per_thread: the cooperative leaf batch's per-wave scratch (grows with the workgroup size)
+#define RT_OCC(M, T, TR)                                                                                  \
+    if (mode == M && tris == TR) {                                                                        \
         int n = 0;                                                                                        \
-        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T, TR, W>));  \
+        hipError_t e = allow_big_lds(reinterpret_cast<const void*>(&rt_pathtrace_kernel<M, T, TR>));     \
         if (e != hipSuccess) return e;                                                                    \
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T, TR, W>, T,        \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_pathtrace_kernel<M, T, TR>, T,           \
                                                          lds_bytes + (size_t)T * lds_bytes_per_thread);  \
         if (e != hipSuccess) return e;                                                                    \
         const int waves = std::min(n * (int)(T / 64), kTargetWavesPerCu);                                 \

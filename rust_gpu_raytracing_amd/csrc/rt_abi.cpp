@@ -24,20 +24,14 @@
 #include "sphere_bvh.h"
 #include "tri_cone.h"
 #include "tri_qnode.h"
-#include "tri_wide.h"
 
 hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
                                    hipStream_t stream);
-hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, bool wide, uint32_t threads,
-                               size_t lds_bytes, uint32_t blocks, hipStream_t stream);
-hipError_t rt_pathtrace_pick_config(int mode, bool tris, bool wide, size_t lds_bytes, size_t lds_bytes_per_thread,
+hipError_t rt_launch_pathtrace(const KernelArgs& ka, int mode, bool tris, uint32_t threads, size_t lds_bytes,
+                               uint32_t blocks, hipStream_t stream);
+hipError_t rt_pathtrace_pick_config(int mode, bool tris, size_t lds_bytes, size_t lds_bytes_per_thread,
                                     uint32_t force_threads, uint32_t waves_cap, uint32_t* threads,
                                     int* blocks_per_cu);
-hipError_t rt_launch_wide_refresh(TriWideNode* nodes, TriLeaf* leaves, uint32_t n_leaves, const TriVertex* verts_in,
-                                  TriVertex* verts, const uint32_t* vsrc, uint32_t n_verts, const RtSubObject* subs,
-                                  const RtTriangleHot* tris, uint32_t n_tri, const uint32_t* order,
-                                  const uint32_t* level_offsets, uint32_t n_levels, float* extent_out, bool refit,
-                                  hipStream_t stream);
 hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const uint32_t* sub_object,
                           const uint2* object_tris, const rt_scene::Placement* place, uint32_t object_count,
                           uint32_t n_tri, uint32_t n_sub, RtTriangleHot* tris, float4* bounds, RtSubObject* subs,
@@ -50,14 +44,10 @@ hipError_t rt_launch_refit(SphereBvhNode* nodes, const SubObjectPrim* prims, con
                            hipStream_t stream);
 hipError_t rt_launch_tri_leafcert(const SubObjectPrim* prims, uint32_t n_prims, const RtSubObject* subs,
                                   const RtTriangleHot* tris, uint32_t n_tri, TriLeafCert* out, hipStream_t stream);
-hipError_t rt_launch_tri_q4_fill(const SphereBvhNode* bin, uint32_t n_bin, const uint32_t* src, uint32_t n_q4,
-                                 TriQ4Node* q4, float4* grid, hipStream_t stream);
 hipError_t rt_launch_tri_leaftris(const SubObjectPrim* prims, uint32_t n_prims, const RtTriangleHot* tris,
                                   uint32_t n_tri, uint4* out, hipStream_t stream);
-hipError_t rt_launch_brute(const KernelArgs& ka, bool tris, size_t lds_bytes, hipStream_t stream);
 hipError_t rt_launch_primary(const KernelArgs& ka, int mode, bool tris, size_t lds_bytes, uint32_t threads,
                              uint32_t min_waves, hipStream_t stream);
-size_t rt_brute_tile_bytes();
 hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, bool scalar_stream, size_t lds_bytes, uint32_t blocks,
                               hipStream_t stream);
 size_t rt_brute_wf_tile_bytes(bool scalar_stream);
@@ -90,10 +80,6 @@ namespace {
 
 constexpr size_t kLdsSceneBudget = 64 * 1024;    // mode 1: spheres/materials/objects/sphere BVH per workgroup
 constexpr size_t kLdsAccelBudget = 150 * 1024;   // mode 2: + triangle accelerator (one 1024-thread workgroup per CU)
-// Compact leaves (tri_wide.h) by default when the triangle records outgrow one
-// XCD's 4 MB L2 (C5: 64 MB -> 26 MB of vertex blocks); smaller meshes stay L2
-// resident and the recomputation would only add VALU work.
-constexpr size_t kCompactMinTriBytes = 4u << 20;
 // d_counter: [0] the ray counter, [1, 1 + kDiagCounters) the diagnostic
 // counters of RT_DIAG / RT_DIAG_TAIL builds (KernelArgs::diag), then the
 // per-wave (queue dry, end) records of RT_DIAG_TAIL builds: room for 65,536 waves.
@@ -177,7 +163,7 @@ struct rt_ctx {
     uint32_t frame_batch = RT_DEFAULT_FRAME_BATCH;  // frames per launch at most (1: one launch per frame)
     uint32_t pending_frames = 0;  // queued, not yet launched (their k already advanced)
     uint32_t pending_bounces = 0;
-    bool frame_parallel = true;     // RT_FRAME_PARALLEL=0: batches run frames back to back per lane (A/B switch)
+    bool frame_parallel = true;     // tuning "frame_parallel" 0: batches run frames back to back per lane
     float4* d_frame_light[2] = {};    // frame-parallel batch lights (by batch parity), owned px x frames x samples
     size_t frame_light_cap = 0;       // float4 entries, each
     // overlapped batches (dispatch_frames): batch i runs on streams[i % 2]
@@ -188,18 +174,21 @@ struct rt_ctx {
     bool aux_outstanding = false;     // aux work the primary stream has not been ordered after yet
     bool primary_dirty = true;        // primary-stream work since then that an aux batch must follow
     uint64_t batches = 0;             // frame-parallel batches launched
-    bool batch_overlap = true;        // RT_BATCH_OVERLAP=0: every batch on the primary stream (A/B switch)
-    bool stage_subs = true;           // RT_STAGE_SUBS=0: mode 2 leaves read sub-objects from global (A/B switch)
-    // 16-B quantized triangle nodes for walks from global memory (RT_TRI_QNODES=0: the 32-B nodes)
+    bool batch_overlap = true;        // tuning "batch_overlap" 0: every batch on the primary stream
+    bool stage_subs = true;           // tuning "stage_subs" 0: mode 2 leaves read sub-objects from global
+    // device memory the batch buffers (frame lights, primary records) may take: a batch that
+    // would need more is rendered as several launches (dispatch_batch); tuning "batch_memory_mb"
+    size_t batch_budget = 0;
+    // 16-B quantized triangle nodes for walks from global memory (tuning "tri_qnodes" 0: the 32-B nodes)
     bool use_qnodes = true;
     bool qnodes_dirty = true;          // the binary accelerator changed since the copy was made
     bool derived_octants = false, derived_qnodes = false;  // what the last derivation produced
     uint4* d_tri_qnodes = nullptr;
     float4* d_tri_qgrid = nullptr;
     size_t qnodes_cap = 0;
-    bool batch_schedule = false;      // RT_BATCH_SCHEDULE=1: cost-ordered claims in batches too (A/B switch)
+    bool batch_schedule = false;      // tuning "batch_schedule" 1: cost-ordered claims in batches too
     // a tile's frames claimed one after another (C3 -12%, C4 -8%, C5 -4%, C2 -1.8% per frame
-    // against frame-major, profiles/archive/r02_knobs2); RT_UNIT_TILE_MAJOR=0: frame-major (A/B switch)
+    // against frame-major, profiles/archive/r02_knobs2); tuning "unit_tile_major" 0: frame-major
     bool unit_tile_major = true;
 
     uint32_t cap_mat = 0, cap_sph = 0, cap_tri = 0, cap_obj = 0, cap_sub = 0;
@@ -212,27 +201,26 @@ struct rt_ctx {
     unsigned long long* d_counter = nullptr;
     uint32_t* d_queue = nullptr;  // [stream][2] x kQueueStripesMax tile-queue counters, kQueueStride apart
     uint32_t queue_parity[2] = {0, 0};  // per stream: which half its next launch uses (the launch zeroes the other)
-    uint32_t queue_stripes = kQueueStripes;  // RT_QUEUE_STRIPES (A/B switch)
+    uint32_t queue_stripes = kQueueStripes;  // tuning "queue_stripes"
     int n_cu = 0;
-    bool force_global_scene = false;   // RT_SCENE_IN_LDS=0 (A/B switch)
+    bool force_global_scene = false;   // tuning "scene_in_lds" 0
     size_t occ_lds_bytes = 0;
     int occ_mode = -1;
     bool occ_tris = false;
-    bool occ_wide = false;
     size_t occ_stack_pt = 0;
-    int max_lds_mode = 2;               // RT_LDS_MODE (A/B switch): highest staging mode allowed
+    int max_lds_mode = 2;               // tuning "lds_mode": highest staging mode allowed
     int occ_blocks_per_cu = 0;
     uint32_t occ_threads = 0;
-    uint32_t force_threads = 0;        // RT_BLOCK_THREADS (A/B switch); 0 = pick by occupancy
-    uint32_t waves_cap = 0;            // RT_WAVES_PER_CU (A/B switch); 0 = default cap
-    uint32_t trav_threshold = 0;  // RT_TRAV_THRESHOLD (A/B switch); 0 = by scene (trav_threshold_for)
-    uint32_t drain_threshold = kDefaultDrainThreshold;  // RT_DRAIN_THRESHOLD (A/B switch)
-    uint32_t drain_min_steps = kDefaultDrainMinSteps;   // RT_DRAIN_MIN_STEPS (A/B switch)
-    uint32_t leaf_batch = 0;  // RT_LEAF_BATCH, in eighths (A/B switch); 0 = by scene (leaf_batch_for)
+    uint32_t force_threads = 0;        // tuning "block_threads"; 0 = pick by occupancy
+    uint32_t waves_cap = 0;            // tuning "waves_per_cu"; 0 = default cap
+    uint32_t trav_threshold = 0;  // tuning "trav_threshold"; 0 = by scene (trav_threshold_for)
+    uint32_t drain_threshold = kDefaultDrainThreshold;  // tuning "drain_threshold"
+    uint32_t drain_min_steps = kDefaultDrainMinSteps;   // tuning "drain_min_steps"
+    uint32_t leaf_batch = 0;  // tuning "leaf_batch", in eighths; 0 = by scene (leaf_batch_for)
     // cost-ordered tile schedule (rt_set_tile_schedule), double-buffered by
     // launch parity: launch L records costs[L&1], reads order[L&1], and its
     // first idle workgroup sorts costs[~L&1] (launch L-1's) into order[~L&1]
-    uint32_t tile_schedule = kDefaultTileSchedule;  // RT_TILE_SCHEDULE (A/B switch)
+    uint32_t tile_schedule = kDefaultTileSchedule;  // rt_set_tile_schedule / tuning "tile_schedule"
     // per stream (launches on the auxiliary stream keep their own history):
     uint32_t* d_tile_sched[2] = {};    // costs[2][n], orders[2][n], flags[2] (n = owned tiles)
     uint64_t sched_launches[2] = {};   // launches since the schedule was (re)set
@@ -245,12 +233,12 @@ struct rt_ctx {
     std::vector<rt_scene_sphere> h_sph;  // host copy: the BVH is rebuilt from it
     bool slots_dirty = true;
     uint32_t slots_count = 0xffffffffu;  // sphere_count the slots were built for
-    bool use_bvh = true;                 // RT_SPHERE_BVH=0 disables (A/B switch)
-    bool sphere_octants = true;          // RT_SPHERE_OCTANTS=0: one BVH layout (A/B switch)
-    bool sphere_box_order = true;        // RT_SPHERE_BOX_ORDER=0: octant layouts keep bmin/bmax (A/B switch)
+    bool use_bvh = true;                 // tuning "sphere_bvh" 0: the brute-force sweep only
+    bool sphere_octants = true;          // tuning "sphere_octants" 0: one BVH layout
+    bool sphere_box_order = true;        // tuning "sphere_box_order" 0: octant layouts keep bmin/bmax
     bool sphere_boxes_ordered = false;   // the uploaded layouts store (near, far) corners
     bool slots_sphere_only = false;      // the uploaded slots were laid out for the sphere-only kernels
-    uint32_t sphere_leaf_max = 0;        // RT_SPHERE_LEAF (A/B switch); 0 = default
+    uint32_t sphere_leaf_max = 0;        // tuning "sphere_leaf"; 0 = default
     uint32_t n_always = 0, n_nodes = 0, n_slots = 0;
     float sphere_extent = 0.0f;
     float sphere_rmin = 0.0f, sphere_rmax = 0.0f;
@@ -260,86 +248,56 @@ struct rt_ctx {
     size_t tri_bvh_cap = 0, tri_prims_cap = 0;
     bool tri_dirty = true;
     uint32_t tri_count_built = 0xffffffffu;
-    bool use_tri_bvh = true;  // RT_TRI_BVH=0 disables (A/B switch)
+    bool use_tri_bvh = true;  // tuning "tri_bvh" 0: the reference's sweep
     // Direction-ordered layouts of the binary accelerator for walks from global memory (LDS
     // modes 0/1; order_bvh_by_octant): per position of the 8 layouts the base node and the
     // layout's skip link (host-built with the tree), and the 32-B copy derived from the base
     // nodes on the device after every upload or refit (with the quantized copy).
-    // RT_TRI_OCTANTS=0: one layout (A/B switch).
+    // tuning "tri_octants" 0: one layout.
     bool use_tri_octants = true;
     uint32_t* d_tri_src8 = nullptr;
     uint32_t* d_tri_skip8 = nullptr;
     SphereBvhNode* d_tri_bvh8 = nullptr;
     size_t tri_src8_cap = 0, tri_skip8_cap = 0, tri_bvh8_cap = 0;
     bool tri_octants_built = false;  // d_tri_src8 / d_tri_skip8 describe the current tree
-    // rt_set_triangle_pruning / RT_TRI_PRUNE: distance pruning of the triangle walk (DESIGN.md
-    // §5.3c): 1 = certified by the leaf certificates (default, exact), 0 = box culling only,
-    // 2 = the round-3 relative slack (not exact)
+    // rt_set_triangle_pruning: distance pruning of the triangle walk: 1 =
+    // certified by the leaf certificates (default, exact), 0 = box culling only, 2 = the round-3
+    // relative slack (not exact: only this explicit call selects it)
     int tri_prune_mode = 1;
-    bool use_leafcert_lds = false;  // RT_TRI_LEAFCERT_LDS=1 (with a -DRT_LEAFCERT_LDS=1 build): mode-2 walks read them
-    // the triangles as a vertex table + 3 u16 indices each (build_compact_triangles), staged
-    // in LDS by mode-2 launches when it fits; valid only while it reproduces every record
-    float4* d_cverts = nullptr;
-    uint16_t* d_cidx = nullptr;
-    size_t cverts_cap = 0, cidx_cap = 0;
-    uint32_t cvert_count = 0;
-    bool compact_valid = false;
-    bool use_lds_compact = false;  // RT_TRI_LDS_COMPACT=1 (with a -DRT_LDS_COMPACT=1 build): stage the table
     // certified pruning (tri_cone.h): one certificate per leaf record, rebuilt on the device
     // after any change of the accelerator or the triangles
     TriLeafCert* d_tri_lcert = nullptr;
     size_t tri_lcert_cap = 0;
     bool cones_dirty = true;
     // cooperative leaf batches of the walks from global memory (pathtrace.hip coop_leaf_batch):
-    // the leaves' triangle blocks, rebuilt with the certificates; RT_COOP_LEAVES=0: per-lane leaf
-    // tests (A/B switch)
+    // the leaves' triangle blocks, rebuilt with the certificates; tuning "coop_leaves" 0:
+    // per-lane leaf tests
     bool use_coop_leaves = true;
-    // the 4-wide quantized accelerator (tri_q4.h) over the binary one, for walks from global
-    // memory: its links and child -> binary node map are built on the host at upload, its boxes on
-    // the device (after every upload or refit); RT_TRI_Q4=0: the binary walk (A/B switch)
-    bool use_q4 = false;
-    bool q4_built = false, q4_dirty = true;
-    uint32_t q4_nodes = 0, q4_depth = 0;
-    TriQ4Node* d_tri_q4 = nullptr;
-    uint32_t* d_tri_q4src = nullptr;
-    float4* d_tri_q4grid = nullptr;
-    size_t tri_q4_cap = 0, tri_q4src_cap = 0, tri_q4grid_cap = 0;
     uint4* d_tri_ltris = nullptr;
     size_t tri_ltris_cap = 0;
     bool ltris_dirty = true;
-    // the 4-wide accelerator (tri_wide.h), RT_TRI_WIDE=1 (A/B switch): measured slower than the
-    // binary one on C3-C5, so off by default
-    bool use_tri_wide = false;
-    int tri_compact = -1;        // RT_TRI_COMPACT: 1 / 0 force compact leaves on / off; -1 by size
-    bool wide_built = false;     // the accelerator on the device is the wide one
-    bool wide_refresh = false;   // triangles uploaded since the compact blocks were checked
-    TriWideNode* d_wide = nullptr;
-    TriLeaf* d_leaves = nullptr;
-    TriVertex* d_verts = nullptr;
-    uint32_t* d_vsrc = nullptr;
-    size_t wide_cap = 0, leaves_cap = 0, verts_cap = 0, vsrc_cap = 0;
-    uint32_t wide_leaves = 0, wide_verts = 0, wide_depth = 0, wide_compact_leaves = 0;
     // rt_set_brute_force: the reference's own sweeps (BASELINE config 5): 0 off, 1 LDS-tiled, 2
     // through the scalar cache (rt_brute_wf_kernel<tris, stream>)
     int brute = 0;
-    // coherent primary rays (rt_primary_kernel): RT_PRIMARY_PASS 1 / 0 force on / off, -1 by scene
+    // coherent primary rays (rt_primary_kernel): tuning "primary_pass" 1 / 0 force on / off, -1 by scene
     int primary_pass = -1;
     // Workgroup size of the pre-pass where the accelerator is walked from global memory (modes
     // 0/1): its packet walks are chains of dependent node loads, so resident waves are what
     // count; at 1024 threads and ~69 VGPRs only one workgroup (16 waves) fits a CU, at 256 seven
     // (28 waves): C5 5.69 -> 5.24 ms per frame (profiles/r03_ai/ab_c5_pthreads.jsonl); held to
     // 64 VGPRs, eight waves per SIMD (32 per CU): 5.04 ms (profiles/r03_aj/ab_c5_pthreads.jsonl).
-    // RT_PRIMARY_THREADS 64 / 128 / 256 / 512 / 1024 and RT_PRIMARY_WAVES 0 / 8 (A/B switches).
+    // tunings "primary_threads" 64 / 128 / 256 / 512 / 1024 and "primary_waves" 0 / 8.
     uint32_t primary_threads = 256;
     uint32_t primary_min_waves = 8;
     // a tile's frames on consecutive pre-pass waves, whose packets walk nearly the same nodes:
-    // C5 5.02 -> 4.93 ms (profiles/r03_al/ab_c5_ptm.jsonl); RT_PRIMARY_TILE_MAJOR=0: frame-major (A/B)
+    // C5 5.02 -> 4.93 ms (profiles/r03_al/ab_c5_ptm.jsonl); tuning "primary_tile_major" 0: frame-major
     bool primary_tile_major = true;
     uint4* d_primary[2] = {};   // per batch parity (overlapped batches), owned px x frames x samples records
     size_t primary_cap = 0;
-    unsigned long long* d_stream = nullptr;  // sub-object bytes the brute-force launches streamed
-    // the brute-force wavefront (rt_brute_wf_kernel; RT_BRUTE_WF=0: the lockstep rt_brute_kernel)
-    bool brute_wf = true;
+    // sub-object bytes of the brute-force launches: [0] SURVEY §8d's tile-streaming convention,
+    // [1] what the sweeps read from L2
+    unsigned long long* d_stream = nullptr;
+    // the brute-force wavefront (rt_brute_wf_kernel)
     float4* d_brute_paths = nullptr;
     uint32_t* d_brute_queue = nullptr;
     uint32_t* d_brute_counts = nullptr;
@@ -556,53 +514,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         return RT_OK;
     };
     int rc;
-    if (ctx->use_tri_wide) {
-        // compact leaves are built from the triangle records as the device holds them
-        const bool compact = ctx->tri_compact == 1 ||
-                             (ctx->tri_compact == -1 && (size_t)ctx->cap_tri * sizeof(RtTriangleHot) > kCompactMinTriBytes);
-        std::vector<RtTriangleHot> hot;
-        if (compact && ctx->cap_tri) {
-            hot.resize(ctx->cap_tri);
-            RT_HIP(ctx, join_aux(ctx));
-            RT_HIP(ctx, hipMemcpyAsync(hot.data(), ctx->d_tri, hot.size() * sizeof(RtTriangleHot), hipMemcpyDeviceToHost,
-                                       ctx->stream));
-            RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        }
-        TriWide w;
-        build_triangle_wide(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(),
-                            hot.empty() ? nullptr : reinterpret_cast<const float*>(hot.data()), (uint32_t)hot.size(), &w);
-        if (w.depth <= kWideMaxDepth) {
-            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_wide), &ctx->wide_cap, w.nodes.size() * sizeof(TriWideNode))) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_leaves), &ctx->leaves_cap, w.leaves.size() * sizeof(TriLeaf))) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_verts), &ctx->verts_cap, w.verts.size() * sizeof(TriVertex))) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_vsrc), &ctx->vsrc_cap, w.vsrc.size() * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_wide, w.nodes.data(), w.nodes.size() * sizeof(TriWideNode))) ||
-                (rc = upload_raw(ctx, ctx->d_leaves, w.leaves.data(), w.leaves.size() * sizeof(TriLeaf))) ||
-                (rc = upload_raw(ctx, ctx->d_verts, w.verts.data(), w.verts.size() * sizeof(TriVertex))) ||
-                (rc = upload_raw(ctx, ctx->d_vsrc, w.vsrc.data(), w.vsrc.size() * 4)) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_order), &ctx->tri_order_cap, w.order.size() * 4)) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_level_off), &ctx->tri_level_cap, w.level_off.size() * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_tri_order, w.order.data(), w.order.size() * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_tri_level_off, w.level_off.data(), w.level_off.size() * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_tri_extent, &w.extent, 4)))
-                return rc;
-            ctx->tri_nodes = (uint32_t)w.nodes.size();
-            ctx->wide_leaves = ctx->tri_prim_count = (uint32_t)w.leaves.size();
-            ctx->wide_verts = (uint32_t)w.verts.size();
-            ctx->wide_depth = w.depth;
-            ctx->wide_compact_leaves = 0;
-            for (const TriLeaf& L : w.leaves) ctx->wide_compact_leaves += (L.count_flags & kWideLeafCompact) ? 1u : 0u;
-            ctx->tri_levels = (uint32_t)w.level_off.size() - 1u;
-            ctx->wide_built = true;
-            ctx->tri_octants_built = false;
-            ctx->wide_refresh = false;
-            ctx->tri_dirty = false;
-            ctx->tri_count_built = object_count;
-            return RT_OK;
-        }
-        // deeper than the kernel's stack: the binary accelerator below
-    }
-    ctx->wide_built = false;
     TriangleAccel acc;
     build_triangle_accel(ctx->h_obj.data(), object_count, ctx->h_sub.data(), (uint32_t)ctx->h_sub.size(), &acc);
     const size_t nb = acc.nodes.size() * sizeof(SphereBvhNode), pb = acc.prims.size() * sizeof(SubObjectPrim);
@@ -612,7 +523,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
         (rc = upload_raw(ctx, ctx->d_tri_prims, acc.prims.data(), pb)))
         return rc;
     ctx->qnodes_dirty = true;
-    ctx->q4_dirty = true;
     ctx->cones_dirty = true;
     ctx->ltris_dirty = true;
     ctx->tri_nodes = (uint32_t)acc.nodes.size();
@@ -632,25 +542,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
             (rc = upload_raw(ctx, ctx->d_tri_skip8, skip.data(), b8)))
             return rc;
         ctx->tri_octants_built = true;
-    }
-    ctx->q4_built = false;
-    if (ctx->use_q4 && acc.nodes.size() > 1) {
-        std::vector<TriQ4Node> q4;
-        std::vector<uint32_t> q4src;
-        uint32_t q4depth = 0;
-        if (build_tri_q4(acc.nodes, &q4, &q4src, &q4depth)) {
-            // the links now; the boxes on the device (rt_tri_q4_fill_kernel, at the next launch)
-            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_q4), &ctx->tri_q4_cap, q4.size() * sizeof(TriQ4Node))) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_q4src), &ctx->tri_q4src_cap, q4src.size() * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_tri_q4, q4.data(), q4.size() * sizeof(TriQ4Node))) ||
-                (rc = upload_raw(ctx, ctx->d_tri_q4src, q4src.data(), q4src.size() * 4)))
-                return rc;
-            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tri_q4grid), &ctx->tri_q4grid_cap, 2 * sizeof(float4))))
-                return rc;
-            ctx->q4_nodes = (uint32_t)q4.size();
-            ctx->q4_depth = q4depth;
-            ctx->q4_built = true;
-        }
     }
     // depth levels for the device refit (preorder: a node precedes its children)
     std::vector<uint32_t> depth(acc.nodes.size(), 0);
@@ -679,93 +570,10 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
     return RT_OK;
 }
 
-// The triangles as a vertex table: vertices a, fl(a + edge_ab), fl(a + edge_ac) deduplicated
-// by bit pattern, and 3 u16 indices per triangle, when SceneTriangle::new's arithmetic
-// (src/buffers.rs:66-95, wide_tri_from_vertices) reproduces every record's edge_ab, edge_ac and
-// calc_normal bit for bit from them (the kernel recomputes those from the vertices), the
-// vertices number at most 65,536, and the table could fit the mode-2 LDS budget at all.
-bool build_compact_triangles(const rt_scene_triangle* t, uint32_t n, std::vector<float4>* verts,
-                             std::vector<uint16_t>* idx) {
-    if (n == 0 || (size_t)n * 6 > kLdsAccelBudget) return false;
-    struct Key {
-        uint32_t b[3];
-        uint32_t id;
-    };
-    std::vector<Key> keys(3 * (size_t)n);
-    for (uint32_t i = 0; i < n; i++) {
-        const rt_scene_triangle& r = t[i];
-        TriVertex v[3];
-        v[0] = TriVertex{r.a[0], r.a[1], r.a[2]};
-        v[1] = TriVertex{r.a[0] + r.edge_ab[0], r.a[1] + r.edge_ab[1], r.a[2] + r.edge_ab[2]};
-        v[2] = TriVertex{r.a[0] + r.edge_ac[0], r.a[1] + r.edge_ac[1], r.a[2] + r.edge_ac[2]};
-        float ab[3], ac[3], cn[3];
-        wide_tri_from_vertices(v[0], v[1], v[2], ab, ac, cn);
-        if (std::memcmp(ab, r.edge_ab, 12) || std::memcmp(ac, r.edge_ac, 12) || std::memcmp(cn, r.calc_normal, 12))
-            return false;
-        for (int k = 0; k < 3; k++) {
-            Key& q = keys[3 * (size_t)i + k];
-            std::memcpy(q.b, &v[k], 12);
-            q.id = 3u * i + (uint32_t)k;
-        }
-    }
-    std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
-        return std::memcmp(x.b, y.b, 12) < 0 || (std::memcmp(x.b, y.b, 12) == 0 && x.id < y.id);
-    });
-    verts->clear();
-    idx->assign(3 * (size_t)n + 1, 0);  // + 1: the kernel stages whole u32 words
-    for (size_t j = 0; j < keys.size(); j++) {
-        if (j == 0 || std::memcmp(keys[j].b, keys[j - 1].b, 12) != 0) {
-            if (verts->size() == 65536) return false;
-            float f[3];
-            std::memcpy(f, keys[j].b, 12);
-            verts->push_back(make_float4(f[0], f[1], f[2], 0.0f));
-        }
-        (*idx)[keys[j].id] = (uint16_t)(verts->size() - 1);
-    }
-    return true;
-}
-
 int upload_triangles(rt_ctx* ctx, const rt_scene_triangle* t, uint32_t n) {
     if (n == 0) return RT_OK;
     ctx->cones_dirty = true;
     ctx->ltris_dirty = true;
-    // the vertex table describes the whole buffer only when this upload rewrites all of it
-    ctx->compact_valid = false;
-    // the table is an option (a -DRT_LDS_COMPACT=1 build with RT_TRI_LDS_COMPACT=1): built only
-    // then, and an allocation failure here only leaves it invalid (the records are read)
-    if (kLdsCompactBuilt && ctx->use_lds_compact && n == ctx->cap_tri) {
-        std::vector<float4> verts;
-        std::vector<uint16_t> idx;
-        if (build_compact_triangles(t, n, &verts, &idx)) {
-            const size_t bv = verts.size() * sizeof(float4), bi = idx.size() * sizeof(uint16_t);
-            bool room = ctx->cverts_cap >= bv && ctx->cidx_cap >= bi;
-            if (!room) {
-                RT_HIP(ctx, join_aux(ctx));
-                RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-                if (ctx->d_cverts) (void)hipFree(ctx->d_cverts);
-                if (ctx->d_cidx) (void)hipFree(ctx->d_cidx);
-                ctx->d_cverts = nullptr;
-                ctx->d_cidx = nullptr;
-                ctx->cverts_cap = ctx->cidx_cap = 0;
-                if (hipMalloc(reinterpret_cast<void**>(&ctx->d_cverts), bv) == hipSuccess &&
-                    hipMalloc(reinterpret_cast<void**>(&ctx->d_cidx), bi) == hipSuccess) {
-                    ctx->cverts_cap = bv;
-                    ctx->cidx_cap = bi;
-                    room = true;
-                } else {
-                    (void)hipGetLastError();  // the optional table stays off; not a context error
-                }
-            }
-            if (room) {
-                int rc;
-                if ((rc = upload_raw(ctx, ctx->d_cverts, verts.data(), bv)) ||
-                    (rc = upload_raw(ctx, ctx->d_cidx, idx.data(), bi)))
-                    return rc;
-                ctx->cvert_count = (uint32_t)verts.size();
-                ctx->compact_valid = true;
-            }
-        }
-    }
     void* p;
     int rc = staging(ctx, (size_t)n * sizeof(RtTriangleHot), &p);
     if (rc) return rc;
@@ -941,82 +749,11 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
         if (e != hipSuccess) return bail(hip_fail(ctx, "hipDeviceGetAttribute", e));
         ctx->n_cu = n_cu;
-        const char* env = std::getenv("RT_SCENE_IN_LDS");
-        ctx->force_global_scene = env && env[0] == '0';
-        env = std::getenv("RT_LDS_MODE");
-        if (env) ctx->max_lds_mode = (int)std::strtol(env, nullptr, 10);
-        env = std::getenv("RT_BLOCK_THREADS");
-        ctx->force_threads = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
-        env = std::getenv("RT_WAVES_PER_CU");
-        ctx->waves_cap = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
-        env = std::getenv("RT_TRI_BVH");
-        ctx->use_tri_bvh = !(env && env[0] == '0');
-        env = std::getenv("RT_TRI_WIDE");
-        if (env) ctx->use_tri_wide = env[0] == '1';
-        env = std::getenv("RT_PRIMARY_PASS");
-        if (env) ctx->primary_pass = env[0] == '0' ? 0 : 1;
-        env = std::getenv("RT_PRIMARY_THREADS");
-        if (env) {
-            const uint32_t t = (uint32_t)std::strtoul(env, nullptr, 10);
-            if (t == 64u || t == 128u || t == 256u || t == 512u || t == 1024u) ctx->primary_threads = t;
-        }
-        env = std::getenv("RT_PRIMARY_TILE_MAJOR");
-        if (env) ctx->primary_tile_major = env[0] == '1';
-        env = std::getenv("RT_PRIMARY_WAVES");
-        if (env) ctx->primary_min_waves = env[0] == '8' ? 8u : 0u;
-        if (ctx->primary_threads != 256u) ctx->primary_min_waves = 0;  // the 64-VGPR variant is built at 256
-        env = std::getenv("RT_BRUTE_FORCE");
-        ctx->brute = !env ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : 0;
-        env = std::getenv("RT_BRUTE_WF");
-        if (env) ctx->brute_wf = env[0] != '0';
-        env = std::getenv("RT_TRI_COMPACT");
-        if (env) ctx->tri_compact = env[0] == '0' ? 0 : 1;
-        env = std::getenv("RT_SPHERE_LEAF");
-        ctx->sphere_leaf_max = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 0u;
-        env = std::getenv("RT_SPHERE_BVH");
-        ctx->use_bvh = !(env && env[0] == '0');
-        env = std::getenv("RT_SPHERE_OCTANTS");
-        ctx->sphere_octants = !(env && env[0] == '0');
-        env = std::getenv("RT_SPHERE_BOX_ORDER");
-        ctx->sphere_box_order = !(env && env[0] == '0');
-        env = std::getenv("RT_QUEUE_STRIPES");
-        if (env) ctx->queue_stripes = std::max<uint32_t>(1u, std::min<uint32_t>(kQueueStripesMax, (uint32_t)std::strtoul(env, nullptr, 10)));
-        env = std::getenv("RT_TRAV_THRESHOLD");
-        if (env) ctx->trav_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
-        env = std::getenv("RT_DRAIN_THRESHOLD");
-        if (env) ctx->drain_threshold = std::min<uint32_t>(63u, (uint32_t)std::strtoul(env, nullptr, 10));
-        env = std::getenv("RT_DRAIN_MIN_STEPS");
-        if (env) ctx->drain_min_steps = (uint32_t)std::strtoul(env, nullptr, 10);
-        env = std::getenv("RT_LEAF_BATCH");
-        if (env) ctx->leaf_batch = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (uint32_t)std::strtoul(env, nullptr, 10)));
-        env = std::getenv("RT_TILE_SCHEDULE");
-        if (env) ctx->tile_schedule = env[0] == '0' ? 0u : 1u;
-        env = std::getenv("RT_FRAME_PARALLEL");
-        if (env) ctx->frame_parallel = env[0] != '0';
-        env = std::getenv("RT_TRI_OCTANTS");
-        if (env) ctx->use_tri_octants = env[0] != '0';
-        env = std::getenv("RT_TRI_PRUNE");
-        if (env) ctx->tri_prune_mode = env[0] == '0' ? 0 : env[0] == '2' ? 2 : 1;
-        env = std::getenv("RT_TRI_QNODES");
-        if (env) ctx->use_qnodes = env[0] != '0';
-        env = std::getenv("RT_TRI_LEAFCERT_LDS");
-        if (env) ctx->use_leafcert_lds = env[0] == '1';
-        env = std::getenv("RT_TRI_Q4");
-        if (env) ctx->use_q4 = kQ4Built && env[0] != '0';
-        env = std::getenv("RT_COOP_LEAVES");
-        if (env) ctx->use_coop_leaves = env[0] != '0';
-        env = std::getenv("RT_TRI_LDS_COMPACT");
-        if (env) ctx->use_lds_compact = kLdsCompactBuilt && env[0] == '1';
-        env = std::getenv("RT_STAGE_SUBS");
-        if (env) ctx->stage_subs = env[0] != '0';
-        env = std::getenv("RT_FRAME_BATCH");
-        if (env) ctx->frame_batch = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxFrameBatch, (uint32_t)std::strtoul(env, nullptr, 10)));
-        env = std::getenv("RT_BATCH_OVERLAP");
-        if (env) ctx->batch_overlap = env[0] != '0';
-        env = std::getenv("RT_BATCH_SCHEDULE");
-        if (env) ctx->batch_schedule = env[0] == '1';
-        env = std::getenv("RT_UNIT_TILE_MAJOR");
-        if (env) ctx->unit_tile_major = env[0] != '0';
+        // the batch buffers' share of device memory: an eighth of the device
+        size_t free_b = 0, total_b = 0;
+        e = hipMemGetInfo(&free_b, &total_b);
+        if (e != hipSuccess) return bail(hip_fail(ctx, "hipMemGetInfo", e));
+        ctx->batch_budget = total_b / 8;
     }
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(hip_fail(ctx, "hipStreamCreate", e));
@@ -1049,7 +786,7 @@ int rt_create(const rt_create_info* info, rt_ctx** out_ctx) {
         (rc = dev_alloc(ctx, &ctx->d_mat, ctx->n_mat_dev)) || (rc = dev_alloc(ctx, &ctx->d_obj, info->object_count)) ||
         (rc = dev_alloc(ctx, &ctx->d_sub, ctx->n_sub_dev)) || (rc = dev_alloc(ctx, &ctx->d_tri, ctx->n_tri_dev)) ||
         (rc = dev_alloc(ctx, &ctx->d_tri_bounds, 2 * (size_t)ctx->n_tri_dev)) ||
-        (rc = dev_alloc(ctx, &ctx->d_tri_extent, 1)) || (rc = dev_alloc(ctx, &ctx->d_stream, 1)) ||
+        (rc = dev_alloc(ctx, &ctx->d_tri_extent, 1)) || (rc = dev_alloc(ctx, &ctx->d_stream, 2)) ||
         (rc = dev_alloc(ctx, &ctx->d_srgb, 256)) || (rc = dev_alloc(ctx, &ctx->d_tex, 1)) ||
         (rc = dev_alloc(ctx, &ctx->d_env, 1)))
         return bail(rc);
@@ -1085,10 +822,9 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_srgb, ctx->d_tri_extent, ctx->d_tri_order, ctx->d_tri_level_off, ctx->d_model,
                     ctx->d_tri_object, ctx->d_sub_object, ctx->d_object_tris, ctx->d_place, ctx->d_tri_bounds,
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
-                    ctx->d_clock, ctx->d_wide, ctx->d_leaves, ctx->d_verts, ctx->d_vsrc, ctx->d_stream,
-                    ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes, ctx->d_tri_qgrid, ctx->d_tri_src8,
-                    ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert, ctx->d_cverts, ctx->d_cidx, ctx->d_tri_ltris, ctx->d_tri_q4, ctx->d_tri_q4src,
-                    ctx->d_tri_q4grid, ctx->d_brute_paths, ctx->d_brute_queue, ctx->d_brute_counts};
+                    ctx->d_clock, ctx->d_stream, ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes,
+                    ctx->d_tri_qgrid, ctx->d_tri_src8, ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert,
+                    ctx->d_tri_ltris, ctx->d_brute_paths, ctx->d_brute_queue, ctx->d_brute_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1237,7 +973,6 @@ int rt_update_triangles(rt_ctx* ctx, const rt_scene_triangle* triangles, uint32_
     RT_ENTER(ctx);
     if (count && !triangles) return fail(ctx, RT_E_INVALID, "triangles is NULL");
     if (count > ctx->cap_tri) return fail(ctx, RT_E_CAPACITY, "more triangles than the buffer holds");
-    if (ctx->wide_built) ctx->wide_refresh = true;  // compact leaves rechecked before the next frame
     return upload_triangles(ctx, triangles, count);
 }
 
@@ -1303,23 +1038,39 @@ int rt_dispatch(rt_ctx* ctx, uint32_t bounces) {
     return dispatch_frames(ctx, bounces, 1);
 }
 
-// One launch rendering `frames` frames starting at Params.accumulation_index.
+static int dispatch_batch(rt_ctx* ctx, uint32_t bounces, uint32_t frames);
+
+// Renders `frames` frames starting at Params.accumulation_index: one launch (dispatch_batch),
+// or, when the batch's buffers -- the frame lights and the primary records, 32 B per owned
+// pixel, frame and sample each -- would outgrow the batch budget (an eighth of the device's
+// memory by default), consecutive launches of as many frames as fit, which render the same
+// bits: frames are independent but for the accumulation, which every launch adds to in order.
 static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
+    const rt_params& p = ctx->params;
+    const uint64_t samples = std::max<uint32_t>(1u, p.accumulate == 1u ? p.compute_per_frame : 1u);
+    const uint64_t per_frame = (uint64_t)ctx->owned_tiles * 64u * samples * 2u * 2u * sizeof(float4);
+    const uint64_t fit = std::max<uint64_t>(1u, ctx->batch_budget / std::max<uint64_t>(1u, per_frame));
+    if (frames <= fit) return dispatch_batch(ctx, bounces, frames);
+    const uint32_t k0 = ctx->params.accumulation_index;
+    int rc = RT_OK;
+    for (uint32_t done = 0; done < frames && rc == RT_OK;) {
+        const uint32_t n = (uint32_t)std::min<uint64_t>(fit, frames - done);
+        if (p.accumulate == 1u) ctx->params.accumulation_index = k0 + done;
+        rc = dispatch_batch(ctx, bounces, n);
+        done += n;
+    }
+    ctx->params.accumulation_index = k0;  // the batch's Params, as one launch leaves them
+    return rc;
+}
+
+// One launch rendering `frames` frames starting at Params.accumulation_index.
+static int dispatch_batch(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     const rt_params& p = ctx->params;
     {
         int rc = refresh_sphere_slots(ctx, p.sphere_count, p.object_count == 0);
         if (rc) return rc;
         rc = refresh_tri_accel(ctx, p.object_count);
         if (rc) return rc;
-        if (ctx->wide_built && ctx->wide_refresh) {  // triangles uploaded: vertex blocks and their check
-            RT_HIP(ctx, join_aux(ctx));
-            RT_HIP(ctx, rt_launch_wide_refresh(ctx->d_wide, ctx->d_leaves, ctx->wide_leaves, ctx->d_verts,
-                                               ctx->d_verts, ctx->d_vsrc, ctx->wide_verts, ctx->d_sub, ctx->d_tri,
-                                               ctx->n_tri_dev, ctx->d_tri_order, ctx->d_tri_level_off,
-                                               ctx->tri_levels, ctx->d_tri_extent, false, ctx->stream));
-            ctx->primary_dirty = true;
-            ctx->wide_refresh = false;
-        }
     }
     KernelArgs ka{};
     ka.camera_rays = ctx->d_rays;
@@ -1343,12 +1094,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tri_extent = ctx->d_tri_extent;
     ka.tri_bvh = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
     ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);
-    ka.tri_wide = reinterpret_cast<const float4*>(ctx->d_wide);
-    ka.tri_leaves = reinterpret_cast<const uint4*>(ctx->d_leaves);
-    ka.tri_verts = ctx->d_verts;
-    ka.tri_cverts = ctx->d_cverts;
-    ka.tri_cidx = ctx->d_cidx;
-    ka.tri_cvert_count = ctx->cvert_count;
     ka.materials = ctx->d_mat;
     ka.objects = ctx->d_obj;
     ka.sub_objects = ctx->d_sub;
@@ -1405,10 +1150,12 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         if (need > ctx->frame_light_cap) {
             // sized for the configured batch too, so a short first batch (a warmup)
             // does not leave a reallocation for a later, timed launch; two buffers,
-            // one per batch parity (overlapped batches)
+            // one per batch parity (overlapped batches), within the batch budget
             const size_t want = std::max<size_t>(
-                need, (size_t)owned_px * std::min<uint64_t>((uint64_t)ctx->frame_batch * p.compute_per_frame,
-                                                            kMaxParallelLights));
+                need, std::min<size_t>(ctx->batch_budget / (2 * sizeof(float4)),
+                                       (size_t)owned_px * std::min<uint64_t>((uint64_t)ctx->frame_batch *
+                                                                                 p.compute_per_frame,
+                                                                             kMaxParallelLights)));
             RT_HIP(ctx, join_aux(ctx));
             RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
             for (float4*& b : ctx->d_frame_light) {
@@ -1416,8 +1163,10 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
                 b = nullptr;
             }
             ctx->frame_light_cap = 0;
-            for (float4*& b : ctx->d_frame_light)
-                RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&b), want * sizeof(float4)));
+            for (float4*& b : ctx->d_frame_light) {
+                const hipError_t ea = hipMalloc(reinterpret_cast<void**>(&b), want * sizeof(float4));
+                if (ea != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("frame lights: ") + hipGetErrorString(ea));
+            }
             ctx->frame_light_cap = want;
         }
         ka.queue_units = ctx->owned_tiles * frames;
@@ -1427,9 +1176,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // dynamic LDS carve-up: sphere slots | materials | objects | slot->orig | sphere materials | BVH | srgb
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
     const bool tris = p.object_count != 0;  // else the sphere-only kernels
-    const bool wide = tris && ka.tri_accel && ctx->wide_built;
-    // the wide walk's stack: one entry per tree level below the root, per thread
-    const size_t stack_pt = wide ? 4u * std::max<uint32_t>(1u, ctx->wide_depth - 1u) : 0u;
     size_t mode1_bytes = 0, mode2_bytes = 0;
     // lays out the LDS image for `layouts` sphere BVH layouts and returns the LDS mode it fits
     auto carve = [&](uint32_t layouts, size_t mode1_budget) -> int {
@@ -1448,30 +1194,13 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         off = al16(off + (size_t)layouts * ctx->n_nodes * sizeof(SphereBvhNode));
         mode1_bytes = off + kLdsTailBytes;
         ka.lds_tri_nodes_offset = (uint32_t)off;
-        if (wide) {  // wide nodes only (leaf records stay in global memory)
-            off = al16(off + (size_t)ka.tri_nodes * sizeof(TriWideNode));
-            ka.lds_tri_prims_offset = (uint32_t)off;
-        } else {
-            off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
-            ka.lds_tri_prims_offset = (uint32_t)off;
-            off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
-        }
-        // the vertex-indexed triangles, when they fit the mode-2 budget (the leaves' triangle
-        // reads then stay in LDS; RT_TRI_LDS_COMPACT=0 switches it off)
-        ka.lds_cvert_offset = ka.lds_cidx_offset = 0;
-        if (!wide && ctx->compact_valid && ctx->use_lds_compact && ka.tri_accel && ka.triangle_count == ctx->cap_tri) {
-            const size_t cv = al16(off + (size_t)ctx->cvert_count * sizeof(float4));
-            const size_t ci = al16(cv + (3u * (size_t)ka.triangle_count + 1u) / 2u * 4u);
-            if (ci + kLdsTailBytes <= kLdsAccelBudget) {
-                ka.lds_cvert_offset = (uint32_t)off;
-                ka.lds_cidx_offset = (uint32_t)cv;
-                off = ci;
-            }
-        }
+        off = al16(off + (size_t)ka.tri_nodes * sizeof(SphereBvhNode));
+        ka.lds_tri_prims_offset = (uint32_t)off;
+        off = al16(off + (size_t)ka.tri_prim_count * sizeof(SubObjectPrim));
         // the sub-object records the leaves read, when they fit the mode-2 budget too
-        // (one dependent global load less per leaf test; RT_STAGE_SUBS=0 switches it off)
+        // (one dependent global load less per leaf test; tuning "stage_subs" 0 switches it off)
         ka.lds_sub_offset = 0;
-        if (!wide && ctx->stage_subs && ka.sub_object_count != 0) {
+        if (ctx->stage_subs && ka.sub_object_count != 0) {
             const size_t with = al16(off + (size_t)ka.sub_object_count * sizeof(RtSubObject));
             if (with + kLdsTailBytes <= kLdsAccelBudget) {
                 ka.lds_sub_offset = (uint32_t)off;
@@ -1480,9 +1209,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         mode2_bytes = off + kLdsTailBytes;
         if (ctx->force_global_scene) return 0;
-        // (the budget holds one 1024-thread workgroup's stack as well)
-        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes + 1024u * stack_pt <= kLdsAccelBudget &&
-            ctx->max_lds_mode >= 2)
+        if (ka.tri_accel && ka.tri_nodes != 0 && mode2_bytes <= kLdsAccelBudget && ctx->max_lds_mode >= 2)
             return 2;
         if (mode1_bytes <= mode1_budget && ctx->max_lds_mode >= 1) return 1;
         return 0;
@@ -1499,17 +1226,18 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             carve(1, kLdsSceneBudget);
     }
     if (ctx->brute) {
-        // the reference's sweeps (rt_brute_kernel): the mode-1 scene image, then one
-        // LDS tile of sub-object records; frames of a batch run back to back per pixel
+        // the reference's sweeps as a wavefront (rt_brute_wf_kernel): the mode-1 scene image,
+        // then the sub-object tiles (mode 1) or the hit lists (mode 2: the records through the
+        // scalar cache; a scene without triangles has no records to stream and sweeps its
+        // spheres in the LDS-tiled kernel); every pass (frame, sample) in order, one launch per
+        // bounce level
         carve(1, kLdsSceneBudget);
         ka.lds_srgb_offset = (uint32_t)(mode1_bytes - kLdsTailBytes);
         ka.lds_stack_offset = (uint32_t)al16(mode1_bytes);
         const uint32_t samples = ka.accumulate == 1u ? ka.compute_per_frame : 1u;
         const uint64_t passes = (uint64_t)frames * samples;
-        // the wavefront: every pass (frame, sample) in order, one launch per bounce level
-        const bool wf = ctx->brute_wf && passes > 0 && passes <= (1u << 20) && bounces + 2u <= kBruteLevels;
-        const bool scalar_stream = wf && tris && ctx->brute == 2;
-        const size_t lds = ka.lds_stack_offset + (wf ? rt_brute_wf_tile_bytes(scalar_stream) : rt_brute_tile_bytes());
+        const bool scalar_stream = tris && ctx->brute == 2;
+        const size_t lds = ka.lds_stack_offset + rt_brute_wf_tile_bytes(scalar_stream);
         int dev = 0, max_optin = 0;
         RT_HIP(ctx, hipGetDevice(&dev));
         RT_HIP(ctx, hipDeviceGetAttribute(&max_optin, hipDeviceAttributeSharedMemPerBlockOptin, dev));
@@ -1518,6 +1246,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.sphere_octant_stride = 0;
         ka.sphere_boxes_ordered = 0;
         ka.stream_bytes = ctx->d_stream;
+        ka.l2_stream_bytes = ctx->d_stream + 1;
         ka.frame_light = nullptr;
         RT_HIP(ctx, join_aux(ctx));
         ka.launch_clock = nullptr;
@@ -1535,35 +1264,33 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             ka.launch_clock = ctx->d_clock + kClockWords * (size_t)slot;  // zero: dev_alloc / collect_timing
             ctx->clock_pending.push_back(slot);
         }
-        if (wf) {
-            const size_t n_slots = (size_t)ctx->owned_tiles * 64u;
-            int rc;
-            if ((rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_paths), &ctx->brute_paths_cap,
-                                  4 * n_slots * sizeof(float4))) ||
-                (rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_queue), &ctx->brute_queue_cap,
-                                  2 * n_slots * sizeof(uint32_t))) ||
-                (rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_counts), &ctx->brute_counts_cap,
-                                  passes * kBruteLevels * sizeof(uint32_t))))
-                return rc;
-            RT_HIP(ctx, hipMemsetAsync(ctx->d_brute_counts, 0, passes * kBruteLevels * sizeof(uint32_t), ctx->stream));
-            ka.brute_paths = ctx->d_brute_paths;
-            ka.brute_queue = ctx->d_brute_queue;
-            ka.brute_counts = ctx->d_brute_counts;
-            // workgroups per launch: enough for every chunk of queue entries, at most 16 per CU
-            const uint32_t chunks = (uint32_t)((n_slots + rt_brute_wf_chunk() - 1u) / rt_brute_wf_chunk());
-            const uint32_t blocks = std::min<uint32_t>(chunks, 16u * (uint32_t)std::max<int>(1, (int)ctx->n_cu));
-            for (uint64_t pass = 0; pass < passes; ++pass)
-                for (uint32_t level = 0; level < std::max(1u, bounces); ++level) {
-                    ka.brute_pass = (uint32_t)pass;
-                    ka.brute_level = level;
-                    RT_HIP(ctx, rt_launch_brute_wf(ka, tris, scalar_stream, lds, blocks, ctx->stream));
-                }
-            ctx->last_blocks = blocks;
-        } else {
-            RT_HIP(ctx, rt_launch_brute(ka, tris, lds, ctx->stream));
-            ctx->last_blocks = (ctx->owned_tiles + 3u) / 4u;
-        }
-        ctx->last_passes = RT_PASS_BRUTE;
+        const size_t n_slots = (size_t)ctx->owned_tiles * 64u;
+        // per pass one counter per bounce level: the entries of each level's queue
+        ka.brute_levels = std::max(1u, bounces) + 1u;
+        const size_t n_counts = (size_t)passes * ka.brute_levels;
+        int rc;
+        if ((rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_paths), &ctx->brute_paths_cap,
+                              4 * n_slots * sizeof(float4))) ||
+            (rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_queue), &ctx->brute_queue_cap,
+                              2 * n_slots * sizeof(uint32_t))) ||
+            (rc = grow_buffer(ctx, reinterpret_cast<void**>(&ctx->d_brute_counts), &ctx->brute_counts_cap,
+                              n_counts * sizeof(uint32_t))))
+            return rc;
+        RT_HIP(ctx, hipMemsetAsync(ctx->d_brute_counts, 0, n_counts * sizeof(uint32_t), ctx->stream));
+        ka.brute_paths = ctx->d_brute_paths;
+        ka.brute_queue = ctx->d_brute_queue;
+        ka.brute_counts = ctx->d_brute_counts;
+        // workgroups per launch: enough for every chunk of queue entries, at most 16 per CU
+        const uint32_t chunks = (uint32_t)((n_slots + rt_brute_wf_chunk() - 1u) / rt_brute_wf_chunk());
+        const uint32_t blocks = std::min<uint32_t>(chunks, 16u * (uint32_t)std::max<int>(1, (int)ctx->n_cu));
+        for (uint64_t pass = 0; pass < passes; ++pass)
+            for (uint32_t level = 0; level < std::max(1u, bounces); ++level) {
+                ka.brute_pass = (uint32_t)pass;
+                ka.brute_level = level;
+                RT_HIP(ctx, rt_launch_brute_wf(ka, tris, scalar_stream, lds, blocks, ctx->stream));
+            }
+        ctx->last_blocks = blocks;
+        ctx->last_passes = RT_PASS_BRUTE | (scalar_stream ? RT_PASS_BRUTE_STREAM : 0u);
         ctx->last_lds = (uint32_t)lds;
         ctx->occ_threads = 256;
         ctx->primary_dirty = true;
@@ -1572,7 +1299,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.sphere_nodes = layouts * ctx->n_nodes;
     ka.sphere_octant_stride = layouts == 8 ? ctx->n_nodes : 0u;
     ka.sphere_boxes_ordered = (layouts == 8 && ctx->sphere_boxes_ordered && !tris) ? 1u : 0u;
-    const bool certified = tris && !wide && mode <= 1 && ka.tri_accel && ctx->tri_prune_mode == 1;
+    const bool certified = tris && mode <= 1 && ka.tri_accel && ctx->tri_prune_mode == 1;
     ka.trav_threshold = ctx->trav_threshold ? ctx->trav_threshold : trav_threshold_for(mode, tris, certified);
     ka.leaf_batch = ctx->leaf_batch ? ctx->leaf_batch : leaf_batch_for(mode, certified);
     // walks of the binary triangle accelerator from global memory read its direction-ordered
@@ -1580,7 +1307,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     ka.tri_qnodes = nullptr;
     ka.tri_qgrid = nullptr;
     ka.tri_octant_stride = 0;
-    const bool global_walk = tris && !wide && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0;
+    const bool global_walk = tris && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0;
     const bool octants = global_walk && ctx->tri_octants_built;
     const bool qnodes = global_walk && ctx->use_qnodes;
     if (octants || qnodes) {
@@ -1594,7 +1321,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
             RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qnodes), (size_t)n_out * sizeof(uint4)));
             ctx->qnodes_cap = n_out;
             ctx->qnodes_dirty = true;
-            ctx->q4_dirty = true;
         }
         if (!ctx->d_tri_qgrid) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_tri_qgrid), 2 * sizeof(float4)));
         if (ctx->qnodes_dirty || ctx->derived_octants != octants || ctx->derived_qnodes != qnodes) {
@@ -1622,10 +1348,10 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     // distance pruning of the binary walk: certified (the leaf certificates,
     // rebuilt on the device after any change), or the round-3 relative slack, or none
-    ka.tri_prune_mode = (tris && !wide && ka.tri_accel && ka.tri_nodes != 0) ? (uint32_t)ctx->tri_prune_mode : 0u;
+    ka.tri_prune_mode = (tris && ka.tri_accel && ka.tri_nodes != 0) ? (uint32_t)ctx->tri_prune_mode : 0u;
     ka.tri_prune = ka.tri_prune_mode == 2u ? kTriPruneRho : 0.0f;
     ka.tri_leafcert = nullptr;
-    if (ka.tri_prune_mode == 1u && ka.tri_prim_count != 0 && (mode <= 1 || ctx->use_leafcert_lds)) {
+    if (ka.tri_prune_mode == 1u && ka.tri_prim_count != 0 && mode <= 1) {  // (mode 2 culls by box alone)
         const size_t bytes = (size_t)ka.tri_prim_count * sizeof(TriLeafCert);
         if (ctx->tri_lcert_cap < bytes) {  // (re)allocate: nothing may still read them
             RT_HIP(ctx, join_aux(ctx));
@@ -1647,7 +1373,7 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     // cooperative leaf batches (walks from global memory): the leaves' triangle blocks
     ka.tri_leaftris = nullptr;
-    const bool coop = tris && !wide && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0 && ka.tri_prim_count != 0 &&
+    const bool coop = tris && mode <= 1 && ka.tri_accel && ka.tri_nodes != 0 && ka.tri_prim_count != 0 &&
                       ctx->use_coop_leaves;
     if (coop) {
         const size_t bytes = (size_t)ka.tri_prim_count * kLeafTriWords * sizeof(uint4);
@@ -1669,21 +1395,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         }
         ka.tri_leaftris = ctx->d_tri_ltris;
     }
-    // the 4-wide quantized walk (needs the cooperative leaf batches' LDS layout beside it)
-    ka.tri_q4 = nullptr;
-    ka.tri_q4grid = nullptr;
-    const bool q4 = coop && ctx->q4_built && ctx->use_q4 && ctx->tri_prune_mode != 2;  // (mode 2: the binary walk's slack)
-    if (q4) {
-        if (ctx->q4_dirty) {
-            RT_HIP(ctx, rt_launch_tri_q4_fill(reinterpret_cast<const SphereBvhNode*>(ctx->d_tri_bvh), ctx->tri_nodes,
-                                              ctx->d_tri_q4src, ctx->q4_nodes, ctx->d_tri_q4, ctx->d_tri_q4grid,
-                                              ctx->stream));
-            ctx->q4_dirty = false;
-            ctx->primary_dirty = true;  // an auxiliary-stream batch waits for it
-        }
-        ka.tri_q4 = reinterpret_cast<const uint4*>(ctx->d_tri_q4);
-        ka.tri_q4grid = ctx->d_tri_q4grid;
-    }
     size_t lds_bytes;
     if (mode == 2) {
         ka.lds_srgb_offset = (uint32_t)(mode2_bytes - kLdsTailBytes);
@@ -1695,33 +1406,27 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
         ka.lds_srgb_offset = 0;
         lds_bytes = kLdsTailBytes;
     }
-    // per-thread LDS after the scene image: the wide walk's stack, or the cooperative leaf
-    // batch's per-wave scratch
-    const size_t lane_pt =
-        wide ? stack_pt : coop ? (size_t)kLeafBatchWaveBytes / 64u + (q4 ? 4u * kQ4StackEntries : 0u) : 0u;
+    // per-thread LDS after the scene image: the cooperative leaf batch's per-wave scratch
+    const size_t lane_pt = coop ? (size_t)kLeafBatchWaveBytes / 64u : 0u;
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode ||
-        ctx->occ_tris != tris || ctx->occ_wide != wide || ctx->occ_stack_pt != lane_pt) {
+        ctx->occ_tris != tris || ctx->occ_stack_pt != lane_pt) {
         int per_cu = 0;
         uint32_t threads = 0;
-        hipError_t oe = rt_pathtrace_pick_config(mode, tris, wide, lds_bytes, lane_pt, ctx->force_threads,
-                                                 ctx->waves_cap, &threads, &per_cu);
+        hipError_t oe = rt_pathtrace_pick_config(mode, tris, lds_bytes, lane_pt, ctx->force_threads, ctx->waves_cap,
+                                                 &threads, &per_cu);
         if (oe != hipSuccess) return hip_fail(ctx, "rt_pathtrace_pick_config (occupancy query)", oe);
         ctx->occ_blocks_per_cu = per_cu;
         ctx->occ_threads = threads;
         ctx->occ_lds_bytes = lds_bytes;
         ctx->occ_mode = mode;
         ctx->occ_tris = tris;
-        ctx->occ_wide = wide;
         ctx->occ_stack_pt = lane_pt;
     }
-    // the stack after the scene image and its tail
-    ka.lds_stack_offset = (uint32_t)al16(lds_bytes);
-    ka.lds_leafbatch_offset = ka.lds_stack_offset;
-    // the 4-wide walk's stacks after the leaf batch scratch: entry e of thread t at [e * threads + t]
-    ka.lds_q4stack_offset = ka.lds_stack_offset + (uint32_t)(ctx->occ_threads / 64u) * kLeafBatchWaveBytes;
-    if (wide || coop) lds_bytes = ka.lds_stack_offset + (size_t)ctx->occ_threads * lane_pt;
+    // the leaf batch scratch after the scene image and its tail
+    ka.lds_leafbatch_offset = (uint32_t)al16(lds_bytes);
+    if (coop) lds_bytes = ka.lds_leafbatch_offset + (size_t)ctx->occ_threads * lane_pt;
     const uint32_t waves_per_block = ctx->occ_threads / 64;
     const uint64_t resident = (uint64_t)ctx->occ_blocks_per_cu * (uint64_t)(ctx->n_cu > 0 ? ctx->n_cu : 1);
     const uint64_t wanted = ((uint64_t)ka.queue_units + waves_per_block - 1) / waves_per_block;
@@ -1798,42 +1503,43 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     // accelerator stays in global memory (mode 1 with triangles, C5: wall -12%); with the
     // accelerator in LDS (C3, C4) or no triangles (C2) the pass costs more wall time than it
     // takes off the path kernel (+13%, +13%, +23%: profiles/r03_i/ab_primary.jsonl)
-    const bool primary = bounces > 0 && mode >= 1 && tris && !wide && ka.compute_per_frame > 0 &&
-                         (ctx->primary_pass == 1 || (ctx->primary_pass == -1 && mode == 1));
+    // (within the batch budget: a batch too large for it traces its first segments in the path kernel)
+    const size_t primary_need =
+        (size_t)owned_px * frames * std::max<uint32_t>(1u, p.accumulate == 1u ? p.compute_per_frame : 1u);
+    const bool primary = bounces > 0 && mode >= 1 && tris && ka.compute_per_frame > 0 &&
+                         (ctx->primary_pass == 1 || (ctx->primary_pass == -1 && mode == 1)) &&
+                         2 * primary_need * sizeof(uint4) <= ctx->batch_budget;
     ka.primary = nullptr;
     if (primary) {
         const int pi = (int)(ctx->batches & 1u);
-        const size_t need = (size_t)owned_px * frames * std::max<uint32_t>(1u, p.accumulate == 1u ? p.compute_per_frame : 1u);
+        const size_t need = primary_need;
         if (need > ctx->primary_cap) {
             RT_HIP(ctx, join_aux(ctx));
             RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            const size_t want = std::max<size_t>(need, (size_t)owned_px * ctx->frame_batch);
+            const size_t want = std::max<size_t>(
+                need, std::min<size_t>(ctx->batch_budget / (2 * sizeof(uint4)), (size_t)owned_px * ctx->frame_batch));
             for (uint4*& b : ctx->d_primary) {
                 if (b) RT_HIP(ctx, hipFree(b));
                 b = nullptr;
             }
             ctx->primary_cap = 0;
-            for (uint4*& b : ctx->d_primary) RT_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&b), want * 16));
+            for (uint4*& b : ctx->d_primary) {
+                const hipError_t ea = hipMalloc(reinterpret_cast<void**>(&b), want * 16);
+                if (ea != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("primary records: ") + hipGetErrorString(ea));
+            }
             ctx->primary_cap = want;
         }
         KernelArgs pka = ka;
         pka.primary = ctx->d_primary[pi];
         pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile)
         pka.primary_tile_major = ctx->primary_tile_major ? 1u : 0u;
-        size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
-        // the 4-wide packet walk's per-wave stacks after the image (3 entries per level at most)
-        pka.lds_q4packet_offset = 0;
-        if (q4 && mode <= 1 && 3u * ctx->q4_depth <= kQ4PacketStack) {
-            pka.lds_q4packet_offset = (uint32_t)al16(image);
-            const uint32_t pthreads = ctx->primary_threads ? ctx->primary_threads : 1024u;
-            image = pka.lds_q4packet_offset + (size_t)(pthreads / 64u) * kQ4PacketStack * 12u;
-        }
-        // (the 4-wide packet walk needs ~90 VGPRs: the 64-VGPR variant would spill)
-        RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, mode == 2 ? 1024u : ctx->primary_threads,
-                                      (mode == 2 || pka.lds_q4packet_offset) ? 0u : ctx->primary_min_waves, S));
+        const size_t image = mode == 2 ? mode2_bytes : mode1_bytes;
+        // (the 64-VGPR variant is built at 256 threads only)
+        const uint32_t min_waves = (mode == 2 || ctx->primary_threads != 256u) ? 0u : ctx->primary_min_waves;
+        RT_HIP(ctx, rt_launch_primary(pka, mode, tris, image, mode == 2 ? 1024u : ctx->primary_threads, min_waves, S));
         ka.primary = pka.primary;
     }
-    hipError_t e = rt_launch_pathtrace(ka, mode, tris, wide, ctx->occ_threads, lds_bytes, blocks, S);
+    hipError_t e = rt_launch_pathtrace(ka, mode, tris, ctx->occ_threads, lds_bytes, blocks, S);
     ctx->last_blocks = blocks;
     ctx->last_passes = RT_PASS_PATH | (primary ? RT_PASS_PRIMARY : 0u) | (frame_par ? RT_PASS_RESOLVE : 0u);
     ctx->last_lds = (uint32_t)lds_bytes;
@@ -1930,6 +1636,16 @@ int rt_synchronize(rt_ctx* ctx) {
 int rt_copy_output_to_device(rt_ctx* ctx, void* dst_device, uint32_t bytes_per_row) {
     RT_ENTER(ctx);  // queued frames launched first: the copy sees the last frame's output
     if (!dst_device) return fail(ctx, RT_E_INVALID, "rt_copy_output_to_device: dst_device is NULL");
+    if (ctx->world > 1)  // a rank's output holds only its own tiles: gather first (rt_gather_frame)
+        return fail(ctx, RT_E_INVALID, "rt_copy_output_to_device: a rank context (world_size > 1) has no full frame");
+    {
+        hipPointerAttribute_t attr{};
+        const hipError_t ea = hipPointerGetAttributes(&attr, dst_device);
+        if (ea != hipSuccess || attr.type != hipMemoryTypeDevice || attr.device != ctx->device) {
+            (void)hipGetLastError();
+            return fail(ctx, RT_E_INVALID, "rt_copy_output_to_device: dst_device is not device memory of the context's device");
+        }
+    }
     if ((uint64_t)bytes_per_row < 4ull * ctx->width)
         return fail(ctx, RT_E_INVALID, "rt_copy_output_to_device: bytes_per_row < 4 * width");
     RT_HIP(ctx, hipMemcpy2DAsync(dst_device, bytes_per_row, ctx->d_out, 4u * (size_t)ctx->width,
@@ -2028,20 +1744,11 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
                                count, ctx->model_tris, (uint32_t)ctx->h_sub.size(), ctx->d_tri, ctx->d_tri_bounds,
                                ctx->d_sub, ctx->d_obj, ctx->stream));
     ctx->geom_on_device = true;
-    ctx->compact_valid = false;  // the triangles changed on the device: mode 2 reads the records
-    // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds,
-    // and the wide one's compact leaves are rechecked against the new triangles
-    if (ctx->wide_built && ctx->tri_nodes && !ctx->tri_dirty) {
-        RT_HIP(ctx, rt_launch_wide_refresh(ctx->d_wide, ctx->d_leaves, ctx->wide_leaves, ctx->d_verts, ctx->d_verts,
-                                           ctx->d_vsrc, ctx->wide_verts, ctx->d_sub, ctx->d_tri, ctx->n_tri_dev,
-                                           ctx->d_tri_order, ctx->d_tri_level_off, ctx->tri_levels,
-                                           ctx->d_tri_extent, true, ctx->stream));
-        ctx->wide_refresh = false;
-    } else if (!ctx->wide_built && ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty) {
+    // the accelerator keeps its topology; its boxes (and the margin extent) follow the new bounds
+    if (ctx->d_tri_bvh && ctx->tri_nodes && !ctx->tri_dirty) {
         RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,
                                     ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
         ctx->qnodes_dirty = true;
-        ctx->q4_dirty = true;
     }
     ctx->cones_dirty = true;  // the triangles changed
     ctx->ltris_dirty = true;
@@ -2128,11 +1835,113 @@ int rt_set_triangle_pruning(rt_ctx* ctx, int mode) {
 int rt_streamed_bytes(rt_ctx* ctx, uint64_t* out) {
     RT_ENTER(ctx);
     if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
-    unsigned long long v = 0;
-    RT_HIP(ctx, hipMemcpyAsync(&v, ctx->d_stream, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long v[2] = {0, 0};
+    RT_HIP(ctx, hipMemcpyAsync(v, ctx->d_stream, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    *out = v;
+    *out = v[0];
     return RT_OK;
+}
+
+int rt_streamed_bytes_l2(rt_ctx* ctx, uint64_t* out) {
+    RT_ENTER(ctx);
+    if (!out) return fail(ctx, RT_E_INVALID, "out is NULL");
+    unsigned long long v[2] = {0, 0};
+    RT_HIP(ctx, hipMemcpyAsync(v, ctx->d_stream, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *out = v[1];
+    return RT_OK;
+}
+
+// Exact variants of the schedule and the acceleration structures, for A/B measurements (the
+// product reads no environment): every setting renders the same bits.
+int rt_set_tuning(rt_ctx* ctx, const char* key, int32_t value) {
+    RT_ENTER(ctx);
+    if (!key) return fail(ctx, RT_E_INVALID, "rt_set_tuning: key is NULL");
+    const std::string k(key);
+    const int32_t v = value;
+    auto range = [&](int32_t lo, int32_t hi) {
+        return v >= lo && v <= hi ? RT_OK
+                                  : fail(ctx, RT_E_INVALID, "rt_set_tuning: " + k + " must be in [" + std::to_string(lo) +
+                                                                ", " + std::to_string(hi) + "]");
+    };
+    auto flag = [&](bool& field) {
+        const int rc = range(0, 1);
+        if (rc == RT_OK) field = v != 0;
+        return rc;
+    };
+    int rc = RT_OK;
+    if (k == "scene_in_lds") {
+        if ((rc = range(0, 1)) == RT_OK) ctx->force_global_scene = v == 0;
+    } else if (k == "lds_mode") {
+        if ((rc = range(0, 2)) == RT_OK) ctx->max_lds_mode = v;
+    } else if (k == "block_threads") {
+        if (v != 0 && v != 256 && v != 512 && v != 1024)
+            return fail(ctx, RT_E_INVALID, "rt_set_tuning: block_threads must be 0, 256, 512 or 1024");
+        ctx->force_threads = (uint32_t)v;
+        ctx->occ_blocks_per_cu = 0;
+    } else if (k == "waves_per_cu") {
+        if ((rc = range(0, 32)) == RT_OK) {
+            ctx->waves_cap = (uint32_t)v;
+            ctx->occ_blocks_per_cu = 0;
+        }
+    } else if (k == "tri_bvh") {
+        if ((rc = flag(ctx->use_tri_bvh)) == RT_OK) ctx->tri_dirty = true;
+    } else if (k == "tri_octants") {
+        if ((rc = flag(ctx->use_tri_octants)) == RT_OK) ctx->tri_dirty = true;
+    } else if (k == "tri_qnodes") {
+        rc = flag(ctx->use_qnodes);
+    } else if (k == "coop_leaves") {
+        rc = flag(ctx->use_coop_leaves);
+    } else if (k == "stage_subs") {
+        rc = flag(ctx->stage_subs);
+    } else if (k == "primary_pass") {
+        if ((rc = range(-1, 1)) == RT_OK) ctx->primary_pass = v;
+    } else if (k == "primary_threads") {
+        if (v != 64 && v != 128 && v != 256 && v != 512 && v != 1024)
+            return fail(ctx, RT_E_INVALID, "rt_set_tuning: primary_threads must be 64, 128, 256, 512 or 1024");
+        ctx->primary_threads = (uint32_t)v;
+    } else if (k == "primary_waves") {
+        if (v != 0 && v != 8) return fail(ctx, RT_E_INVALID, "rt_set_tuning: primary_waves must be 0 or 8");
+        ctx->primary_min_waves = (uint32_t)v;
+    } else if (k == "primary_tile_major") {
+        rc = flag(ctx->primary_tile_major);
+    } else if (k == "sphere_bvh") {
+        if ((rc = flag(ctx->use_bvh)) == RT_OK) ctx->slots_dirty = true;
+    } else if (k == "sphere_leaf") {
+        if ((rc = range(0, 64)) == RT_OK) {
+            ctx->sphere_leaf_max = (uint32_t)v;
+            ctx->slots_dirty = true;
+        }
+    } else if (k == "sphere_octants") {
+        rc = flag(ctx->sphere_octants);
+    } else if (k == "sphere_box_order") {
+        if ((rc = flag(ctx->sphere_box_order)) == RT_OK) ctx->slots_dirty = true;
+    } else if (k == "queue_stripes") {
+        if ((rc = range(1, (int32_t)kQueueStripesMax)) == RT_OK) ctx->queue_stripes = (uint32_t)v;
+    } else if (k == "trav_threshold") {
+        if ((rc = range(0, 63)) == RT_OK) ctx->trav_threshold = (uint32_t)v;
+    } else if (k == "drain_threshold") {
+        if ((rc = range(0, 63)) == RT_OK) ctx->drain_threshold = (uint32_t)v;
+    } else if (k == "drain_min_steps") {
+        if ((rc = range(0, 1 << 20)) == RT_OK) ctx->drain_min_steps = (uint32_t)v;
+    } else if (k == "leaf_batch") {
+        if ((rc = range(0, 8)) == RT_OK) ctx->leaf_batch = (uint32_t)v;
+    } else if (k == "tile_schedule") {
+        if ((rc = range(0, 1)) == RT_OK) ctx->tile_schedule = (uint32_t)v;
+    } else if (k == "frame_parallel") {
+        rc = flag(ctx->frame_parallel);
+    } else if (k == "batch_overlap") {
+        rc = flag(ctx->batch_overlap);
+    } else if (k == "batch_schedule") {
+        rc = flag(ctx->batch_schedule);
+    } else if (k == "unit_tile_major") {
+        rc = flag(ctx->unit_tile_major);
+    } else if (k == "batch_memory_mb") {
+        if ((rc = range(1, 1 << 30)) == RT_OK) ctx->batch_budget = (size_t)v << 20;
+    } else {
+        return fail(ctx, RT_E_INVALID, "rt_set_tuning: unknown key " + k);
+    }
+    return rc;
 }
 
 int rt_set_tile_schedule(rt_ctx* ctx, uint32_t schedule) {
@@ -2172,7 +1981,7 @@ int rt_tile_schedule_state(rt_ctx* ctx, uint32_t* order, uint32_t* costs) {
 int rt_reset_ray_count(rt_ctx* ctx) {
     RT_ENTER(ctx);
     RT_HIP(ctx, hipMemsetAsync(ctx->d_counter, 0, (1 + kDiagCounters) * sizeof(unsigned long long), ctx->stream));
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_stream, 0, sizeof(unsigned long long), ctx->stream));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_stream, 0, 2 * sizeof(unsigned long long), ctx->stream));
     return RT_OK;
 }
 

@@ -9,9 +9,6 @@
 #include <stdint.h>
 
 #include "tri_cone.h"
-#include "tri_q4.h"
-#include "tri_wide.h"
-
 
 struct RtSphere {  // src/buffers.rs:40-45, 32 B
     float position[3];
@@ -103,22 +100,9 @@ constexpr uint32_t kLeafTriSlots = 8;                       // triangle slots pe
 constexpr uint32_t kLeafTriWords = 3 * kLeafTriSlots;       // uint4 per block (384 B)
 constexpr uint32_t kLeafBatchWaveBytes = 64 * 48;
 
-// The brute-force wavefront: counters per pass (bounce levels 0..kBruteLevels-1, the last two
-// words the pass's claim counters); a launch has at most kBruteLevels - 2 bounces per path.
-constexpr uint32_t kBruteLevels = 64;
-
 // Diagnostic counters ahead of the per-wave records in KernelArgs::diag
 // (RT_DIAG: words 0-25; RT_DIAG_TAIL: words 0-7, then 2 words per wave from here).
 constexpr uint32_t kDiagHeaderWords = 32;
-
-// The LDS vertex table (mode 2, pathtrace.hip compact_tri): build switch, off
-// by default -- compiled in, its code cost the LDS-resident instances more registers than its
-// smaller triangle reads saved (C3 0.304 -> 0.317 ms per frame with it off at run time, 0.349
-// on). Without it the host builds no table and leaves the LDS offsets at 0.
-#ifndef RT_LDS_COMPACT
-#define RT_LDS_COMPACT 0
-#endif
-constexpr bool kLdsCompactBuilt = RT_LDS_COMPACT != 0;
 
 struct KernelArgs {
     // framebuffer (bindings 1, 2, 6)
@@ -152,15 +136,6 @@ struct KernelArgs {
     // (LDS modes 0/1); tri_qgrid = {origin.xyz, valid}, {scale.xyz, 0}. Null: the 32-B nodes.
     const uint4* __restrict__ tri_qnodes;
     const float4* __restrict__ tri_qgrid;
-    // 4-wide triangle accelerator (tri_wide.h), used by the kWide instances instead of tri_bvh / tri_prims
-    const float4* __restrict__ tri_wide;          // TriWideNode[tri_nodes] as 8 float4 each
-    const uint4* __restrict__ tri_leaves;         // TriLeaf as 4 uint4 each
-    const TriVertex* __restrict__ tri_verts;      // compact leaves' vertex blocks
-    // vertex-indexed copy of the triangle records (mode 2 stages it in LDS): vertices, and per
-    // triangle 3 u16 indices (a, fl(a + edge_ab), fl(a + edge_ac))
-    const float4* __restrict__ tri_cverts;
-    const uint16_t* __restrict__ tri_cidx;
-    uint32_t tri_cvert_count;
     // textures (bindings 9, 11), RGBA8 sRGB, + decode table
     const uint32_t* __restrict__ textures;
     const uint32_t* __restrict__ env;
@@ -207,13 +182,6 @@ struct KernelArgs {
     // 128-B line; slots past the leaf's count are zero. Null: the leaf batches test per lane.
     const uint4* __restrict__ tri_leaftris;
     uint32_t lds_leafbatch_offset;  // per wave kLeafBatchWaveBytes of LDS for the cooperative leaf batch
-    // The 4-wide quantized accelerator (tri_q4.h): TriQ4Node[] as 4 uint4 each, its grid ({origin,
-    // valid}, {scale, 0}); null: the binary walk. Its walk's per-lane stacks in LDS at
-    // lds_q4stack_offset (kQ4StackEntries u32 per thread, entry e of thread t at [e * threads + t]).
-    const uint4* __restrict__ tri_q4;
-    const float4* __restrict__ tri_q4grid;
-    uint32_t lds_q4stack_offset;
-    uint32_t lds_q4packet_offset;  // rt_primary_kernel: per wave kQ4PacketStack x 3 u32 of packet stack (0: none)
     uint32_t compute_per_frame;
     uint32_t frames;          // frames rendered by this launch (rt_compute_frames), >= 1
     // Frame-parallel batch (frames > 1, accumulating): the queue holds one unit per
@@ -231,16 +199,20 @@ struct KernelArgs {
     // pixel), indexed like frame_light; the path kernel starts its paths from them. Null: off.
     uint4* __restrict__ primary;
     uint32_t primary_tile_major;  // the pre-pass takes its (frame, tile) units tile-major (1) or frame-major
-    // brute-force launches (rt_brute_kernel): bytes of sub-object records streamed through LDS
+    // brute-force launches (rt_brute_wf_kernel): the tile-streaming bytes of SURVEY §8d's
+    // convention (32 B x the sweep's sub-objects per 256-ray chunk of a bounce level), and the
+    // sub-object bytes the sweeps actually read from L2 (per LDS tile, or per wave when streamed)
     unsigned long long* __restrict__ stream_bytes;
+    unsigned long long* __restrict__ l2_stream_bytes;
     // the brute-force wavefront (rt_brute_wf_kernel): per owned pixel slot the path state (4
     // planes of float4: o + seed, d + bounce, light, contribution, plane stride = owned slots),
-    // two queues of live slots (ping-pong by bounce level), per pass kBruteLevels counters
-    // (entries of each level's queue); this launch's pass (frame * compute_per_frame + sample)
-    // and bounce level
+    // two queues of live slots (ping-pong by bounce level), per pass brute_levels counters
+    // (entries of each level's queue, bounces + 1 of them); this launch's pass (frame *
+    // compute_per_frame + sample) and bounce level
     float4* __restrict__ brute_paths;
     uint32_t* __restrict__ brute_queue;
     uint32_t* __restrict__ brute_counts;
+    uint32_t brute_levels;
     uint32_t brute_pass;
     uint32_t brute_level;
     uint32_t texture_width;
@@ -278,11 +250,6 @@ struct KernelArgs {
     uint32_t lds_tri_nodes_offset;
     uint32_t lds_tri_prims_offset;
     uint32_t lds_sub_offset;  // mode 2: sub-object records staged in LDS at this offset; 0: read from global
-    // mode 2: the triangles as a vertex table (float4 per vertex) and 3 u16 vertex indices per
-    // triangle, staged in LDS at these offsets when every record is reproduced bit for bit by
-    // SceneTriangle::new's arithmetic from its vertices (tri_compact_*; 0: the 64-B records)
-    uint32_t lds_cvert_offset;
-    uint32_t lds_cidx_offset;
-    uint32_t lds_stack_offset;    // kWide: the walk's per-lane stack, tri_stack_depth x threads u32
+    uint32_t lds_stack_offset;    // brute force: the sub-object tiles and hit lists after the scene image
     uint32_t lds_srgb_offset;
 };

@@ -29,9 +29,7 @@
 #include "rt_scene_math.h"
 #include "sphere_bvh.h"
 #include "tri_cone.h"
-#include "tri_q4.h"
 #include "tri_qnode.h"
-#include "tri_wide.h"
 
 #pragma clang fp contract(off)
 
@@ -189,159 +187,6 @@ extern "C" __global__ void __launch_bounds__(kRefitThreads) rt_refit_tri_bvh_ker
     if (threadIdx.x == 0) *extent_out = __uint_as_float(__float_as_uint(s_ext[0]) + 1u);  // nextafter up
 }
 
-// ---- the 4-wide accelerator (tri_wide.h) -----------------------------------
-//
-// rt_wide_vertices_kernel: compact leaves' vertex blocks from the current
-// triangles (vertex v = corner vsrc[v] & 3 of triangle vsrc[v] >> 2: a, fl(a + ab)
-// or fl(a + ac), as the host builder took them). rt_wide_leaves_kernel: each leaf
-// record's copy of its sub-object's bounds, and whether its compact block still
-// reproduces every triangle record bit for bit (SceneTriangle::new's arithmetic,
-// src/buffers.rs:66-95) -- a leaf that no longer does reads the records instead.
-// rt_refit_tri_wide_kernel: node boxes level by level, deepest first, and the
-// margin extent. Together: the wide accelerator after a triangle upload or a
-// device edit, exact without a host rebuild.
-
-__device__ __forceinline__ TriVertex hot_corner(const RtTriangleHot& t, uint32_t k) {
-    const float ax = t.p0.x, ay = t.p0.y, az = t.p0.z;
-    if (k == 1u) return TriVertex{ax + t.p0.w, ay + t.p1.x, az + t.p1.y};
-    if (k == 2u) return TriVertex{ax + t.p1.z, ay + t.p1.w, az + t.p2.x};
-    return TriVertex{ax, ay, az};
-}
-
-extern "C" __global__ void __launch_bounds__(256) rt_wide_vertices_kernel(const RtTriangleHot* __restrict__ tris,
-                                                                         uint32_t n_tri,
-                                                                         const uint32_t* __restrict__ vsrc,
-                                                                         uint32_t n_verts,
-                                                                         TriVertex* __restrict__ verts) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n_verts) return;
-    const uint32_t src = vsrc[v];
-    verts[v] = hot_corner(tris[min(src >> 2, n_tri - 1u)], src & 3u);
-}
-
-extern "C" __global__ void __launch_bounds__(256) rt_wide_leaves_kernel(TriLeaf* __restrict__ leaves, uint32_t n_leaves,
-                                                                       const RtSubObject* __restrict__ subs,
-                                                                       const RtTriangleHot* __restrict__ tris,
-                                                                       uint32_t n_tri,
-                                                                       const TriVertex* __restrict__ verts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_leaves) return;
-    TriLeaf L = leaves[i];
-    const RtSubObject sb = subs[L.sub];
-    for (int k = 0; k < 3; k++) {
-        L.mn[k] = sb.min_bounds[k];
-        L.mx[k] = sb.max_bounds[k];
-    }
-    if (L.count_flags & kWideLeafCompactBuilt) {
-        bool ok = true;
-        const uint32_t count = L.count_flags & 0xffu;
-        for (uint32_t j = 0; j < count && ok; j++) {
-            const uint32_t t = L.first_tri + j;
-            if (t >= n_tri) {
-                ok = false;
-                break;
-            }
-            const TriVertex a = verts[L.vbase + wide_leaf_index(L.idx, j, 0)];
-            const TriVertex b = verts[L.vbase + wide_leaf_index(L.idx, j, 1)];
-            const TriVertex c = verts[L.vbase + wide_leaf_index(L.idx, j, 2)];
-            float ab[3], ac[3], cn[3];
-            wide_tri_from_vertices(a, b, c, ab, ac, cn);
-            float ta[3], tab[3], tac[3], tcn[3], tfn[3];
-            unpack_triangle(tris[t], ta, tab, tac, tcn, tfn);
-            const float got[12] = {a.x, a.y, a.z, ab[0], ab[1], ab[2], ac[0], ac[1], ac[2], cn[0], cn[1], cn[2]};
-            const float want[12] = {ta[0], ta[1], ta[2], tab[0], tab[1], tab[2], tac[0], tac[1], tac[2],
-                                    tcn[0], tcn[1], tcn[2]};
-            for (int q = 0; q < 12; q++) ok = ok && __float_as_uint(got[q]) == __float_as_uint(want[q]);
-        }
-        L.count_flags = ok ? (L.count_flags | kWideLeafCompact) : (L.count_flags & ~kWideLeafCompact);
-    }
-    leaves[i] = L;
-}
-
-// the culling box of a leaf slot (tri_wide.cpp leaf_cull_box)
-__device__ __forceinline__ void leaf_cull_box_dev(const TriLeaf& L, float* lo, float* hi, bool& finite) {
-    finite = true;
-    for (int k = 0; k < 3; k++)
-        finite = finite && __builtin_isfinite(L.mn[k]) && __builtin_isfinite(L.mx[k]);
-    for (int k = 0; k < 3; k++) {
-        lo[k] = finite ? fminf(L.mn[k], L.mx[k]) : -3.0e38f;
-        hi[k] = finite ? fmaxf(L.mn[k], L.mx[k]) : 3.0e38f;
-    }
-}
-
-extern "C" __global__ void __launch_bounds__(kRefitThreads) rt_refit_tri_wide_kernel(
-    TriWideNode* __restrict__ nodes, const TriLeaf* __restrict__ leaves, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ level_offsets, uint32_t n_levels, float* __restrict__ extent_out) {
-    __shared__ float s_ext[kRefitThreads];
-    float ext = 0.0f;
-    for (uint32_t l = 0; l < n_levels; l++) {
-        for (uint32_t i = level_offsets[l] + threadIdx.x; i < level_offsets[l + 1]; i += kRefitThreads) {
-            const uint32_t n = order[i];
-            TriWideNode nd = nodes[n];
-            const uint32_t n_int = nd.slots & 0xfu, n_leaf = (nd.slots >> 4) & 0xfu;
-            for (uint32_t s = 0; s < n_int; s++) {  // union of the child's slot boxes (deeper: done)
-                const TriWideNode& c = nodes[nd.child_base + s];
-                const uint32_t cs = (c.slots & 0xfu) + ((c.slots >> 4) & 0xfu);
-                for (int k = 0; k < 3; k++) {
-                    float lo = c.lo[k][0], hi = c.hi[k][0];
-                    for (uint32_t q = 1; q < cs; q++) {
-                        lo = fminf(lo, c.lo[k][q]);
-                        hi = fmaxf(hi, c.hi[k][q]);
-                    }
-                    nd.lo[k][s] = lo;
-                    nd.hi[k][s] = hi;
-                }
-            }
-            for (uint32_t r = 0; r < n_leaf; r++) {
-                float lo[3], hi[3];
-                bool finite;
-                leaf_cull_box_dev(leaves[nd.leaf_base + r], lo, hi, finite);
-                for (int k = 0; k < 3; k++) {
-                    nd.lo[k][n_int + r] = lo[k];
-                    nd.hi[k][n_int + r] = hi[k];
-                    if (finite) ext = fmaxf(ext, fmaxf(fabsf(lo[k]), fabsf(hi[k])));
-                }
-            }
-            nodes[n] = nd;
-        }
-        __syncthreads();
-    }
-    s_ext[threadIdx.x] = ext;
-    __syncthreads();
-    for (uint32_t w = kRefitThreads / 2; w > 0; w /= 2) {
-        if (threadIdx.x < w) s_ext[threadIdx.x] = fmaxf(s_ext[threadIdx.x], s_ext[threadIdx.x + w]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *extent_out = __uint_as_float(__float_as_uint(s_ext[0]) + 1u);  // nextafter up
-}
-
-// After a triangle upload (boxes unchanged) or a device edit (refit too).
-hipError_t rt_launch_wide_refresh(TriWideNode* nodes, TriLeaf* leaves, uint32_t n_leaves, const TriVertex* verts_in,
-                                  TriVertex* verts, const uint32_t* vsrc, uint32_t n_verts, const RtSubObject* subs,
-                                  const RtTriangleHot* tris, uint32_t n_tri, const uint32_t* order,
-                                  const uint32_t* level_offsets, uint32_t n_levels, float* extent_out, bool refit,
-                                  hipStream_t stream) {
-    (void)verts_in;
-    if (n_verts) {
-        hipLaunchKernelGGL(rt_wide_vertices_kernel, dim3((n_verts + 255) / 256), dim3(256), 0, stream, tris, n_tri,
-                           vsrc, n_verts, verts);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    if (n_leaves) {
-        hipLaunchKernelGGL(rt_wide_leaves_kernel, dim3((n_leaves + 255) / 256), dim3(256), 0, stream, leaves, n_leaves,
-                           subs, tris, n_tri, verts);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    if (refit && n_levels) {
-        hipLaunchKernelGGL(rt_refit_tri_wide_kernel, dim3(1), dim3(kRefitThreads), 0, stream, nodes, leaves, order,
-                           level_offsets, n_levels, extent_out);
-        return hipGetLastError();
-    }
-    return hipSuccess;
-}
-
 hipError_t rt_launch_edit(const float* model, const uint32_t* tri_object, const uint32_t* sub_object,
                           const uint2* object_tris, const Placement* place, uint32_t object_count, uint32_t n_tri,
                           uint32_t n_sub, RtTriangleHot* tris, float4* bounds, RtSubObject* subs, RtObject* objects,
@@ -479,50 +324,5 @@ hipError_t rt_launch_tri_leaftris(const SubObjectPrim* prims, uint32_t n_prims, 
     const uint64_t n = (uint64_t)n_prims * kLeafTriWords;
     hipLaunchKernelGGL(rt_tri_leaftris_kernel, dim3((uint32_t)((n + 255u) / 256u)), dim3(256), 0, stream, prims,
                        n_prims, tris, n_tri, out);
-    return hipGetLastError();
-}
-
-// ---- the 4-wide quantized accelerator (tri_q4.h) --------------------------------------
-// Child boxes of every 4-wide node from the binary nodes they stand for (src[4 i + k]), on the
-// binary accelerator's quantization grid (tri_qgrid of its root): after every upload or refit,
-// so device-side edits keep the two trees the same. grid[0] = {origin.xyz, valid}, grid[1] =
-// {scale.xyz, 0}: with valid = 0 (a root box that is not finite) the walks use the binary tree.
-extern "C" __global__ void __launch_bounds__(256) rt_tri_q4_fill_kernel(const SphereBvhNode* __restrict__ bin,
-                                                                       uint32_t n_bin, const uint32_t* __restrict__ src,
-                                                                       uint32_t n_q4, TriQ4Node* __restrict__ q4,
-                                                                       float4* __restrict__ grid) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    TriQGrid g{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, false};
-    if (n_bin != 0) g = tri_qgrid(bin[0]);
-    if (i == 0) {
-        grid[0] = make_float4(g.origin[0], g.origin[1], g.origin[2], g.valid ? 1.f : 0.f);
-        grid[1] = make_float4(g.scale[0], g.scale[1], g.scale[2], 0.f);
-    }
-    if (i >= 4u * n_q4 || !g.valid) return;
-    TriQ4Node& nd = q4[i >> 2];
-    const uint32_t k = i & 3u;
-    const uint32_t sk = src[i];
-    uint32_t w[3];
-    if (sk == kQ4Empty) {
-        w[0] = 0u;
-        w[1] = 0xffff0000u;
-        w[2] = 0xffffffffu;
-    } else {
-        uint32_t qq[4];
-        tri_qnode(bin[sk], g, qq);
-        w[0] = qq[0];
-        w[1] = qq[1];
-        w[2] = qq[2];
-    }
-    nd.box[k][0] = w[0];
-    nd.box[k][1] = w[1];
-    nd.box[k][2] = w[2];
-}
-
-hipError_t rt_launch_tri_q4_fill(const SphereBvhNode* bin, uint32_t n_bin, const uint32_t* src, uint32_t n_q4,
-                                 TriQ4Node* q4, float4* grid, hipStream_t stream) {
-    const uint32_t n = 4u * n_q4;
-    hipLaunchKernelGGL(rt_tri_q4_fill_kernel, dim3(n ? (n + 255u) / 256u : 1u), dim3(256), 0, stream, bin, n_bin, src,
-                       n_q4, q4, grid);
     return hipGetLastError();
 }

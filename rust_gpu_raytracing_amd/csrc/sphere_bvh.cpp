@@ -375,69 +375,3 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
     out->r_min = (float)r_min;
     out->r_max = (float)r_max;
 }
-
-// ---- the 4-wide quantized triangle accelerator (tri_q4.h) --------------------------------
-#include "tri_q4.h"
-
-bool build_tri_q4(const std::vector<SphereBvhNode>& bin, std::vector<TriQ4Node>* nodes, std::vector<uint32_t>* src,
-                  uint32_t* depth) {
-    nodes->clear();
-    src->clear();
-    *depth = 0;
-    if (bin.empty()) return false;
-    auto is_leaf = [&](uint32_t b) { return bin[b].leaf != kSphereBvhInternal; };
-    for (const SphereBvhNode& nd : bin)
-        if (nd.leaf != kSphereBvhInternal && (nd.leaf & 0xffffffu) >= kQ4MaxPrims) return false;
-    auto area = [&](uint32_t b) {
-        const double dx = (double)bin[b].bmax[0] - bin[b].bmin[0], dy = (double)bin[b].bmax[1] - bin[b].bmin[1],
-                     dz = (double)bin[b].bmax[2] - bin[b].bmin[2];
-        return (dx >= 0.0 && dy >= 0.0 && dz >= 0.0) ? 2.0 * (dx * dy + dy * dz + dz * dx) : 0.0;
-    };
-    // the binary nodes under 4-wide node `b` (the binary node it expands)
-    auto children_of = [&](uint32_t b, uint32_t* kids) -> uint32_t {
-        if (is_leaf(b)) {  // a tree that is a single leaf
-            kids[0] = b;
-            return 1;
-        }
-        uint32_t n = 0;
-        kids[n++] = b + 1;
-        kids[n++] = bin[b + 1].skip;
-        while (n < 4) {
-            int best = -1;
-            double best_a = -1.0;
-            for (uint32_t i = 0; i < n; i++)
-                if (!is_leaf(kids[i]) && area(kids[i]) > best_a) {
-                    best_a = area(kids[i]);
-                    best = (int)i;
-                }
-            if (best < 0) break;
-            const uint32_t c = kids[best];
-            kids[best] = c + 1;
-            kids[n++] = bin[c + 1].skip;
-        }
-        return n;
-    };
-    std::vector<uint32_t> bin_of{0}, level{1};
-    nodes->emplace_back();
-    for (size_t w = 0; w < nodes->size(); w++) {  // breadth-first: a level's nodes are contiguous
-        uint32_t kids[4];
-        const uint32_t n = children_of(bin_of[w], kids);
-        TriQ4Node nd{};
-        for (uint32_t k = 0; k < 4; k++) {
-            nd.ref[k] = kQ4Empty;
-            src->push_back(k < n ? kids[k] : kQ4Empty);
-            if (k >= n) continue;
-            if (is_leaf(kids[k])) {
-                nd.ref[k] = kQ4Leaf | (bin[kids[k]].leaf & 0xffffffu);
-            } else {
-                nd.ref[k] = (uint32_t)bin_of.size();  // the index the child's node gets
-                bin_of.push_back(kids[k]);
-                level.push_back(level[w] + 1);
-            }
-        }
-        (*nodes)[w] = nd;
-        while (nodes->size() < bin_of.size()) nodes->emplace_back();
-        *depth = std::max(*depth, level[w]);
-    }
-    return true;
-}

@@ -44,6 +44,7 @@ class Renderer:
         camera_rays: np.ndarray | None = None,
         device_rays: bool | None = None,
         frame_batch: int | None = None,
+        tuning: dict[str, int] | None = None,
         lib=None,
     ):
         """``camera_rays``: explicit per-pixel directions (the reference's ray buffer;
@@ -54,7 +55,9 @@ class Renderer:
         ``frame_batch``: frames one launch may render (rt_set_frame_batch): with
         F > 1, ``compute_frame`` queues frames and launches F at a time (or at the
         next readback / update / sync), each frame's results written as before.
-        None keeps the library's default (RT_DEFAULT_FRAME_BATCH, include/rt_abi.h)."""
+        None keeps the library's default (RT_DEFAULT_FRAME_BATCH, include/rt_abi.h).
+        ``tuning``: exact variants of the schedule and acceleration structures for A/B
+        runs, {key: value} passed to rt_set_tuning (include/rt_abi.h lists the keys)."""
         self._lib = N.load_library() if lib is None else lib
         self.scene = scene
         self.accumulate = accumulate
@@ -89,6 +92,8 @@ class Renderer:
             self._set_camera_matrices(scene.camera)
         if frame_batch is not None:
             self.set_frame_batch(frame_batch)
+        for key, value in (tuning or {}).items():
+            self.set_tuning(key, value)
 
     # ------------------------------------------------------------------ helpers
     def _params(self, accumulation_index: int) -> np.ndarray:
@@ -322,8 +327,19 @@ class Renderer:
         on incoherent meshes, not exact)."""
         self._call("rt_set_triangle_pruning", int(mode))
 
+    def set_tuning(self, key: str, value: int) -> None:
+        """An exact variant of the schedule or of an acceleration structure (rt_set_tuning)."""
+        self._call("rt_set_tuning", key.encode(), int(value))
+
+    def streamed_bytes_l2(self) -> int:
+        """Sub-object bytes the brute-force sweeps read from L2 (rt_streamed_bytes_l2)."""
+        v = ctypes.c_uint64()
+        self._call("rt_streamed_bytes_l2", ctypes.byref(v))
+        return v.value
+
     def streamed_bytes(self) -> int:
-        """Sub-object bytes the brute-force launches streamed through LDS."""
+        """The brute-force launches' tile-streaming bytes by SURVEY §8d's convention
+        (32 B x the swept sub-objects per started 256 rays of a bounce level)."""
         v = ctypes.c_uint64()
         self._call("rt_streamed_bytes", ctypes.byref(v))
         return v.value
@@ -399,10 +415,12 @@ class Renderer:
         return dict(zip(("threads", "blocks", "lds_bytes", "scene_in_lds"), (x.value for x in v)))
 
     def last_launch_passes(self) -> list:
-        """Kernels the last launch ran: "path", "primary" (pre-pass), "resolve", "brute"."""
+        """Kernels the last launch ran: "path", "primary" (pre-pass), "resolve", "brute",
+        "brute_stream" (the brute-force sweep's scalar-cache variant)."""
         v = ctypes.c_uint32()
         N.check(self._ctx, self._lib.rt_last_launch_passes(self._ctx, ctypes.byref(v)), self._lib)
-        names = ((1, "path"), (2, "primary"), (4, "resolve"), (8, "brute"))
+        names = ((N.RT_PASS_PATH, "path"), (N.RT_PASS_PRIMARY, "primary"), (N.RT_PASS_RESOLVE, "resolve"),
+                 (N.RT_PASS_BRUTE, "brute"), (N.RT_PASS_BRUTE_STREAM, "brute_stream"))
         return [n for bit, n in names if v.value & bit]
 
     @property

@@ -2,12 +2,10 @@
 // kernel's BVH traversal logic (same f32 operation order, -ffp-contract=off)
 // must return exactly the triangle, object and distance of the reference's
 // sequential sweep (check_triangles, compute_shader.wgsl:422-517).
-// The 4-wide accelerator (tri_wide.h: 4-slot nodes, stack walk, compact vertex-
-// block leaves) and the binary walk over the 16-B quantized nodes (tri_qnode.h) are
-// checked the same way, ray by ray; every quantized box must contain its node's box.
+// The binary walk over the 16-B quantized nodes (tri_qnode.h) is checked the same way, ray
+// by ray; every quantized box must contain its node's box.
 // usage: tri_exactness <objects.bin> <subs.bin> <tris.bin> <rays.f32> [margin_scale]
 //   -> "ok <rays> <hits> <avg_tri_tests> <avg_nodes> <nan_fallbacks>"
-//      "wide <avg_tri_tests> <avg_node_loads> <compact_leaves> <leaves> <depth> <max_stack>"
 //      "qnodes <valid> <avg_nodes>"
 //   or the first mismatch
 #include <cmath>
@@ -21,9 +19,7 @@
 #include "rt_bvh_slab.h"
 #include "sphere_bvh.h"
 #include "tri_cone.h"
-#include "tri_q4.h"
 #include "tri_qnode.h"
-#include "tri_wide.h"
 
 static const float F32_MAX_ = 3.4028235e+38f;
 struct V { float x, y, z; };
@@ -292,279 +288,6 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     return r;
 }
 
-// ---- the 4-wide quantized walk (tri_q4.h; pathtrace.hip q4_node_step) ----
-// Children tested four at a time, visited nearest entry first; the rest wait on a per-lane stack
-// of kQ4StackEntries (a leaf entry carries its box's certified gap, coded in 11 bits); a push
-// beyond it restarts the ray on the binary walk. Leaves are tested as the kernel's cooperative
-// batch merges them (tested here when popped or reached: the order the kernel's batches follow).
-static long q4_rays = 0, q4_fetch = 0, q4_overflow = 0, q4_leaves = 0, q4_cert_checked = 0, q4_cert_skipped = 0,
-            q4_tests = 0;
-static uint32_t q4_max_sp = 0;
-
-static Res q4_walk(const TriangleAccel& A, const std::vector<TriQ4Node>& Q, const TriQGrid& g,
-                   const std::vector<TriLeafCert>& lcert, const std::vector<rt_object_info>& ob,
-                   const std::vector<rt_sub_object_info>& sb, const std::vector<rt_scene_triangle>& tr, V o, V d,
-                   float scale, bool* overflowed) {
-    q4_rays++;
-    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    const float m = scale * (std::sqrt(dot(o, o)) + A.extent) + 1.0e-30f;
-    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
-    const TriConeRay tcr = tri_cone_ray(o.x, o.y, o.z, d.x, d.y, d.z);
-    float best = F32_MAX_;
-    uint32_t best_seq = 0;
-    Res r{F32_MAX_, -1, -1, 0};
-    bool nan_hit = false;
-    *overflowed = false;
-    auto leaf = [&](uint32_t prim, uint32_t gap_code) {
-        q4_leaves++;
-        if (gap_code != 0u && best != F32_MAX_) {  // the deferred certificate test (tri_leafcert_skips_gap)
-            q4_cert_checked++;
-            if (tri_leafcert_skips_gap(lcert[prim].w, tcr, best, q4_gap_decode(gap_code)) == kLeafCertAll) {
-                q4_cert_skipped++;
-                return;
-            }
-        }
-        const SubObjectPrim& p = A.prims[prim];
-        const rt_object_info& OB = ob[p.object];
-        const rt_sub_object_info& s = sb[p.sub];
-        if (!rib(o, inv, OB.min_bounds, OB.max_bounds)) return;
-        if (p.range == kPrimRangeNone || (p.range >> 27) >= 8u) {
-            // tri_leaf's sequential loop (the kernel's per-lane test of such leaves): the sub-object
-            // box tested up front when the range is not in the record, else at the first candidate
-            const bool lazy = p.range != kPrimRangeNone;
-            if (!lazy && !rib(o, inv, s.min_bounds, s.max_bounds)) return;
-            int sub_state = lazy ? 0 : 1;
-            const uint32_t f0 = lazy ? (p.range & ((1u << 27) - 1u)) : s.first_triangle_index;
-            const uint32_t c0 = lazy ? (p.range >> 27) : s.triangle_count;
-            for (uint32_t j = 0; j < c0; j++) {
-                q4_tests++;
-                const uint32_t ti = std::min<uint32_t>(f0 + j, (uint32_t)tr.size() - 1u), seq = p.seq_base + j;
-                const rt_scene_triangle& t = tr[ti];
-                V cn = ld(t.calc_normal);
-                float det = -dot(d, cn), inv_det = 1.0f / det;
-                V ao = sub(o, ld(t.a));
-                float dist = dot(ao, cn) * inv_det;
-                bool nan_dist = dist != dist;
-                if (dist < 0.0f) continue;
-                if (!nan_dist && !(dist < best || (dist == best && seq < best_seq))) continue;
-                V dao = cross(ao, d);
-                float v = -dot(ld(t.edge_ab), dao) * inv_det;
-                if (v < 0.0f) continue;
-                float u = dot(ld(t.edge_ac), dao) * inv_det;
-                if (u < 0.0f) continue;
-                float w = 1.0f - u - v;
-                if (w < 0.0f) continue;
-                if (sub_state == 0) {
-                    if (!rib(o, inv, s.min_bounds, s.max_bounds)) return;
-                    sub_state = 1;
-                }
-                if (nan_dist) { nan_hit = true; continue; }
-                best = dist;
-                best_seq = seq;
-                r = {dist, (int)ti, (int)p.object, det > 0.0f};
-            }
-            return;
-        }
-        const uint32_t first = p.range & ((1u << 27) - 1u), count = p.range >> 27;  // coop_leaf_batch's merge
-        float cd = INFINITY;
-        uint32_t cs = 0xffffffffu;
-        int cti = -1, cfront = 0;
-        bool cnan = false;
-        for (uint32_t j = 0; j < count; j++) {
-            q4_tests++;
-            const rt_scene_triangle& t = tr[std::min<uint32_t>(first + j, (uint32_t)tr.size() - 1u)];
-            V cn = ld(t.calc_normal);
-            float det = -dot(d, cn), inv_det = 1.0f / det;
-            V ao = sub(o, ld(t.a));
-            float dist = dot(ao, cn) * inv_det;
-            V dao = cross(ao, d);
-            float v = -dot(ld(t.edge_ab), dao) * inv_det;
-            float u = dot(ld(t.edge_ac), dao) * inv_det;
-            float w = 1.0f - u - v;
-            if (dist < 0.0f || v < 0.0f || u < 0.0f || w < 0.0f) continue;
-            if (dist != dist) { cnan = true; continue; }
-            const uint32_t seq = p.seq_base + j;
-            if (dist < cd || (dist == cd && seq < cs)) {
-                cd = dist;
-                cs = seq;
-                cti = (int)std::min<uint32_t>(first + j, (uint32_t)tr.size() - 1u);
-                cfront = det > 0.0f;
-            }
-        }
-        const bool beats = cd < best || (cd == best && cs < best_seq);
-        if ((cnan || beats) && rib(o, inv, s.min_bounds, s.max_bounds)) {
-            if (cnan) nan_hit = true;
-            if (beats) {
-                best = cd;
-                best_seq = cs;
-                r = {cd, cti, (int)p.object, cfront};
-            }
-        }
-    };
-    uint32_t stk[kQ4StackEntries];
-    uint32_t sp = 0, node = 0;
-    while (true) {
-        if (node == kQ4None) {
-            if (sp == 0) break;
-            const uint32_t e = stk[--sp];
-            if (e & kQ4Leaf) {
-                leaf(e & 0xfffffu, (e >> 20) & 0x7ffu);
-                continue;
-            }
-            node = e;
-        }
-        q4_fetch++;
-        const TriQ4Node& nd = Q[node];
-        float key[4];
-        uint32_t ent[4];
-        for (uint32_t k = 0; k < 4; k++) {
-            key[k] = INFINITY;
-            ent[k] = 0u;
-            if (nd.ref[k] == kQ4Empty) continue;
-            const uint32_t q[4] = {nd.box[k][0], nd.box[k][1], nd.box[k][2], 0u};
-            float lo[3], hi[3];
-            tri_qnode_box(q, g, lo, hi);
-            float nt, ft;
-            slab_hit(sr, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], nt, ft);
-            if (!(nt <= ft && ft >= 0.0f)) continue;
-            key[k] = nt;
-            ent[k] = nd.ref[k];
-            if ((nd.ref[k] & kQ4Leaf) && best != F32_MAX_ && nt > best) {  // node_step's gap, as a code
-                const float t1x = fminf(fmaf(lo[0], sr.ix, sr.lx), fmaf(hi[0], sr.ix, sr.hx));
-                const float t1y = fminf(fmaf(lo[1], sr.iy, sr.ly), fmaf(hi[1], sr.iy, sr.hy));
-                const float t1z = fminf(fmaf(lo[2], sr.iz, sr.lz), fmaf(hi[2], sr.iz, sr.hz));
-                const float tbs = best * (1.0f + 0x1p-20f);
-                const float gap = fmaxf(fmaxf((t1x - tbs) * fabsf(d.x), (t1y - tbs) * fabsf(d.y)), (t1z - tbs) * fabsf(d.z)) *
-                                  (1.0f - 0x1p-20f);
-                ent[k] = (nd.ref[k] & ~(0x7ffu << 20)) | (q4_gap_code(gap) << 20);
-            }
-        }
-        // nearest first: a sorting network on (entry distance, slot); misses (inf) last
-        uint32_t ord[4] = {0, 1, 2, 3};
-        auto cx = [&](int i, int j) {
-            if (key[ord[j]] < key[ord[i]]) std::swap(ord[i], ord[j]);
-        };
-        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-        int n_hit = 0;
-        for (int k = 0; k < 4; k++) n_hit += key[ord[k]] != INFINITY;
-        node = kQ4None;
-        if (n_hit == 0) continue;
-        for (int k = n_hit - 1; k >= 1; k--) {  // the others, farthest first
-            if (sp == kQ4StackEntries) {  // the kernel restarts the ray on the binary walk
-                *overflowed = true;
-                q4_overflow++;
-                return r;
-            }
-            stk[sp++] = ent[ord[k]];
-            q4_max_sp = std::max(q4_max_sp, sp);
-        }
-        const uint32_t e0 = ent[ord[0]];
-        if (e0 & kQ4Leaf)
-            leaf(e0 & 0xfffffu, (e0 >> 20) & 0x7ffu);
-        else
-            node = e0;
-    }
-    if (nan_hit) return {F32_MAX_, -2, -2, 0};  // the kernel reruns the sweep
-    return r;
-}
-
-static long w_tests = 0, w_nodes = 0;
-static uint32_t w_max_stack = 0;
-
-// The kernel's wide walk (pathtrace.hip: wide_node_step / tri_leaf_wide), leaves
-// tested as soon as they are reached (the kernel's batching only reorders leaf
-// tests, which the lexicographic minimum does not see).
-static Res wide(const TriWide& W, const std::vector<rt_object_info>& ob, const std::vector<rt_scene_triangle>& tr, V o,
-                V d, float scale) {
-    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    float m = scale * (std::sqrt(dot(o, o)) + W.extent) + 1.0e-30f;
-    float best = F32_MAX_;
-    uint32_t best_seq = 0;
-    Res r{F32_MAX_, -1, -1, 0};
-    bool nan_hit = false;
-    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
-    if (W.nodes.empty()) return r;
-    std::vector<uint32_t> stack;
-    uint32_t node = 0;
-    while (true) {
-        if (node == 0xffffffffu) {
-            if (stack.empty()) break;
-            uint32_t& e = stack.back();
-            node = (e >> 4) + (uint32_t)__builtin_ctz(e & 0xfu);
-            e &= e - 1u;
-            if ((e & 0xfu) == 0u) stack.pop_back();
-        }
-        w_nodes++;
-        const TriWideNode& nd = W.nodes[node];
-        const uint32_t n_int = nd.slots & 0xfu, n_slots = n_int + ((nd.slots >> 4) & 0xfu);
-        uint32_t hit = 0;
-        for (uint32_t k = 0; k < 4; k++) {
-            float nt, ft;
-            slab_hit(sr, nd.lo[0][k], nd.lo[1][k], nd.lo[2][k], nd.hi[0][k], nd.hi[1][k], nd.hi[2][k], nt, ft);
-            if (nt <= ft && ft >= 0.0f) hit |= 1u << k;
-        }
-        hit &= (1u << n_slots) - 1u;
-        const uint32_t hl = hit >> n_int, hi = hit & ((1u << n_int) - 1u);
-        for (uint32_t q = 0; q < 4; q++) {
-            if (!((hl >> q) & 1u)) continue;
-            const TriLeaf& L = W.leaves[nd.leaf_base + q];
-            const rt_object_info& OB = ob[L.object];
-            if (!rib(o, inv, OB.min_bounds, OB.max_bounds) || !rib(o, inv, L.mn, L.mx)) continue;
-            const uint32_t count = L.count_flags & 0xffu;
-            const bool compact = (L.count_flags & kWideLeafCompact) != 0u;
-            for (uint32_t j = 0; j < count; j++) {
-                w_tests++;
-                const uint32_t ti = L.first_tri + j, seq = L.seq_base + j;
-                V a, eab, eac, cn;
-                if (compact) {
-                    const TriVertex& va = W.verts[L.vbase + wide_leaf_index(L.idx, j, 0)];
-                    const TriVertex& vb = W.verts[L.vbase + wide_leaf_index(L.idx, j, 1)];
-                    const TriVertex& vc = W.verts[L.vbase + wide_leaf_index(L.idx, j, 2)];
-                    float ab3[3], ac3[3], cn3[3];
-                    wide_tri_from_vertices(va, vb, vc, ab3, ac3, cn3);
-                    a = {va.x, va.y, va.z};
-                    eab = ld(ab3);
-                    eac = ld(ac3);
-                    cn = ld(cn3);
-                } else {
-                    const rt_scene_triangle& t = tr[ti];
-                    a = ld(t.a);
-                    eab = ld(t.edge_ab);
-                    eac = ld(t.edge_ac);
-                    cn = ld(t.calc_normal);
-                }
-                float det = -dot(d, cn), inv_det = 1.0f / det;
-                V ao = sub(o, a);
-                float dist = dot(ao, cn) * inv_det;
-                bool nan_dist = dist != dist;
-                if (dist < 0.0f) continue;
-                if (!nan_dist && !(dist < best || (dist == best && seq < best_seq))) continue;
-                V dao = cross(ao, d);
-                float v = -dot(eab, dao) * inv_det;
-                if (v < 0.0f) continue;
-                float u = dot(eac, dao) * inv_det;
-                if (u < 0.0f) continue;
-                float w = 1.0f - u - v;
-                if (w < 0.0f) continue;
-                if (nan_dist) { nan_hit = true; continue; }
-                best = dist;
-                best_seq = seq;
-                r = {dist, (int)ti, (int)L.object, det > 0.0f};
-            }
-        }
-        if (hi != 0u) {
-            const uint32_t rest = hi & (hi - 1u);
-            if (rest) stack.push_back((nd.child_base << 4) | rest);
-            node = nd.child_base + (uint32_t)__builtin_ctz(hi);
-        } else {
-            node = 0xffffffffu;
-        }
-        w_max_stack = std::max<uint32_t>(w_max_stack, (uint32_t)stack.size());
-    }
-    if (nan_hit) return {F32_MAX_, -2, -2, 0};  // the kernel reruns the sweep: checked by the caller
-    return r;
-}
-
 int main(int argc, char** argv) {
     if (argc < 5) return 2;
     auto ob = load<rt_object_info>(argv[1]);
@@ -576,18 +299,6 @@ int main(int argc, char** argv) {
     if (getenv("TRI_SUBTREE_MAX")) g_subtree_max = (uint32_t)atoi(getenv("TRI_SUBTREE_MAX"));
     TriangleAccel A;
     build_triangle_accel(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), &A);
-    // the wide accelerator, with compact leaves from the records in the kernel's 64-B layout
-    std::vector<float> hot(16 * tr.size());
-    for (size_t i = 0; i < tr.size(); i++) {
-        const rt_scene_triangle& t = tr[i];
-        const float f[16] = {t.a[0], t.a[1], t.a[2], t.edge_ab[0], t.edge_ab[1], t.edge_ab[2], t.edge_ac[0], t.edge_ac[1],
-                             t.edge_ac[2], t.calc_normal[0], t.calc_normal[1], t.calc_normal[2], t.face_normal[0],
-                             t.face_normal[1], t.face_normal[2], 0.0f};
-        memcpy(&hot[16 * i], f, sizeof(f));
-    }
-    TriWide W;
-    build_triangle_wide(ob.data(), (uint32_t)ob.size(), sb.data(), (uint32_t)sb.size(), hot.data(), (uint32_t)tr.size(),
-                        &W);
     // the quantized copy, as rt_quantize_tri_nodes_kernel makes it; each box must contain its node's
     std::vector<uint32_t> qn(4 * A.nodes.size());
     g_grid = A.nodes.empty() ? TriQGrid{} : tri_qgrid(A.nodes[0]);
@@ -626,26 +337,6 @@ int main(int argc, char** argv) {
         lcert[pi] = tricone::leafcert_build(cnt, ta, tab, tac, tcn, lo, hi);
         lcert_valid += lcert[pi].w[7] != kLeafCertNone;
     }
-    // the 4-wide quantized accelerator over the same tree (boxes as rt_tri_q4_fill_kernel fills them)
-    std::vector<TriQ4Node> q4;
-    std::vector<uint32_t> q4src;
-    uint32_t q4depth = 0;
-    const bool q4ok = g_grid.valid && build_tri_q4(A.nodes, &q4, &q4src, &q4depth);
-    if (q4ok)
-        for (size_t i = 0; i < q4.size(); i++)
-            for (uint32_t k = 0; k < 4; k++) {
-                tri_q4_fill_child(q4[i], k, A.nodes.data(), q4src[4 * i + k], g_grid);
-                if (q4src[4 * i + k] == kQ4Empty) continue;
-                const uint32_t qw[4] = {q4[i].box[k][0], q4[i].box[k][1], q4[i].box[k][2], 0u};
-                float lo[3], hi[3];
-                tri_qnode_box(qw, g_grid, lo, hi);
-                const SphereBvhNode& bn = A.nodes[q4src[4 * i + k]];
-                for (int a = 0; a < 3; a++)
-                    if (!(lo[a] <= bn.bmin[a] && hi[a] >= bn.bmax[a])) {
-                        printf("Q4 BOX node %zu child %u axis %d does not contain its binary node\n", i, k, a);
-                        return 1;
-                    }
-            }
     std::vector<SphereBvhNode> oct;
     std::vector<uint32_t> qoct;
     order_bvh_by_octant(A.nodes, &oct, false, nullptr);
@@ -668,8 +359,6 @@ int main(int argc, char** argv) {
     for (long i = 0; i < n; i++) {
         V o = ld(&rays[6 * i]), d = ld(&rays[6 * i + 3]);
         Res a = sweep(ob, sb, tr, o, d), b = accel(A, ob, sb, tr, o, d, scale);
-        Res c = wide(W, ob, tr, o, d, scale);
-        if (c.tri == -2) c = sweep(ob, sb, tr, o, d);  // NaN distance met: the kernel's sweep fallback
         Res e = b;
         if (g_grid.valid) {
             g_q = &qn;
@@ -701,24 +390,15 @@ int main(int argc, char** argv) {
         Res y = accel(A, ob, sb, tr, o, d, scale);
         g_exact_nodes = saved_nodes;
         g_exact_tests = saved_tests;
-        // the 4-wide walk (its overflow restarts on the binary walk above: y)
-        Res z = y;
-        if (q4ok) {
-            bool ovf = false;
-            z = q4_walk(A, q4, g_grid, lcert, ob, sb, tr, o, d, scale, &ovf);
-            if (ovf) z = y;
-            if (z.tri == -2) z = sweep(ob, sb, tr, o, d);
-        }
         g_kernel_default = false;
         g_lcert = nullptr;
         g_oct = nullptr;
         g_qoct = nullptr;
         g_q = nullptr;
         g_lazy = false;
-        const Res* const walks[] = {&b, &c, &e, &f, &h, &x, &y, &z};
-        const char* const names[] = {"binary", "wide", "qnodes", "qnodes+lazy", "octants+prune", "certified",
-                                     "kernel-default", "q4"};
-        for (int wi = 0; wi < 8; wi++) {
+        const Res* const walks[] = {&b, &e, &f, &h, &x, &y};
+        const char* const names[] = {"binary", "qnodes", "qnodes+lazy", "octants+prune", "certified", "kernel-default"};
+        for (int wi = 0; wi < 6; wi++) {
             const Res* w = walks[wi];
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
@@ -731,11 +411,7 @@ int main(int argc, char** argv) {
         }
         hits += a.tri >= 0;
     }
-    long compact = 0;
-    for (const TriLeaf& L : W.leaves) compact += (L.count_flags & kWideLeafCompact) ? 1 : 0;
     printf("ok %ld %ld %.2f %.2f %ld\n", n, hits, (double)g_tests / n, (double)g_nodes / n, g_nan);
-    printf("wide %.2f %.2f %ld %zu %u %u\n", (double)w_tests / n, (double)w_nodes / n, compact, W.leaves.size(), W.depth,
-           w_max_stack);
     printf("qnodes %d %.2f\n", g_grid.valid ? 1 : 0, (double)g_qnodes / n);
     printf("prune %.2f %.2f\n", (double)g_prune_nodes / n, (double)g_prune_tests / n);
     printf("certified %.2f %.2f %.2f %.2f %.2f %ld %zu\n", (double)g_exact_nodes / n, (double)g_exact_tests / n,
@@ -743,11 +419,6 @@ int main(int argc, char** argv) {
            lcert.size());
     printf("heuristic_misses %ld\n", g_heur_miss);
     printf("kernel_default %ld %ld %ld %ld\n", g_gap_checked, g_gap_skipped, g_coop_leaves, g_coop_nan);
-    // q4 <valid> <fetches/ray> <leaves reached/ray> <cert checks/ray> <cert skips/ray> <tri tests/ray>
-    //    <overflowed rays> <max stack> <depth> <nodes>
-    printf("q4 %d %.2f %.2f %.2f %.2f %.2f %ld %u %u %zu\n", q4ok ? 1 : 0, (double)q4_fetch / n, (double)q4_leaves / n,
-           (double)q4_cert_checked / n, (double)q4_cert_skipped / n, (double)q4_tests / n, q4_overflow, q4_max_sp,
-           q4depth, q4.size());
     if (!g_depth.empty()) {  // depth, visits per ray at that depth, nodes of one layout at that depth
         std::vector<long> per(64, 0);
         for (size_t i = 0; i < A.nodes.size(); i++) per[std::min<int>(g_depth[i], 63)]++;

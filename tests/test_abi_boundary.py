@@ -41,7 +41,29 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version(native_lib):
-    assert native_lib.rt_abi_version() == 11
+    assert native_lib.rt_abi_version() == 12
+
+
+def test_library_reads_no_environment():
+    """The product library takes no input from the process environment (ABI 12: the round-1..5
+    RT_* A/B switches became rt_set_tuning keys, the inexact pruning mode only
+    rt_set_triangle_pruning(ctx, 2)): it imports neither getenv nor secure_getenv, so no
+    environment can change what it renders (tests/test_gpu_parity.py checks the same on the GPU)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", str(N.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", out), out
+
+
+def test_tuning_keys_documented():
+    """Every rt_set_tuning key the library accepts is listed in include/rt_abi.h."""
+    src = (ROOT / "rust_gpu_raytracing_amd" / "csrc" / "rt_abi.cpp").read_text()
+    body = src[src.index("int rt_set_tuning("):]
+    body = body[:body.index("\n}\n")]
+    keys = set(re.findall(r'k == "(\w+)"', body))
+    assert len(keys) >= 25
+    header = HEADER.read_text()
+    doc = header[header.index("Exact variants of the launch schedule"):header.index("RT_API int rt_set_tuning")]
+    assert keys == set(re.findall(r'"(\w+)"', doc)), keys ^ set(re.findall(r'"(\w+)"', doc))
 
 
 def test_library_built_from_these_sources(native_lib):
@@ -171,3 +193,5 @@ def test_header_constants_match_binding():
     text = HEADER.read_text()
     assert re.search(r"#define RT_DEFAULT_FRAME_BATCH (\d+)", text).group(1) == str(N.RT_DEFAULT_FRAME_BATCH)
     assert re.search(r"#define RT_GROUP_COPY_TRANSPORT (\d+)u", text).group(1) == str(N.RT_GROUP_COPY_TRANSPORT)
+    for name in ("PATH", "PRIMARY", "RESOLVE", "BRUTE", "BRUTE_STREAM"):
+        assert re.search(rf"#define RT_PASS_{name} (\d+)u", text).group(1) == str(getattr(N, f"RT_PASS_{name}"))

@@ -30,8 +30,10 @@ def assert_same(acc_g, out_g, rays_g, acc_o, out_o, rays_o):
     assert np.array_equal(acc_g.view(np.uint32), acc_o.view(np.uint32))
 
 
-def gpu_render(scene, bounces, frames, *, spp=1, accumulate=1, rays=None, **kw):
+def gpu_render(scene, bounces, frames, *, spp=1, accumulate=1, rays=None, prune=None, **kw):
     with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp, camera_rays=rays, **kw) as r:
+        if prune is not None:
+            r.set_triangle_pruning(prune)
         for _ in range(frames):
             r.compute_frame(bounces)
         return r.read_accumulation(), r.read_output(), r.ray_count()
@@ -163,7 +165,12 @@ def test_gpu_full_size_brute_force_c5(gpu, oracle_lib, mode):
         for _ in range(2):
             r.compute_frame(bounces)
         acc, out, n = r.read_accumulation(), r.read_output(), r.ray_count()
-        assert r.streamed_bytes() > 0
+        # SURVEY §8d's tile-streaming term: 32 B x 142,858 sub-objects per started 256 rays of
+        # each bounce level -- at least the first level's whole frame of rays, per frame
+        n_sub = sum(len(o.sub_object_info) for o in scene.objects)
+        assert r.streamed_bytes() >= 2 * -(-1920 * 1080 // 256) * 32 * n_sub
+        assert r.streamed_bytes() % (32 * n_sub) == 0
+        assert r.streamed_bytes_l2() > 0
         assert "brute" in r.last_launch_passes()
     _check_c5_sample(smp, acc, out)
     acc_d, out_d, n_d = gpu_render(scene, bounces, 2, rays=rays)
@@ -371,18 +378,17 @@ def test_gpu_unpack_all_ranks_one_launch(gpu, accumulate, world, dst):
     ("c2_rtiow", 1, 1, 20, "1", {}),  # the bench's launch at its default 20 steps
     ("c3_chess", 1, 1, 64, "1", dict(env_size=(512, 256))),  # the largest batch
 ])
-def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, batch, parallel, kw):
+def test_gpu_frame_batch(gpu, oracle_lib, config, spp, accumulate, batch, parallel, kw):
     """rt_set_frame_batch: queued frames launched F at a time give, after every
     observable point, exactly the single-frame sequence (the oracle's): a readback
     in the middle of a batch, a bounce change, and a tail shorter than F (frames queued
     one call at a time and through rt_submit_frames). Both batch
     kernels: frame-parallel (a queue unit per (frame, tile), lights resolved in order,
-    the default) and RT_FRAME_PARALLEL=0 (each pixel's frames back to back on a lane)."""
-    monkeypatch.setenv("RT_FRAME_PARALLEL", parallel)
+    the default) and tuning "frame_parallel" 0 (each pixel's frames back to back on a lane)."""
     scene, bounces = build_config(config, width=96, height=56, **kw)
     rays = scene.camera.recalculate_ray_directions()
     with Renderer(scene, accumulate=bool(accumulate), compute_per_frame=spp, camera_rays=rays,
-                  frame_batch=batch) as r:
+                  frame_batch=batch, tuning={"frame_parallel": int(parallel)}) as r:
         assert r.frame_batch() == (batch, 0)
         for f in range(batch - 1):
             r.compute_frame(bounces)
@@ -408,15 +414,15 @@ def test_gpu_frame_batch(gpu, oracle_lib, monkeypatch, config, spp, accumulate, 
 
 
 @pytest.mark.parametrize("stage", ["0", "1"])
-def test_gpu_sub_objects_in_lds(gpu, oracle_lib, monkeypatch, stage):
-    """Mode 2 stages the leaves' sub-object records in LDS when they fit (RT_STAGE_SUBS);
+def test_gpu_sub_objects_in_lds(gpu, oracle_lib, stage):
+    """Mode 2 stages the leaves' sub-object records in LDS when they fit (tuning "stage_subs");
     both ways, and through the in-plane sweep fallback that reads them too, the result is
     the oracle's."""
-    monkeypatch.setenv("RT_STAGE_SUBS", stage)
+    tuning = {"stage_subs": int(stage)}
     scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
     rays = scene.camera.recalculate_ray_directions()
-    acc, out, n = gpu_render(scene, bounces, 3, rays=rays)
-    with Renderer(scene, camera_rays=rays) as r:
+    acc, out, n = gpu_render(scene, bounces, 3, rays=rays, tuning=tuning)
+    with Renderer(scene, camera_rays=rays, tuning=tuning) as r:
         r.compute_frame(bounces)
         assert r.launch_config()["scene_in_lds"] == 2
     o = oracle_lib.Oracle(scene, camera_rays=rays)
@@ -482,19 +488,28 @@ def test_gpu_last_launch_passes(gpu):
         r.compute_frame(bounces)
         r.synchronize()
         assert r.last_launch_passes() == ["brute"]
+        r.set_brute_force(2)
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["brute", "brute_stream"]
+    scene, bounces = build_config("c2_rtiow", width=64, height=48)
+    with Renderer(scene) as r:  # no triangles: mode 2 has no records to stream and runs mode 1's sweep
+        r.set_brute_force(2)
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["brute"]
 
 
 @pytest.mark.parametrize("qnodes,primary", [("1", "0"), ("0", "0"), ("1", "1")])
-def test_gpu_quantized_triangle_nodes(gpu, oracle_lib, monkeypatch, qnodes, primary):
+def test_gpu_quantized_triangle_nodes(gpu, oracle_lib, qnodes, primary):
     """Walks of the binary triangle accelerator from global memory read its 16-B quantized
     copy (tri_qnode.h: boxes rounded outward onto an exact f32 grid). Per-lane walk, and the
     primary pre-pass beside it: the oracle's result either way."""
-    monkeypatch.setenv("RT_TRI_QNODES", qnodes)
-    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
+    tuning = {"tri_qnodes": int(qnodes), "primary_pass": int(primary)}
     scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
     rays = scene.camera.recalculate_ray_directions()
-    acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
-    with Renderer(scene, camera_rays=rays) as r:
+    acc, out, n = gpu_render(scene, bounces, 2, rays=rays, tuning=tuning)
+    with Renderer(scene, camera_rays=rays, tuning=tuning) as r:
         r.compute_frame(bounces)
         assert r.launch_config()["scene_in_lds"] <= 1  # the accelerator in global memory
     o = oracle_lib.Oracle(scene, camera_rays=rays)
@@ -506,21 +521,61 @@ def test_gpu_quantized_triangle_nodes(gpu, oracle_lib, monkeypatch, qnodes, prim
 
 @pytest.mark.parametrize("prune,octants,primary", [("1", "1", "0"), ("1", "0", "0"), ("1", "1", "1"),
                                                    ("0", "1", "0"), ("2", "1", "0"), ("2", "1", "1")])
-def test_gpu_triangle_pruning(gpu, oracle_lib, monkeypatch, prune, octants, primary):
+def test_gpu_triangle_pruning(gpu, oracle_lib, prune, octants, primary):
     """Distance pruning of the triangle walk over the direction-ordered layouts (DESIGN.md
     §5.3c): certified (1, default), none (0), the round-3 relative slack (2); per-lane walk
     and primary pre-pass, and each switch alone: the oracle's result on this scene."""
-    monkeypatch.setenv("RT_TRI_PRUNE", prune)
-    monkeypatch.setenv("RT_TRI_OCTANTS", octants)
-    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
     scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
     rays = scene.camera.recalculate_ray_directions()
-    acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
+    acc, out, n = gpu_render(scene, bounces, 2, rays=rays, prune=int(prune),
+                             tuning={"tri_octants": int(octants), "primary_pass": int(primary)})
     o = oracle_lib.Oracle(scene, camera_rays=rays)
     acc_o = np.zeros((48, 64, 4), np.float32)
     out_o = np.zeros((48, 64), np.uint32)
     n_o = sum(o.render_frame(scene.params(accumulation_index=k), bounces, acc_o, out_o) for k in (1, 2))
     assert_same(acc, out, n, acc_o, out_o, n_o)
+
+
+def test_gpu_environment_has_no_effect(gpu, oracle_lib, monkeypatch):
+    """The library reads no environment (ABI 12): with the round-1..5 switches set
+    -- among them RT_TRI_PRUNE=2, the inexact pruning, and RT_BRUTE_FORCE=1 -- a default context
+    launches the default kernels and renders the oracle's bits on the grazing-ray scene where
+    the inexact mode differs from the sweep."""
+    for k, v in {"RT_TRI_PRUNE": "2", "RT_BRUTE_FORCE": "1", "RT_LDS_MODE": "0", "RT_PRIMARY_PASS": "0",
+                 "RT_FRAME_BATCH": "1", "RT_TRI_OCTANTS": "0", "RT_COOP_LEAVES": "0", "RT_TRI_BVH": "0"}.items():
+        monkeypatch.setenv(k, v)
+    scene, bounces = build_config("c5_heightfield", width=64, height=48, nx=200, nz=100)
+    rays = scene.camera.recalculate_ray_directions()
+    with Renderer(scene, camera_rays=rays) as r:
+        assert r.frame_batch()[0] == N.RT_DEFAULT_FRAME_BATCH
+        r.compute_frame(bounces)
+        r.synchronize()
+        assert r.last_launch_passes() == ["path", "primary"]
+        assert r.launch_config()["scene_in_lds"] == 1
+        r.compute_frame(bounces)
+        acc, out, n = r.read_accumulation(), r.read_output(), r.ray_count()
+    assert_same(acc, out, n, *oracle_frames(oracle_lib, scene, bounces, 2, rays))
+
+
+def test_gpu_tuning_keys_refuse_bad_input(gpu):
+    """rt_set_tuning refuses unknown keys and out-of-range values (RT_E_INVALID), and
+    rt_copy_output_to_device refuses host memory and rank contexts."""
+    scene, bounces = build_config("c2_rtiow", width=64, height=48)
+    with Renderer(scene) as r:
+        for key, value in (("no_such_key", 1), ("lds_mode", 3), ("block_threads", 300), ("queue_stripes", 0),
+                           ("primary_pass", 2), ("batch_memory_mb", 0)):
+            with pytest.raises(RtError) as e:
+                r.set_tuning(key, value)
+            assert e.value.code == N.RT_E_INVALID
+        host = np.zeros(64 * 48, np.uint32)
+        with pytest.raises(RtError):
+            r.copy_output_to_device(host.ctypes.data, 4 * 64)
+    with Renderer(scene, rank=1, world_size=2) as r:
+        import torch
+
+        dev = torch.zeros(64 * 48, dtype=torch.int32, device="cuda")
+        with pytest.raises(RtError):
+            r.copy_output_to_device(dev.data_ptr(), 4 * 64)
 
 
 def test_gpu_leaf_certificates_match_host(gpu):
@@ -560,15 +615,13 @@ def test_gpu_triangle_pruning_full_frames(gpu, config, kw, frames):
 
 
 @pytest.mark.parametrize("prune,primary", [("1", "0"), ("1", "1"), ("0", "0")])
-def test_gpu_grazing_rays_certified_pruning(gpu, oracle_lib, monkeypatch, prune, primary):
+def test_gpu_grazing_rays_certified_pruning(gpu, oracle_lib, prune, primary):
     """Adversarial primary rays (tests/adversarial.py): the camera 1e-4 from a tilted plane
     of 12,800 triangles, every direction within 1e-6..1e-3 rad of that plane after the
     kernel's own jitter (:217-219, cancelled per pixel), so the reference's f32 distances and
     barycentrics are rounding-dominated; then the paths' bounces. The certified walk
     (default) and box culling must give the oracle's result bit for bit, with and without
     the primary pre-pass."""
-    monkeypatch.setenv("RT_TRI_PRUNE", prune)
-    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
     from rust_gpu_raytracing_amd.camera import Camera
     from tests.adversarial import grazing_directions, tilted_plane_grid
 
@@ -592,45 +645,8 @@ def test_gpu_grazing_rays_certified_pruning(gpu, oracle_lib, monkeypatch, prune,
     acc_o = np.zeros((h, w, 4), np.float32)
     out_o = np.zeros((h, w), np.uint32)
     rays_o = o.render_frame(scene.params(accumulation_index=1), bounces, acc_o, out_o)
-    acc, out, n = gpu_render(scene, bounces, 1, rays=rays)
+    acc, out, n = gpu_render(scene, bounces, 1, rays=rays, prune=int(prune), tuning={"primary_pass": int(primary)})
     assert_same(acc, out, n, acc_o, out_o, rays_o)
-
-
-@pytest.mark.parametrize("compact,perturb", [("1", False), ("0", False), ("1", True)])
-def test_gpu_lds_vertex_indexed_triangles(gpu, oracle_lib, monkeypatch, compact, perturb):
-    """Mode 2 stages the triangles as an LDS vertex table (3 u16 indices per triangle) when
-    SceneTriangle::new's arithmetic reproduces every record from its vertices; the leaves then
-    recompute edge_ab / edge_ac / calc_normal (src/buffers.rs:66-95). On (chess), off, and with
-    records that do not follow from their vertices (calc_normal a few ulp off on some
-    triangles: the table is refused and the 64-B records are read): the oracle's result.
-    The table is a build switch (-DRT_LDS_COMPACT=1, off in the product build): whether the
-    loaded library stages it is read from the launch's LDS image (the table adds to it), and the
-    'on' cases skip when it does not."""
-    scene, bounces = build_config("c3_chess", width=96, height=64, env_size=(512, 256))
-    rays = scene.camera.recalculate_ray_directions()
-
-    def lds_bytes(env):
-        monkeypatch.setenv("RT_TRI_LDS_COMPACT", env)
-        with Renderer(scene, camera_rays=rays) as r:
-            r.compute_frame(bounces)
-            cfg = r.launch_config()
-            assert cfg["scene_in_lds"] == 2
-            return cfg["lds_bytes"]
-
-    off = lds_bytes("0")
-    if compact == "1":
-        on = lds_bytes("1")
-        if on == off:
-            pytest.skip("library built without -DRT_LDS_COMPACT=1: no vertex table to test")
-        assert on > off  # the table is staged for the consistent records
-    if perturb:
-        obj = scene.objects[3]
-        obj.triangles = obj.triangles.copy()
-        obj.triangles["calc_normal"][::5] *= np.float32(1.0000002)
-        assert lds_bytes(compact) == off  # refused: the records are read
-    monkeypatch.setenv("RT_TRI_LDS_COMPACT", compact)
-    acc, out, n = gpu_render(scene, bounces, 2, rays=rays)
-    assert_same(acc, out, n, *oracle_frames(oracle_lib, scene, bounces, 2, rays))
 
 
 def test_gpu_update_scene_and_reset(gpu, oracle_lib):
@@ -869,125 +885,59 @@ def test_gpu_device_camera_rays(gpu, config, w, h):
 
 
 @pytest.mark.parametrize("config,kw", [("c3_chess", dict(env_size=(512, 256))), ("c5_heightfield", dict(nx=40, nz=20))])
-def test_gpu_reference_sweep_without_accelerator(gpu, oracle_lib, monkeypatch, config, kw):
-    """RT_TRI_BVH=0: the kernel walks the reference's own object -> sub-object -> triangle
-    sweep (phase 3 of the trace state), same results as the oracle."""
-    monkeypatch.setenv("RT_TRI_BVH", "0")
+def test_gpu_reference_sweep_without_accelerator(gpu, oracle_lib, config, kw):
+    """Tuning "tri_bvh" 0: the kernel walks the reference's own object -> sub-object -> triangle
+    sweep, same results as the oracle."""
     scene, bounces = build_config(config, width=64, height=40, **kw)
     acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
-    assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
+    assert_same(*gpu_render(scene, bounces, 2, tuning={"tri_bvh": 0}), acc_o, out_o, rays_o)
 
 
-@pytest.mark.parametrize("wide,compact", [("0", None), ("1", "0"), ("1", "1")])
-@pytest.mark.parametrize("config,kw", [("c3_chess", dict(env_size=(512, 256))), ("c4_mixed", dict(env_size=(256, 128))),
-                                       ("c5_heightfield", dict(nx=60, nz=30))])
-def test_gpu_triangle_accelerators(gpu, oracle_lib, monkeypatch, config, kw, wide, compact):
-    """Both triangle accelerators against the oracle: the binary stackless walk
-    (RT_TRI_WIDE=0) and the 4-wide stack walk (tri_wide.h), whose leaves either read
-    the triangle records (RT_TRI_COMPACT=0) or recompute them from vertex blocks
-    (RT_TRI_COMPACT=1; by default only for meshes beyond one XCD's L2)."""
-    monkeypatch.setenv("RT_TRI_WIDE", wide)
-    if compact is not None:
-        monkeypatch.setenv("RT_TRI_COMPACT", compact)
-    scene, bounces = build_config(config, width=96, height=64, **kw)
-    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
-    assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
-
-
-@pytest.mark.parametrize("env", [
-    {"RT_TRI_Q4": "1"},
-    {"RT_COOP_LEAVES": "0"},
-    {"RT_BLOCK_THREADS": "256"},
-    {"RT_TRI_PRUNE": "0", "RT_PRIMARY_PASS": "0"},
+@pytest.mark.parametrize("tuning", [
+    {"coop_leaves": 0},
+    {"block_threads": 256},
+    {"primary_pass": 0, "prune": 0},
+    {"tri_octants": 0, "tri_qnodes": 0},
+    {"leaf_batch": 8, "trav_threshold": 63, "drain_threshold": 0},
 ])
 @pytest.mark.parametrize("config,kw", [("c4_mixed", dict(env_size=(256, 128))), ("c5_heightfield", dict(nx=60, nz=30)),
                                        ("c3_chess", dict(env_size=(512, 256)))])
-def test_gpu_global_walk_variants(gpu, oracle_lib, monkeypatch, config, kw, env):
-    """The walks from global memory (scene not staged in LDS: RT_LDS_MODE=1): per-lane leaf tests
-    instead of the cooperative leaf batches (RT_COOP_LEAVES=0), 256-thread workgroups, box
-    culling without the primary pre-pass, and the 4-wide quantized accelerator with its per-lane
-    LDS stack (tri_q4.h, RT_TRI_Q4=1 in a -DRT_Q4=1 build -- skipped otherwise): the oracle's
-    images and ray counts."""
-    monkeypatch.setenv("RT_LDS_MODE", "1")
+def test_gpu_global_walk_variants(gpu, oracle_lib, config, kw, tuning):
+    """The walks from global memory (scene not staged in LDS: tuning "lds_mode" 1): per-lane leaf
+    tests instead of the cooperative leaf batches, 256-thread workgroups, box culling without the
+    primary pre-pass, one layout of 32-B nodes, extreme schedule thresholds: the oracle's images
+    and ray counts."""
     scene, bounces = build_config(config, width=96, height=64, **kw)
-
-    def lds_bytes():
-        with Renderer(scene) as r:
-            r.compute_frame(bounces)
-            cfg = r.launch_config()
-            assert cfg["scene_in_lds"] <= 1
-            return cfg["lds_bytes"]
-
-    if env.get("RT_TRI_Q4") == "1":
-        # the 4-wide walk is a build switch (-DRT_Q4=1, off in the product build); its per-lane
-        # stacks add to the launch's LDS image when it runs
-        base = lds_bytes()
-        monkeypatch.setenv("RT_TRI_Q4", "1")
-        if lds_bytes() == base:
-            pytest.skip("library built without -DRT_Q4=1: no 4-wide walk to test")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    tuning = dict(tuning, lds_mode=1)
+    prune = tuning.pop("prune", None)
+    with Renderer(scene, tuning=tuning) as r:
+        r.compute_frame(bounces)
+        assert r.launch_config()["scene_in_lds"] <= 1
     acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 2)
-    assert_same(*gpu_render(scene, bounces, 2), acc_o, out_o, rays_o)
-
-
-def test_gpu_wide_compact_after_triangle_updates(gpu, oracle_lib, monkeypatch):
-    """rt_update_triangles with records a compact leaf cannot reproduce (calc_normal
-    off by a few ulp): the device recheck turns those leaves back to reading the
-    records, and restores compactness when consistent records return -- the image
-    follows the oracle given the same records each time."""
-    monkeypatch.setenv("RT_TRI_COMPACT", "1")
-    scene, bounces = build_config("c5_heightfield", width=80, height=48, nx=50, nz=25)
-    objs, subs, tris = scene.flatten()
-    bad = tris.copy()
-    sel = np.arange(0, bad.shape[0], 5)
-    bad["calc_normal"][sel] *= np.float32(1.0000002)
-    with Renderer(scene) as r:
-        r.compute_frame(bounces)
-        r._call("rt_update_triangles", N.ptr(bad), bad.shape[0])
-        r.reset_accumulation()
-        r.compute_frame(bounces)
-        got_bad = r.read_accumulation(), r.read_output(), r.ray_count()
-        r._call("rt_update_triangles", N.ptr(tris), tris.shape[0])
-        r.reset_accumulation()
-        r.reset_ray_count()
-        r.compute_frame(bounces)
-        got_good = r.read_accumulation(), r.read_output(), r.ray_count()
-    o = oracle_lib.Oracle(scene)
-    acc = np.zeros((48, 80, 4), np.float32)
-    out = np.zeros((48, 80), np.uint32)
-    n = o.render_frame(scene.params(accumulation_index=1), bounces, acc, out)
-    assert_same(*got_good, acc, out, n)
-    # the inconsistent records, through the oracle
-    bad_scene, _ = build_config("c5_heightfield", width=80, height=48, nx=50, nz=25)
-    bad_scene.objects[0].triangles = bad
-    ob = oracle_lib.Oracle(bad_scene)
-    acc_b = np.zeros((48, 80, 4), np.float32)
-    out_b = np.zeros((48, 80), np.uint32)
-    nb = ob.render_frame(bad_scene.params(accumulation_index=1), bounces, acc_b, out_b)
-    assert np.array_equal(got_bad[1], out_b)
-    assert np.array_equal(got_bad[0].view(np.uint32), acc_b.view(np.uint32))
+    assert_same(*gpu_render(scene, bounces, 2, prune=prune, tuning=tuning), acc_o, out_o, rays_o)
 
 
 @pytest.mark.parametrize("config,kw,spp,accumulate,batch,world,env", [
-    ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {"RT_PRIMARY_PASS": "1"}),
-    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {"RT_PRIMARY_PASS": "1"}),  # non-accumulating batch
-    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 4, 3, {"RT_PRIMARY_PASS": "1"}),  # tile split
-    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 2, 1, {"RT_FRAME_PARALLEL": "0", "RT_PRIMARY_PASS": "1"}),
-    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 1, 1, {"RT_PRIMARY_PASS": "1", "RT_LDS_MODE": "1"}),
+    ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {"primary_pass": 1}),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {"primary_pass": 1}),  # non-accumulating batch
+    ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 4, 3, {"primary_pass": 1}),  # tile split
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 2, 1, {"frame_parallel": 0, "primary_pass": 1}),
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 1, 1, 1, {"primary_pass": 1, "lds_mode": 1}),
     ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 2, 1, {}),       # default: on (accelerator in global memory)
     # pre-pass workgroup sizes and unit orders (the default is 256 threads held to 64 VGPRs)
-    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 3, 1, {"RT_PRIMARY_THREADS": "64", "RT_PRIMARY_TILE_MAJOR": "1"}),
-    ("c5_heightfield", dict(nx=200, nz=100), 2, 1, 3, 2, {"RT_PRIMARY_THREADS": "1024", "RT_PRIMARY_TILE_MAJOR": "1"}),
-    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 3, 1, {"RT_PRIMARY_WAVES": "0"}),
+    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 3, 1, {"primary_threads": 64, "primary_tile_major": 0}),
+    ("c5_heightfield", dict(nx=200, nz=100), 2, 1, 3, 2, {"primary_threads": 1024, "primary_tile_major": 1}),
+    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 3, 1, {"primary_waves": 0}),
+    # a batch budget of 1 MB (ADVICE r05): the batches run as consecutive launches of the
+    # frames whose lights and primary records fit
+    ("c5_heightfield", dict(nx=200, nz=100), 2, 1, 3, 1, {"batch_memory_mb": 1}),
+    ("c3_chess", dict(env_size=(512, 256)), 1, 1, 4, 3, {"batch_memory_mb": 1}),
 ])
-def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumulate, batch, world, env):
+def test_gpu_primary_pass(gpu, oracle_lib, config, kw, spp, accumulate, batch, world, env):
     """rt_primary_kernel traces every path's first segment as 8x8 packets (wave-uniform
     node walk, per-lane culling and exact leaf tests); the path kernel starts from its
     records. Results must equal the oracle's (and therefore the per-lane walk's) in
     batches, with several samples, without accumulation and in tile splits."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     scene, bounces = build_config(config, width=96, height=64, **kw)
     rays = scene.camera.recalculate_ray_directions()
     o = oracle_lib.Oracle(scene, camera_rays=rays)
@@ -1002,7 +952,7 @@ def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumul
     n = 0
     for rank in range(world):
         with Renderer(scene, camera_rays=rays, frame_batch=batch, rank=rank, world_size=world,
-                      compute_per_frame=spp, accumulate=bool(accumulate)) as r:
+                      compute_per_frame=spp, accumulate=bool(accumulate), tuning=env) as r:
             for _ in range(4):
                 r.compute_frame(bounces)
             a, oo, k = r.read_accumulation(), r.read_output(), r.ray_count()
@@ -1023,15 +973,13 @@ def test_gpu_primary_pass(gpu, oracle_lib, monkeypatch, config, kw, spp, accumul
     ("c4_mixed", dict(env_size=(256, 128)), 2, 3),
     ("c5_heightfield", dict(nx=60, nz=30), 2, 1),
 ])
-@pytest.mark.parametrize("wf,mode", [("1", 1), ("1", 2), ("0", 1)])
-def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, world, wf, mode):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gpu_brute_force_mode(gpu, oracle_lib, config, kw, batch, world, mode):
     """rt_set_brute_force: the reference's own sphere and object -> sub-object ->
     triangle sweeps, sub-objects streamed through LDS tiles (BASELINE config 5's
-    stress mode) -- bit-identical to the oracle, in frame batches and tile splits. Both
-    kernels: the wavefront over compacted queues of live paths (rt_brute_wf_kernel, the
-    default; the sub-object records LDS-tiled, or streamed through the scalar cache with
-    rt_set_brute_force(ctx, 2)) and the lockstep workgroups (RT_BRUTE_WF=0, rt_brute_kernel)."""
-    monkeypatch.setenv("RT_BRUTE_WF", wf)
+    stress mode) -- bit-identical to the oracle, in frame batches and tile splits: the
+    wavefront over compacted queues of live paths (rt_brute_wf_kernel), the sub-object records
+    LDS-tiled, or streamed through the scalar cache with rt_set_brute_force(ctx, 2)."""
     scene, bounces = build_config(config, width=96, height=64, **kw)
     rays = scene.camera.recalculate_ray_directions()
     acc_o, out_o, n_o = oracle_frames(oracle_lib, scene, bounces, 4, rays)
@@ -1061,6 +1009,8 @@ def test_gpu_brute_force_mode(gpu, oracle_lib, monkeypatch, config, kw, batch, w
     ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, None, 2),
     ("c4_mixed", dict(env_size=(256, 128)), 1, 1, 1, 0, 1),
     ("c1_four_spheres", {}, 1, 1, 2, 40, 1),
+    ("c5_heightfield", dict(nx=40, nz=20), 1, 1, 2, 80, 2),  # beyond round 5's 62-bounce limit
+    ("c2_rtiow", {}, 1, 1, 2, None, 2),  # no triangles: mode 2 runs mode 1's sweep
 ])
 def test_gpu_brute_force_samples_and_modes(gpu, oracle_lib, config, kw, spp, accumulate, batch, bounces, mode):
     """The brute-force wavefront's passes: several samples per frame (each pass = one (frame,
@@ -1078,7 +1028,7 @@ def test_gpu_brute_force_samples_and_modes(gpu, oracle_lib, config, kw, spp, acc
         for _ in range(3):
             r.compute_frame(bounces)
         got = r.read_accumulation(), r.read_output(), r.ray_count()
-        assert r.last_launch_passes() == ["brute"]
+        assert r.last_launch_passes() == (["brute", "brute_stream"] if mode == 2 and scene.objects else ["brute"])
     o = oracle_lib.Oracle(scene, camera_rays=rays)
     acc = np.zeros((48, 80, 4), np.float32)
     out = np.zeros((48, 80), np.uint32)
@@ -1101,14 +1051,13 @@ def _pcg_f32(seed):
 
 
 @pytest.mark.parametrize("primary", ["0", "1"])
-def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib, monkeypatch, primary):
+def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib, primary):
     """Rays lying exactly in a triangle's plane (det == 0, origin on the plane) give a NaN
     distance that the reference's sweep accepts (:449-481, :457); the accelerator hands such
     lanes to the sweep itself. Primary directions are chosen so that d.y + jitter.y == 0
     exactly (the jitter is the kernel's own PCG draw, :217-219). Such a hit has NaN
     barycentrics too, which pass the reference's `< 0` rejections (:467-481). With and
     without the primary pre-pass."""
-    monkeypatch.setenv("RT_PRIMARY_PASS", primary)
     from rust_gpu_raytracing_amd.camera import Camera
     from rust_gpu_raytracing_amd.scene import SceneObject
 
@@ -1135,7 +1084,7 @@ def test_gpu_in_plane_rays_nan_distance(gpu, oracle_lib, monkeypatch, primary):
     acc_o = np.zeros((32, 48, 4), np.float32)
     out_o = np.zeros((32, 48), np.uint32)
     rays_o = o.render_frame(scene.params(accumulation_index=1), bounces, acc_o, out_o)
-    acc, out, n = gpu_render(scene, bounces, 1, rays=rays)
+    acc, out, n = gpu_render(scene, bounces, 1, rays=rays, tuning={"primary_pass": int(primary)})
     assert_same(acc, out, n, acc_o, out_o, rays_o)
 
 
@@ -1175,17 +1124,16 @@ def test_gpu_device_edit_models_invalidated_by_range_change(gpu):
 
 
 @pytest.mark.parametrize("overlap", ["1", "0"])
-def test_gpu_overlapped_batches_with_updates(gpu, oracle_lib, monkeypatch, overlap):
+def test_gpu_overlapped_batches_with_updates(gpu, oracle_lib, overlap):
     """Consecutive frame-parallel batches alternate between two HIP streams (the path
     kernel of batch i overlaps batch i-1's drain; only its resolve waits for batch
     i-1's): results must equal the one-frame-at-a-time sequence, including when
     scene updates, a reset and readbacks are interleaved with queued batches."""
-    monkeypatch.setenv("RT_BATCH_OVERLAP", overlap)
     scene, bounces = build_config("c2_rtiow", width=128, height=72)
     rays = scene.camera.recalculate_ray_directions()
 
     def run(batch):
-        with Renderer(scene, camera_rays=rays, frame_batch=batch) as r:
+        with Renderer(scene, camera_rays=rays, frame_batch=batch, tuning={"batch_overlap": int(overlap)}) as r:
             for _ in range(7):
                 r.compute_frame(bounces)
             a1 = r.read_accumulation()
@@ -1215,18 +1163,17 @@ def test_gpu_overlapped_batches_with_updates(gpu, oracle_lib, monkeypatch, overl
     assert np.array_equal(got[1], out_o) and np.array_equal(got[0].view(np.uint32), acc_o.view(np.uint32))
 
 
-def test_gpu_overlapped_batch_after_plain_launch(gpu, oracle_lib, monkeypatch):
+def test_gpu_overlapped_batch_after_plain_launch(gpu, oracle_lib):
     """A one-frame flush (a bounce change flushing a single queued frame) is a plain
     launch on the primary stream that reads and writes the accumulation; the next
     batch lands on the auxiliary stream and its resolve must wait for that launch too
     (primary_dirty after a plain launch). Sequence: batches on primary,
     aux, primary, then 1 frame at b, compute_frame(b + 1) flushing it alone, then a
     full batch at b + 1 on aux -- against the oracle's single frames."""
-    monkeypatch.setenv("RT_BATCH_OVERLAP", "1")
     scene, b = build_config("c2_rtiow", width=320, height=184)
     rays = scene.camera.recalculate_ray_directions()
     seq = [b] * 13 + [b + 1] * 4
-    with Renderer(scene, camera_rays=rays, frame_batch=4) as r:
+    with Renderer(scene, camera_rays=rays, frame_batch=4, tuning={"batch_overlap": 1}) as r:
         for bb in seq:
             r.compute_frame(bb)
         got = r.read_accumulation(), r.read_output(), r.ray_count()

@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
-    ap.add_argument("--env", nargs="*", default=[], help="KNOB=V settings for every build (before its own :knobs)")
+    ap.add_argument("--tune", nargs="*", default=[], help="key=v rt_set_tuning settings for every build (before its own)")
     ap.add_argument("--device-rays", action="store_true", help="generate primary rays on the device")
     ap.add_argument("--frame-batch", type=int, default=8, help="rt_set_frame_batch (frames is rounded to a multiple)")
     ap.add_argument("--world", type=int, default=1, help="time rank --rank's share of an N-way tile split")
@@ -44,23 +44,18 @@ def main():
     scene, bounces = build_config(args.config, width=args.width, height=args.height)
     rays_dirs = scene.camera.recalculate_ray_directions()
     rs = []
-    import os
     for spec in args.libs:
-        # "path.so" or "path.so:KNOB=V,KNOB2=V": env knobs are read when the context is created
+        # "path.so" or "path.so:key=v,key2=v": rt_set_tuning settings of that build's context
         p, _, knobs = spec.partition(":")
-        saved = dict(os.environ)
-        for kv in [*args.env, *filter(None, knobs.split(","))]:  # --env applies to every build
-            k, _, v = kv.partition("=")
-            os.environ[k] = v
+        tuning = {k: int(v) for k, v in (kv.split("=", 1) for kv in [*args.tune, *filter(None, knobs.split(","))])}
         lib = N.load_library(Path(p).resolve())
+        kw = dict(lib=lib, frame_batch=args.frame_batch, rank=args.rank, world_size=args.world)
+        if tuning:  # (older builds predate rt_set_tuning: pass none to them)
+            kw["tuning"] = tuning
         if args.device_rays:
-            rs.append(Renderer(scene, lib=lib, device_rays=True, frame_batch=args.frame_batch,
-                               rank=args.rank, world_size=args.world))
+            rs.append(Renderer(scene, device_rays=True, **kw))
         else:
-            rs.append(Renderer(scene, camera_rays=rays_dirs, lib=lib, frame_batch=args.frame_batch,
-                               rank=args.rank, world_size=args.world))
-        os.environ.clear()
-        os.environ.update(saved)
+            rs.append(Renderer(scene, camera_rays=rays_dirs, **kw))
     args.frames = max(1, args.frames // args.frame_batch) * args.frame_batch
     for r in rs:  # warmup
         for _ in range(args.frame_batch):

@@ -1,12 +1,11 @@
-"""Interleaved A/B of ONE build under different per-context environment settings.
+"""Interleaved A/B of ONE build under different per-context tunings (rt_set_tuning).
 
-usage: python tools/ab_env.py "RT_BLOCK_THREADS=256" "RT_BLOCK_THREADS=512" ... [--config ...]
-Each spec is a space-separated list of VAR=VALUE applied while that variant's
-context is created (the runtime reads its switches at rt_create).
+usage: python tools/ab_env.py "block_threads=256" "block_threads=512 leaf_batch=4" ... [--config ...]
+Each spec is a space-separated list of KEY=VALUE tuning settings (include/rt_abi.h lists the
+keys; "prune=N" calls rt_set_triangle_pruning) for that variant's context; "" is the default.
 """
 import argparse
 import json
-import os
 import statistics
 import sys
 import time
@@ -35,14 +34,13 @@ def main():
     dirs = scene.camera.recalculate_ray_directions()
     rs = []
     for spec in args.specs:
-        saved = dict(os.environ)
-        for kv in spec.split():
-            k, v = kv.split("=", 1)
-            os.environ[k] = v
+        tuning = {k: int(v) for k, v in (kv.split("=", 1) for kv in spec.split())}
+        prune = tuning.pop("prune", None)
         rank, world = map(int, args.split.split("/"))
-        rs.append(Renderer(scene, camera_rays=dirs, frame_batch=args.frame_batch, rank=rank, world_size=world))
-        os.environ.clear()
-        os.environ.update(saved)
+        r = Renderer(scene, camera_rays=dirs, frame_batch=args.frame_batch, rank=rank, world_size=world, tuning=tuning)
+        if prune is not None:
+            r.set_triangle_pruning(prune)
+        rs.append(r)
     for r in rs:
         for _ in range(args.frame_batch):
             r.compute_frame(bounces)

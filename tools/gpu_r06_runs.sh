@@ -1,0 +1,31 @@
+#!/bin/bash
+# The round-6 GPU sessions, one case per run tag (outputs: gpurun_out/<tag>/, copied to
+# profiles/r06/<tag>/ when DESIGN.md cites them). usage (via gpurun): bash tools/gpu_r06_runs.sh <tag>
+set -o pipefail
+T=$1
+mkdir -p gpurun_out/$T
+case "$T" in
+  r06a)
+    # C2 regression bisect: the round-4 final kernel and each round-5 kernel commit against the
+    # round-5 head, one process (tools/build_at_commit.py builds, abvar/bisect/)
+    L="abvar/bisect/lib_797545e.so"
+    for c in fcb6cf7 3e2677f f524fdb 25c7b12 a054092 6da6bce 37b2ecf; do L="$L abvar/bisect/lib_$c.so"; done
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    ;;
+  r06b)
+    # the cleaned ABI-12 build: every GPU test, smoke, then same-process A/B against the r05
+    # head and the r04 final builds on C2, C3, C5
+    timeout -k 10 900 python3 -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    L="rust_gpu_raytracing_amd/librt_pathtrace.so abvar/bisect/lib_797545e.so abvar/bisect/lib_fcb6cf7.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 5 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    timeout -k 10 300 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_tiled.json 2> gpurun_out/$T/brute_tiled.err || exit 1
+    timeout -k 10 300 python3 bench.py --config c5_heightfield --brute-force stream --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_stream.json 2> gpurun_out/$T/brute_stream.err || exit 1
+    timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    ;;
+  *)
+    echo "unknown tag $T"; exit 2
+    ;;
+esac
