@@ -25,6 +25,25 @@ case "$T" in
     timeout -k 10 300 python3 bench.py --config c5_heightfield --brute-force stream --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_stream.json 2> gpurun_out/$T/brute_stream.err || exit 1
     timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
     ;;
+  r06c)
+    # what the C2 kernel time is sensitive to: the culling bound's range check compiled out
+    # (diagnostic), loop alignment off, non-fallthrough blocks aligned to 64 B
+    L="rust_gpu_raytracing_amd/librt_pathtrace.so abvar/bisect/lib_fcb6cf7.so abvar/r06c/lib_noguard.so abvar/r06c/lib_noalign.so abvar/r06c/lib_blk64.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 5 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    # the bench step's wall time against its launch span (one 20-frame launch between syncs)
+    timeout -k 10 200 python3 tools/launch_gap.py rust_gpu_raytracing_amd/librt_pathtrace.so abvar/bisect/lib_797545e.so abvar/bisect/lib_fcb6cf7.so > gpurun_out/$T/launch_gap.jsonl 2> gpurun_out/$T/launch_gap.err || exit 1
+    timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/$T/bench1.json 2> gpurun_out/$T/bench1.err || exit 1
+    timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-cadences > gpurun_out/$T/bench2.json 2> gpurun_out/$T/bench2.err || exit 1
+    ;;
+  r06d)
+    # the treelet wavefront: its GPU tests, then C5 against the persistent walk (same process and bench)
+    timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -m gpu -k "treelet or environment or tuning" > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 400 python3 tools/ab_env.py "" "treelet_walk=1" --config c5_heightfield --frame-batch 20 --frames 40 --rounds 3 > gpurun_out/$T/ab_c5.jsonl 2> gpurun_out/$T/ab_c5.err || exit 1
+    timeout -k 10 300 python3 bench.py --config c5_heightfield --tune treelet_walk=1 --no-cpu-baseline --no-cadences > gpurun_out/$T/bench_c5_tl.json 2> gpurun_out/$T/bench_c5_tl.err || exit 1
+    timeout -k 10 300 python3 bench.py --config c5_heightfield --no-cpu-baseline --no-cadences > gpurun_out/$T/bench_c5.json 2> gpurun_out/$T/bench_c5.err || exit 1
+    ;;
   *)
     echo "unknown tag $T"; exit 2
     ;;

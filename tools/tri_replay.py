@@ -2,8 +2,8 @@
 
 Renders a sample of a BASELINE configuration's pixels with the CPU oracle (trace log on),
 dumps the scene's object / sub-object / triangle records and every traced ray, and runs
-tests/cpp/tri_exactness on them: every walk (binary, wide, quantized, octant layouts with
-the relative slack, certified cones, leaf certificates) checked ray by ray against the
+tests/cpp/tri_exactness on them: every walk (binary, quantized, octant layouts with the
+relative slack, leaf certificates, the kernel's default) checked ray by ray against the
 reference's sweep, with node visits and triangle tests per ray.
 
 usage: python tools/tri_replay.py [config] [stride] [extra env VAR=VAL ...]
@@ -29,8 +29,8 @@ from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 def harness(out: Path) -> Path:
     csrc = ROOT / "rust_gpu_raytracing_amd" / "csrc"
     subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", f"-I{ROOT / 'include'}", f"-I{csrc}",
-                    str(ROOT / "tests" / "cpp" / "tri_exactness.cpp"), str(csrc / "sphere_bvh.cpp"),
-                    str(csrc / "tri_wide.cpp"), "-o", str(out)], check=True)
+                    str(ROOT / "tests" / "cpp" / "tri_exactness.cpp"), str(csrc / "sphere_bvh.cpp"), "-o", str(out)],
+                   check=True)
     return out
 
 
