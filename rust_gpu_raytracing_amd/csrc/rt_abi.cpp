@@ -298,7 +298,8 @@ struct rt_ctx {
     uint32_t* d_tl_lists = nullptr;
     uint32_t* d_tl_ctl = nullptr;
     uint32_t* d_tl_cnt = nullptr;
-    size_t tl_paths_cap = 0, tl_walk_cap = 0, tl_lists_cap = 0, tl_ctl_cap = 0, tl_cnt_cap = 0;
+    uint4* d_tl_chunks = nullptr;
+    size_t tl_paths_cap = 0, tl_walk_cap = 0, tl_lists_cap = 0, tl_ctl_cap = 0, tl_cnt_cap = 0, tl_chunks_cap = 0;
     uint32_t* h_tl_ctl = nullptr;  // pinned: the list lengths read back every few rounds
     uint64_t tl_rounds = 0;        // wavefront rounds of the last treelet launch (diagnostics)
     size_t tri_ltris_cap = 0;
@@ -876,7 +877,7 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tri_qgrid, ctx->d_tri_src8, ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert,
                     ctx->d_tri_ltris, ctx->d_brute_paths, ctx->d_brute_queue, ctx->d_brute_counts,
                     ctx->d_tl_subtrees, ctx->d_tl_src, ctx->d_tl_links, ctx->d_tl_top, ctx->d_tl_paths,
-                    ctx->d_tl_walk, ctx->d_tl_lists, ctx->d_tl_ctl, ctx->d_tl_cnt};
+                    ctx->d_tl_walk, ctx->d_tl_lists, ctx->d_tl_ctl, ctx->d_tl_cnt, ctx->d_tl_chunks};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1159,7 +1160,9 @@ static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32
         (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_walk), &ctx->tl_walk_cap, 2 * n_slots * sizeof(uint4))) ||
         (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_lists), &ctx->tl_lists_cap, 5 * n_slots * sizeof(uint32_t))) ||
         (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_ctl), &ctx->tl_ctl_cap, 8 * sizeof(uint32_t))) ||
-        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_cnt), &ctx->tl_cnt_cap, (2 * (size_t)ctx->tl_n_sub + 1) * 4)))
+        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_cnt), &ctx->tl_cnt_cap, (2 * (size_t)ctx->tl_n_sub + 1) * 4)) ||
+        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_chunks), &ctx->tl_chunks_cap,
+                   ((size_t)ctx->tl_n_sub + n_slots / kTlChunk + 1) * sizeof(uint4))))
         return rc;
     if (!ctx->h_tl_ctl) RT_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_tl_ctl), 8 * sizeof(uint32_t), hipHostMallocDefault));
     // the top layouts' boxes, from the base accelerator as it is now
@@ -1214,6 +1217,7 @@ static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32
     ta.ctl = ctx->d_tl_ctl;
     ta.sub_cnt = ctx->d_tl_cnt;
     ta.sub_off = ctx->d_tl_cnt + ctx->tl_n_sub;
+    ta.chunks = ctx->d_tl_chunks;
     ta.subtrees = ctx->d_tl_subtrees;
     ta.top = ctx->d_tl_top;
     ta.base_nodes = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
@@ -1221,6 +1225,9 @@ static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32
     ta.n_slots = (uint32_t)n_slots;
     ta.n_sub = ctx->tl_n_sub;
     const uint32_t grid = 4u * (uint32_t)std::max(1, ctx->n_cu);
+    // the treelet walks: as many workgroups as stay resident with their LDS image (5 per CU at 30 KB)
+    const uint32_t walk_grid = (uint32_t)std::min<uint64_t>(5u * (uint32_t)std::max(1, ctx->n_cu),
+                                                            (uint64_t)ctx->tl_n_sub + n_slots / kTlChunk + 1);
     const size_t tl_lds = rt_tl_subtree_lds_bytes(kTreeletNodes, ctx->tl_max_leaves);
     ta.round = 0;
     RT_HIP(ctx, rt_launch_tl(0, ka, ta, (uint32_t)std::min<uint64_t>(grid, (n_slots + 255) / 256), image, S));
@@ -1235,7 +1242,7 @@ static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32
         RT_HIP(ctx, rt_launch_tl(2, ka, ta, grid, 0, S));
         RT_HIP(ctx, rt_launch_tl(3, ka, ta, 1, 0, S));
         RT_HIP(ctx, rt_launch_tl(4, ka, ta, grid, 0, S));
-        RT_HIP(ctx, rt_launch_tl(5, ka, ta, ctx->tl_n_sub, tl_lds, S));
+        RT_HIP(ctx, rt_launch_tl(5, ka, ta, walk_grid, tl_lds, S));
         if (r % kCheck == kCheck - 1) {
             RT_HIP(ctx, hipMemcpyAsync(ctx->h_tl_ctl, ctx->d_tl_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, S));
             RT_HIP(ctx, hipStreamSynchronize(S));

@@ -15,12 +15,15 @@ constexpr uint32_t kTlNone = 0xffffffffu;
 // Largest treelet (nodes of the base layout's pre-order range): its nodes, leaf records and
 // leaf triangle blocks in one workgroup's LDS (<= 128 nodes, <= 64 leaves: 29 KB).
 constexpr uint32_t kTreeletNodes = 128;
+// Rays per work item of a round's treelet walks: a treelet's queue in chunks of this many.
+constexpr uint32_t kTlChunk = 1024;
 
 struct TreeletArgs {
     float4* paths;             // 4 planes x n_slots: o + seed, d + bounce, light, contribution
     uint4* walk;               // 2 planes x n_slots: best triangle, {resume position, treelet, rank, -}
     uint32_t* lists;           // walk lists A[2], shading lists R[2], treelet entries: 5 x n_slots slot ids
-    uint32_t* ctl;             // list lengths: A[0], A[1], R[0], R[1]
+    uint32_t* ctl;             // list lengths: A[0], A[1], R[0], R[1]; [4]: the round's treelet chunks
+    uint4* chunks;             // the round's work list: {treelet, first entry, rays, -}
     uint32_t* sub_cnt;         // per treelet: rays queued this round
     uint32_t* sub_off;         // per treelet: exclusive prefix of sub_cnt (n_sub + 1)
     const uint4* subtrees;     // per treelet: {base root, nodes, first leaf record, leaf records}

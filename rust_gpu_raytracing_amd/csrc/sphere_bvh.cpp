@@ -420,7 +420,7 @@ bool build_treelet_cut(const std::vector<SphereBvhNode>& nodes, uint32_t max_nod
             if (tid[src] != kInternal) {
                 leafw = kTreelet | tid[src];
             } else if (nodes[src].leaf != kSphereBvhInternal) {
-                leafw = nodes[src].leaf;
+                leafw = nodes[src].leaf & 0xffffffu;  // the leaf record
             } else {
                 leafw = kInternal;
                 uint32_t a = src + 1, b = nodes[src + 1].skip;  // order_bvh_by_octant's child order

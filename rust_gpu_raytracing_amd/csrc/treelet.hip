@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(kTlThreads) rt_tl_top_kernel(KernelArgs ka, Tr
                     pos = skip;
                     break;
                 }
-                if (hit) tri_leaf<true>(sv, ka, o, d, ts, leaf);  // a leaf above the cut
+                if (hit) tri_leaf<true>(sv, ka, o, d, ts, leaf & 0xffffffu);  // a leaf above the cut (its record index)
                 pos = skip;
             }
             if (target != kTlNone) {
@@ -253,27 +253,40 @@ __global__ void __launch_bounds__(kTlThreads) rt_tl_top_kernel(KernelArgs ka, Tr
     }
 }
 
-// Exclusive prefix of the treelets' queue lengths (one workgroup of 1024 threads).
+// Exclusive prefix of the treelets' queue lengths, and the round's work list: each treelet's
+// queue cut into chunks of at most kTlChunk rays, {treelet, first entry, rays} (a hot treelet --
+// the ground under the camera -- is walked by many workgroups at once). One workgroup of 1024
+// threads; it also zeroes the queue lengths for the next round's top walk (their last reader).
 __global__ void __launch_bounds__(1024) rt_tl_scan_kernel(TreeletArgs ta) {
-    __shared__ uint32_t part[1024];
+    __shared__ uint32_t part[1024], cpart[1024];
     const uint32_t tid = threadIdx.x, n = ta.n_sub;
     const uint32_t per = (n + 1023u) / 1024u, lo = min(n, tid * per), hi = min(n, lo + per);
-    uint32_t s = 0;
-    for (uint32_t k = lo; k < hi; ++k) s += ta.sub_cnt[k];
+    uint32_t s = 0, c = 0;
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t m = ta.sub_cnt[k];
+        s += m;
+        c += (m + kTlChunk - 1u) / kTlChunk;
+    }
     part[tid] = s;
+    cpart[tid] = c;
     __syncthreads();
     for (uint32_t off = 1; off < 1024u; off <<= 1) {
         const uint32_t add = tid >= off ? part[tid - off] : 0u;
+        const uint32_t cadd = tid >= off ? cpart[tid - off] : 0u;
         __syncthreads();
         part[tid] += add;
+        cpart[tid] += cadd;
         __syncthreads();
     }
-    uint32_t run = part[tid] - s;  // exclusive
+    uint32_t run = part[tid] - s, crun = cpart[tid] - c;  // exclusive
     for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t m = ta.sub_cnt[k];
         ta.sub_off[k] = run;
-        run += ta.sub_cnt[k];
+        for (uint32_t j = 0; j < m; j += kTlChunk) ta.chunks[crun++] = make_uint4(k, run + j, min(kTlChunk, m - j), 0u);
+        run += m;
+        ta.sub_cnt[k] = 0u;
     }
-    if (tid == 1023u) ta.sub_off[n] = part[1023];
+    if (tid == 1023u) ta.ctl[4] = cpart[1023];
 }
 
 // Queue entries in treelet order: entries[sub_off[t] + rank] = slot.
@@ -289,114 +302,121 @@ __global__ void __launch_bounds__(kTlThreads) rt_tl_scatter_kernel(TreeletArgs t
     }
 }
 
-// One workgroup per treelet: its nodes (the base layout's pre-order range), leaf records and
-// leaf triangle blocks staged in LDS, then every ray queued on it walked from there; the rays
-// go back to the top walk (A[q ^ 1]).
+// The treelet walks, a chunk of a treelet's queue per workgroup step: the treelet's nodes (the
+// base layout's pre-order range), leaf records and leaf triangle blocks staged in LDS, then the
+// chunk's rays walked from there; the rays go back to the top walk (A[q ^ 1]).
 __global__ void __launch_bounds__(kTlThreads) rt_tl_subtree_kernel(KernelArgs ka, TreeletArgs ta) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint32_t tid = threadIdx.x, t = blockIdx.x, q = ta.round & 1u;
-    if (t == 0 && tid == 0) ta.ctl[q] = 0u;  // A[q] was walked and scattered (the previous kernels)
-    if (t >= ta.n_sub) return;
-    const uint32_t n = ta.sub_cnt[t];
-    if (n == 0) return;
-    const uint4 st = ta.subtrees[t];  // root (base layout), nodes, first leaf record, leaf records
-    const uint32_t root = st.x, nn = st.y, p0 = st.z, np = st.w;
-    float4* l_nodes = reinterpret_cast<float4*>(lds);
-    uint4* l_prims = reinterpret_cast<uint4*>(lds + (size_t)nn * 32u);
-    uint4* l_tris = l_prims + np;
-    const float4* g_nodes = ta.base_nodes + 2u * (size_t)root;
-    for (uint32_t k = tid; k < 2u * nn; k += kTlThreads) l_nodes[k] = g_nodes[k];
-    for (uint32_t k = tid; k < np; k += kTlThreads) l_prims[k] = ka.tri_prims[p0 + k];
-    const uint4* g_tris = ka.tri_leaftris + (size_t)p0 * kLeafTriWords;
-    for (uint32_t k = tid; k < np * kLeafTriWords; k += kTlThreads) l_tris[k] = g_tris[k];
-    __syncthreads();
-    if (tid == 0) ta.sub_cnt[t] = 0u;  // (every thread has read n) zero for the next round's queueing
+    const uint32_t tid = threadIdx.x, q = ta.round & 1u;
+    if (blockIdx.x == 0 && tid == 0) ta.ctl[q] = 0u;  // A[q] was walked and scattered (the previous kernels)
+    const uint32_t n_chunks = ta.ctl[4];
     const SceneView sv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ka.objects, nullptr, nullptr,
                        ka.tri_prims, *ka.tri_extent, ka.sub_objects};
-    const uint32_t* entries = tl_entries(ta) + ta.sub_off[t];
-    for (uint32_t base = 0; base < n; base += kTlThreads) {
-        const uint32_t k = base + tid;
-        uint32_t slot = 0u;
-        if (k < n) {
-            slot = entries[k];
-            const size_t ns = ta.n_slots;
-            const float4 a = ta.paths[slot], b = ta.paths[ns + slot];
-            const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
-            TraceState ts;
-            tl_load_best(ta, slot, ts);
-            tl_ray_setup(ka, o, d, ts);
-            uint32_t node = 0u;
-            while (node < nn) {
-                const float4 lo = l_nodes[2u * node], hi = l_nodes[2u * node + 1u];
-                float near_t, far_t;
-                slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
-                const bool hit = near_t <= far_t && far_t >= 0.0f;
-                const uint32_t leaf = __float_as_uint(hi.w);
-                if (hit && leaf == kTlInternal) {
-                    node += 1u;
-                    continue;
-                }
-                if (hit) {
-                    const uint32_t lp = leaf - p0;
-                    const uint4 pr = l_prims[lp];  // object, sub-object, sweep position, range
-                    const RtObject& ob = ka.objects[pr.x];
-                    if (ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) {  // :431
-                        if (pr.w == kPrimRangeNone || (pr.w >> 27) >= kLeafTriSlots) {
-                            tri_leaf<true>(sv, ka, o, d, ts, leaf);  // no triangle block: from global memory
-                        } else {
-                            // the leaf's candidates, as the cooperative leaf batch tests and merges them
-                            const uint32_t cnt = pr.w >> 27, first = pr.w & ((1u << 27) - 1u);
-                            const uint4* blk = l_tris + (size_t)lp * kLeafTriWords;
-                            float cd = __builtin_inff();
-                            uint32_t cs = 0xffffffffu, ct = 0u;
-                            bool cnan = false;
-                            for (uint32_t j = 0; j < cnt; ++j) {
-                                const uint4 q0 = blk[j], q1 = blk[kLeafTriSlots + j], q2 = blk[2u * kLeafTriSlots + j];
-                                const f3 ta_ = mk(__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z));
-                                const f3 cn = mk(__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w));
-                                // the reference's test (:449-481), tri_leaf's operations
-                                const float det = -dot(d, cn);
-                                const float inv_det = 1.0f / det;
-                                const f3 ao = o - ta_;
-                                const float dist = dot(ao, cn) * inv_det;
-                                // (a distance beyond the best hit cannot win; NaN goes on)
-                                if (dist < 0.0f || dist > ts.tri.t) continue;
-                                const f3 ab = mk(__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y));
-                                const f3 ac = mk(__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x));
-                                const f3 dao = cross(ao, d);
-                                const float v = -dot(ab, dao) * inv_det;
-                                if (v < 0.0f) continue;
-                                const float u = dot(ac, dao) * inv_det;
-                                if (u < 0.0f) continue;
-                                const float w = 1.0f - u - v;
-                                if (w < 0.0f) continue;
-                                if (dist != dist) {
-                                    cnan = true;
-                                } else {
-                                    const uint32_t seq = pr.z + j;
-                                    if (dist < cd || (dist == cd && seq < cs)) {
-                                        cd = dist;
-                                        cs = seq;
-                                        ct = min(first + j, ka.triangle_count - 1u) | (det > 0.0f ? 0x80000000u : 0u);
+    const uint32_t* all_entries = tl_entries(ta);
+    uint32_t staged = kTlNone;
+    for (uint32_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const uint4 ch = ta.chunks[c];  // treelet, first entry, rays
+        const uint32_t t = ch.x, n = ch.z;
+        const uint4 st = ta.subtrees[t];  // root (base layout), nodes, first leaf record, leaf records
+        const uint32_t root = st.x, nn = st.y, p0 = st.z, np = st.w;
+        float4* l_nodes = reinterpret_cast<float4*>(lds);
+        uint4* l_prims = reinterpret_cast<uint4*>(lds + (size_t)nn * 32u);
+        uint4* l_tris = l_prims + np;
+        if (t != staged) {
+            __syncthreads();  // the previous chunk's readers are done
+            const float4* g_nodes = ta.base_nodes + 2u * (size_t)root;
+            for (uint32_t k = tid; k < 2u * nn; k += kTlThreads) l_nodes[k] = g_nodes[k];
+            for (uint32_t k = tid; k < np; k += kTlThreads) l_prims[k] = ka.tri_prims[p0 + k];
+            const uint4* g_tris = ka.tri_leaftris + (size_t)p0 * kLeafTriWords;
+            for (uint32_t k = tid; k < np * kLeafTriWords; k += kTlThreads) l_tris[k] = g_tris[k];
+            __syncthreads();
+            staged = t;
+        }
+        const uint32_t* entries = all_entries + ch.y;
+        for (uint32_t base = 0; base < n; base += kTlThreads) {
+            const uint32_t k = base + tid;
+            uint32_t slot = 0u;
+            if (k < n) {
+                slot = entries[k];
+                const size_t ns = ta.n_slots;
+                const float4 a = ta.paths[slot], b = ta.paths[ns + slot];
+                const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
+                TraceState ts;
+                tl_load_best(ta, slot, ts);
+                tl_ray_setup(ka, o, d, ts);
+                uint32_t node = 0u;
+                while (node < nn) {
+                    const float4 lo = l_nodes[2u * node], hi = l_nodes[2u * node + 1u];
+                    float near_t, far_t;
+                    slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+                    const bool hit = near_t <= far_t && far_t >= 0.0f;
+                    const uint32_t leaf = __float_as_uint(hi.w);
+                    if (hit && leaf == kTlInternal) {
+                        node += 1u;
+                        continue;
+                    }
+                    if (hit) {
+                        const uint32_t lp = (leaf & 0xffffffu) - p0;  // (a leaf word: record | count << 24)
+                        const uint4 pr = l_prims[lp];  // object, sub-object, sweep position, range
+                        const RtObject& ob = ka.objects[pr.x];
+                        if (ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) {  // :431
+                            if (pr.w == kPrimRangeNone || (pr.w >> 27) >= kLeafTriSlots) {
+                                tri_leaf<true>(sv, ka, o, d, ts, leaf & 0xffffffu);  // no triangle block: from global memory
+                            } else {
+                                // the leaf's candidates, as the cooperative leaf batch tests and merges them
+                                const uint32_t cnt = pr.w >> 27, first = pr.w & ((1u << 27) - 1u);
+                                const uint4* blk = l_tris + (size_t)lp * kLeafTriWords;
+                                float cd = __builtin_inff();
+                                uint32_t cs = 0xffffffffu, ct = 0u;
+                                bool cnan = false;
+                                for (uint32_t j = 0; j < cnt; ++j) {
+                                    const uint4 q0 = blk[j], q1 = blk[kLeafTriSlots + j], q2 = blk[2u * kLeafTriSlots + j];
+                                    const f3 ta_ = mk(__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z));
+                                    const f3 cn = mk(__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w));
+                                    // the reference's test (:449-481), tri_leaf's operations
+                                    const float det = -dot(d, cn);
+                                    const float inv_det = 1.0f / det;
+                                    const f3 ao = o - ta_;
+                                    const float dist = dot(ao, cn) * inv_det;
+                                    // (a distance beyond the best hit cannot win; NaN goes on)
+                                    if (dist < 0.0f || dist > ts.tri.t) continue;
+                                    const f3 ab = mk(__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y));
+                                    const f3 ac = mk(__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x));
+                                    const f3 dao = cross(ao, d);
+                                    const float v = -dot(ab, dao) * inv_det;
+                                    if (v < 0.0f) continue;
+                                    const float u = dot(ac, dao) * inv_det;
+                                    if (u < 0.0f) continue;
+                                    const float w = 1.0f - u - v;
+                                    if (w < 0.0f) continue;
+                                    if (dist != dist) {
+                                        cnan = true;
+                                    } else {
+                                        const uint32_t seq = pr.z + j;
+                                        if (dist < cd || (dist == cd && seq < cs)) {
+                                            cd = dist;
+                                            cs = seq;
+                                            ct = min(first + j, ka.triangle_count - 1u) | (det > 0.0f ? 0x80000000u : 0u);
+                                        }
                                     }
                                 }
-                            }
-                            const bool beats = cd < ts.tri.t || (cd == ts.tri.t && cs < ts.tri.seq);
-                            if (cnan || beats) {
-                                const RtSubObject so = ka.sub_objects[pr.y];  // :441, when the leaf would change the result
-                                if (ray_in_bounds(o, ts.inv, so.min_bounds, so.max_bounds)) {
-                                    if (cnan) ts.nan_hit = true;
-                                    if (beats) ts.tri = TriHit{cd, cs, ct & 0x7fffffffu, pr.x, (ct >> 31) != 0u};
+                                const bool beats = cd < ts.tri.t || (cd == ts.tri.t && cs < ts.tri.seq);
+                                if (cnan || beats) {
+                                    const RtSubObject so = ka.sub_objects[pr.y];  // :441, when the leaf would change the result
+                                    if (ray_in_bounds(o, ts.inv, so.min_bounds, so.max_bounds)) {
+                                        if (cnan) ts.nan_hit = true;
+                                        if (beats) ts.tri = TriHit{cd, cs, ct & 0x7fffffffu, pr.x, (ct >> 31) != 0u};
+                                    }
                                 }
                             }
                         }
                     }
+                    node = __float_as_uint(lo.w) - root;  // the skip link, local
                 }
-                node = __float_as_uint(lo.w) - root;  // the skip link, local
+                tl_store_best(ta, slot, ts);
             }
-            tl_store_best(ta, slot, ts);
+            tl_append(tl_walk_list(ta, q ^ 1u), ta.ctl + (q ^ 1u), k < n, slot);
         }
-        tl_append(tl_walk_list(ta, q ^ 1u), ta.ctl + (q ^ 1u), k < n, slot);
     }
 }
 
