@@ -1225,6 +1225,8 @@ static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32
     ta.n_slots = (uint32_t)n_slots;
     ta.n_sub = ctx->tl_n_sub;
     const uint32_t grid = 4u * (uint32_t)std::max(1, ctx->n_cu);
+    // the top walk: dependent node loads per lane, so as many resident waves as fit (8 per SIMD)
+    const uint32_t top_grid = 8u * (uint32_t)std::max(1, ctx->n_cu);
     // the treelet walks: as many workgroups as stay resident with their LDS image (5 per CU at 30 KB)
     const uint32_t walk_grid = (uint32_t)std::min<uint64_t>(5u * (uint32_t)std::max(1, ctx->n_cu),
                                                             (uint64_t)ctx->tl_n_sub + n_slots / kTlChunk + 1);
@@ -1239,9 +1241,9 @@ static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32
         if (r >= kMaxRounds) return fail(ctx, RT_E_HIP, "treelet wavefront: paths still running after 4096 rounds");
         ta.round = r;
         if (r > 0) RT_HIP(ctx, rt_launch_tl(1, ka, ta, grid, image, S));
-        RT_HIP(ctx, rt_launch_tl(2, ka, ta, grid, 0, S));
+        RT_HIP(ctx, rt_launch_tl(2, ka, ta, top_grid, 0, S));
         RT_HIP(ctx, rt_launch_tl(3, ka, ta, 1, 0, S));
-        RT_HIP(ctx, rt_launch_tl(4, ka, ta, grid, 0, S));
+        RT_HIP(ctx, rt_launch_tl(4, ka, ta, top_grid, 0, S));
         RT_HIP(ctx, rt_launch_tl(5, ka, ta, walk_grid, tl_lds, S));
         if (r % kCheck == kCheck - 1) {
             RT_HIP(ctx, hipMemcpyAsync(ctx->h_tl_ctl, ctx->d_tl_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, S));

@@ -35,6 +35,8 @@
 namespace {
 
 constexpr uint32_t kTlThreads = 256;
+constexpr uint32_t kTlSteps = 4;  // treelet node steps per leaf-pass check
+constexpr uint32_t kTlTopSteps = 8;  // top-walk node steps per refill check
 
 // The list and counter block of a round (TreeletArgs::lists, ::ctl): walk lists A[2] and shading
 // lists R[2] of slot ids, by round parity, and the treelet entries of the round.
@@ -54,6 +56,29 @@ __device__ __forceinline__ void tl_append(uint32_t* list, uint32_t* count, bool 
     base = __builtin_amdgcn_readlane(base, lead);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     if (want) list[base + rank] = slot;
+}
+
+// A rank in the queue of treelet `target` (kTlNone: none) for every lane: the wave's lanes are
+// grouped by treelet, one atomic per group (its leader's), ranks by mbcnt within the group.
+__device__ __forceinline__ uint32_t tl_enqueue(uint32_t* counts, uint32_t target) {
+    bool pending = target != kTlNone;
+    uint32_t rank = 0u;
+    for (;;) {
+        const uint64_t m = __ballot(pending);
+        if (m == 0) break;
+        const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+        const uint32_t lt = (uint32_t)__builtin_amdgcn_readlane((int)target, (int)lead);
+        const bool mine = pending && target == lt;
+        const uint64_t g = __ballot(mine);
+        uint32_t base = 0u;
+        if ((threadIdx.x & 63u) == lead) base = atomicAdd(counts + lt, (uint32_t)__popcll(g));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
+        if (mine) {
+            rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(g >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)g, 0u));
+            pending = false;
+        }
+    }
+    return rank;
 }
 
 // A slot's pixel: slot = (frame * samples + sample) * owned_px + local pixel (frame_light's indexing).
@@ -196,60 +221,75 @@ __global__ void __launch_bounds__(kTlThreads) rt_tl_shade_kernel(KernelArgs ka, 
 // it enters a treelet (queued there, counted in sub_cnt) or its walk is over (queued for shading
 // next round: R[q ^ 1]). Leaves above the cut are tested on the spot.
 __global__ void __launch_bounds__(kTlThreads) rt_tl_top_kernel(KernelArgs ka, TreeletArgs ta) {
+    __shared__ uint32_t s_next;
     const uint32_t q = ta.round & 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) ta.ctl[2u + q] = 0u;  // R[q] was shaded (the previous kernel)
     const uint32_t count = ta.ctl[q];
-    if (blockIdx.x * kTlThreads >= count) return;
+    // the block's share of A[q]; each lane takes the share's next ray when its walk stops
+    const uint32_t per = (count + gridDim.x - 1u) / gridDim.x;
+    const uint32_t lo = min(count, blockIdx.x * per), hi = min(count, lo + per);
+    if (lo >= hi) return;
+    if (threadIdx.x == 0) s_next = lo;
+    __syncthreads();
     const SceneView sv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ka.objects, nullptr, nullptr,
                        ka.tri_prims, *ka.tri_extent, ka.sub_objects};
     const uint32_t* in = tl_walk_list(ta, q);
-    for (uint32_t base = blockIdx.x * kTlThreads; base < count; base += gridDim.x * kTlThreads) {
-        const uint32_t i = base + threadIdx.x;
-        bool finished = false;
-        uint32_t slot = 0u;
-        if (i < count) {
-            slot = in[i];
-            const size_t n = ta.n_slots;
-            const float4 a = ta.paths[slot], b = ta.paths[n + slot];
-            const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
-            TraceState ts;
-            tl_load_best(ta, slot, ts);
-            tl_ray_setup(ka, o, d, ts);
-            uint32_t pos = ta.walk[n + slot].x;
-            uint32_t target = kTlNone;
-            while (pos < kTlEnd) {
-                const float4 lo = ta.top[2u * pos], hi = ta.top[2u * pos + 1u];
-                float near_t, far_t;
-                slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
-                const bool hit = near_t <= far_t && far_t >= 0.0f;
-                const uint32_t leaf = __float_as_uint(hi.w);
-                if (hit && leaf == kTlInternal) {
-                    pos += 1u;
-                    continue;
-                }
-                const uint32_t skip = __float_as_uint(lo.w);
-                if (hit && (leaf & kTlTreelet)) {
-                    target = leaf & ~kTlTreelet;
-                    pos = skip;
-                    break;
-                }
-                if (hit) tri_leaf<true>(sv, ka, o, d, ts, leaf & 0xffffffu);  // a leaf above the cut (its record index)
-                pos = skip;
+    const size_t n = ta.n_slots;
+    uint32_t slot = 0u, pos = kTlEnd, target = kTlNone;
+    bool live = false;
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = o;
+    TraceState ts;
+    for (;;) {
+        const uint64_t idle = __ballot(!live);
+        if (idle != 0u) {
+            const uint32_t lead = (uint32_t)__builtin_ctzll(idle);
+            uint32_t b0 = 0u;
+            if ((threadIdx.x & 63u) == lead) b0 = atomicAdd(&s_next, (uint32_t)__popcll(idle));
+            b0 = (uint32_t)__builtin_amdgcn_readlane((int)b0, (int)lead);
+            const uint32_t k = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            if (!live && k < hi) {
+                slot = in[k];
+                const float4 a = ta.paths[slot], b = ta.paths[n + slot];
+                o = mk(a.x, a.y, a.z);
+                d = mk(b.x, b.y, b.z);
+                tl_load_best(ta, slot, ts);
+                tl_ray_setup(ka, o, d, ts);
+                pos = ta.walk[n + slot].x;
+                target = kTlNone;
+                live = true;
             }
-            if (target != kTlNone) {
-                const uint32_t rank = atomicAdd(ta.sub_cnt + target, 1u);
-                ta.walk[n + slot] = make_uint4(pos, target, rank, 0u);
-            } else {
-                if (ts.nan_hit) {  // measure-zero case: the sweep decides
-                    ts.tri = sweep_triangles(sv, ka, o, d);
-                    ts.nan_hit = false;
-                }
-                ta.walk[n + slot] = make_uint4(kTlEnd, kTlNone, 0u, 0u);
-                finished = true;
+        }
+        if (__ballot(live) == 0u) break;
+        for (uint32_t step = 0; step < kTlTopSteps && live && target == kTlNone && pos < kTlEnd; ++step) {
+            const float4 blo = ta.top[2u * pos], bhi = ta.top[2u * pos + 1u];
+            float near_t, far_t;
+            slab_hit(ts.slab, blo.x, blo.y, blo.z, bhi.x, bhi.y, bhi.z, near_t, far_t);
+            const bool hit = near_t <= far_t && far_t >= 0.0f;
+            const uint32_t leaf = __float_as_uint(bhi.w);
+            if (hit && leaf == kTlInternal) {
+                pos += 1u;
+                continue;
             }
+            if (hit && (leaf & kTlTreelet)) target = leaf & ~kTlTreelet;
+            else if (hit) tri_leaf<true>(sv, ka, o, d, ts, leaf & 0xffffffu);  // a leaf above the cut (its record index)
+            pos = __float_as_uint(blo.w);
+        }
+        const bool stop = live && (target != kTlNone || pos >= kTlEnd);
+        const bool finished = stop && target == kTlNone;
+        if (finished && ts.nan_hit) {  // measure-zero case: the sweep decides
+            ts.tri = sweep_triangles(sv, ka, o, d);
+            ts.nan_hit = false;
+        }
+        // queue ranks: one atomic per distinct treelet of the wave (coherent rays enter the same
+        // treelets; an atomic per ray serialises on the hot ones)
+        const uint32_t rank = tl_enqueue(ta.sub_cnt, stop ? target : kTlNone);
+        if (stop) {
             tl_store_best(ta, slot, ts);
+            ta.walk[n + slot] = finished ? make_uint4(kTlEnd, kTlNone, 0u, 0u) : make_uint4(pos, target, rank, 0u);
         }
         tl_append(tl_shade_list(ta, q ^ 1u), ta.ctl + 2u + (q ^ 1u), finished, slot);
+        if (stop) live = false;
     }
 }
 
@@ -302,17 +342,74 @@ __global__ void __launch_bounds__(kTlThreads) rt_tl_scatter_kernel(TreeletArgs t
     }
 }
 
+// One leaf of a treelet from LDS: the object box (:431), the leaf's candidates as the
+// cooperative leaf batch tests and merges them (tri_leaf's operations, :449-481), and the
+// sub-object box (:441) only when a candidate would change the result.
+__device__ __forceinline__ void tl_leaf_lds(const SceneView& sv, const KernelArgs& ka, f3 o, f3 d, TraceState& ts,
+                                            const uint4 pr, const uint4* blk, uint32_t record) {
+    const RtObject& ob = ka.objects[pr.x];  // object, sub-object, sweep position, range
+    if (!ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) return;
+    if (pr.w == kPrimRangeNone || (pr.w >> 27) >= kLeafTriSlots) {
+        tri_leaf<true>(sv, ka, o, d, ts, record);  // no triangle block: from global memory
+        return;
+    }
+    const uint32_t cnt = pr.w >> 27, first = pr.w & ((1u << 27) - 1u);
+    float cd = __builtin_inff();
+    uint32_t cs = 0xffffffffu, ct = 0u;
+    bool cnan = false;
+    for (uint32_t j = 0; j < cnt; ++j) {
+        const uint4 q0 = blk[j], q1 = blk[kLeafTriSlots + j], q2 = blk[2u * kLeafTriSlots + j];
+        const f3 ta_ = mk(__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z));
+        const f3 cn = mk(__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w));
+        const float det = -dot(d, cn);
+        const float inv_det = 1.0f / det;
+        const f3 ao = o - ta_;
+        const float dist = dot(ao, cn) * inv_det;
+        // (a distance beyond the best hit cannot win; NaN goes on)
+        if (dist < 0.0f || dist > ts.tri.t) continue;
+        const f3 ab = mk(__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y));
+        const f3 ac = mk(__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x));
+        const f3 dao = cross(ao, d);
+        const float v = -dot(ab, dao) * inv_det;
+        if (v < 0.0f) continue;
+        const float u = dot(ac, dao) * inv_det;
+        if (u < 0.0f) continue;
+        const float w = 1.0f - u - v;
+        if (w < 0.0f) continue;
+        if (dist != dist) {
+            cnan = true;
+        } else {
+            const uint32_t seq = pr.z + j;
+            if (dist < cd || (dist == cd && seq < cs)) {
+                cd = dist;
+                cs = seq;
+                ct = min(first + j, ka.triangle_count - 1u) | (det > 0.0f ? 0x80000000u : 0u);
+            }
+        }
+    }
+    const bool beats = cd < ts.tri.t || (cd == ts.tri.t && cs < ts.tri.seq);
+    if (cnan || beats) {
+        const RtSubObject so = ka.sub_objects[pr.y];
+        if (ray_in_bounds(o, ts.inv, so.min_bounds, so.max_bounds)) {
+            if (cnan) ts.nan_hit = true;
+            if (beats) ts.tri = TriHit{cd, cs, ct & 0x7fffffffu, pr.x, (ct >> 31) != 0u};
+        }
+    }
+}
+
 // The treelet walks, a chunk of a treelet's queue per workgroup step: the treelet's nodes (the
 // base layout's pre-order range), leaf records and leaf triangle blocks staged in LDS, then the
 // chunk's rays walked from there; the rays go back to the top walk (A[q ^ 1]).
 __global__ void __launch_bounds__(kTlThreads) rt_tl_subtree_kernel(KernelArgs ka, TreeletArgs ta) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t s_next, s_out;
     const uint32_t tid = threadIdx.x, q = ta.round & 1u;
     if (blockIdx.x == 0 && tid == 0) ta.ctl[q] = 0u;  // A[q] was walked and scattered (the previous kernels)
     const uint32_t n_chunks = ta.ctl[4];
     const SceneView sv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ka.objects, nullptr, nullptr,
                        ka.tri_prims, *ka.tri_extent, ka.sub_objects};
     const uint32_t* all_entries = tl_entries(ta);
+    uint32_t* out_list = tl_walk_list(ta, q ^ 1u);
     uint32_t staged = kTlNone;
     for (uint32_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
         const uint4 ch = ta.chunks[c];  // treelet, first entry, rays
@@ -322,100 +419,78 @@ __global__ void __launch_bounds__(kTlThreads) rt_tl_subtree_kernel(KernelArgs ka
         float4* l_nodes = reinterpret_cast<float4*>(lds);
         uint4* l_prims = reinterpret_cast<uint4*>(lds + (size_t)nn * 32u);
         uint4* l_tris = l_prims + np;
+        __syncthreads();  // the previous chunk's readers are done (LDS image, s_next, s_out)
         if (t != staged) {
-            __syncthreads();  // the previous chunk's readers are done
             const float4* g_nodes = ta.base_nodes + 2u * (size_t)root;
             for (uint32_t k = tid; k < 2u * nn; k += kTlThreads) l_nodes[k] = g_nodes[k];
             for (uint32_t k = tid; k < np; k += kTlThreads) l_prims[k] = ka.tri_prims[p0 + k];
             const uint4* g_tris = ka.tri_leaftris + (size_t)p0 * kLeafTriWords;
             for (uint32_t k = tid; k < np * kLeafTriWords; k += kTlThreads) l_tris[k] = g_tris[k];
-            __syncthreads();
             staged = t;
         }
+        // every ray of the chunk goes back to the top walk: one append for the chunk
+        if (tid == 0) {
+            s_next = 0u;
+            s_out = atomicAdd(ta.ctl + (q ^ 1u), n);
+        }
+        __syncthreads();
         const uint32_t* entries = all_entries + ch.y;
-        for (uint32_t base = 0; base < n; base += kTlThreads) {
-            const uint32_t k = base + tid;
-            uint32_t slot = 0u;
-            if (k < n) {
-                slot = entries[k];
-                const size_t ns = ta.n_slots;
-                const float4 a = ta.paths[slot], b = ta.paths[ns + slot];
-                const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
-                TraceState ts;
-                tl_load_best(ta, slot, ts);
-                tl_ray_setup(ka, o, d, ts);
-                uint32_t node = 0u;
-                while (node < nn) {
-                    const float4 lo = l_nodes[2u * node], hi = l_nodes[2u * node + 1u];
-                    float near_t, far_t;
-                    slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
-                    const bool hit = near_t <= far_t && far_t >= 0.0f;
-                    const uint32_t leaf = __float_as_uint(hi.w);
-                    if (hit && leaf == kTlInternal) {
-                        node += 1u;
-                        continue;
-                    }
-                    if (hit) {
-                        const uint32_t lp = (leaf & 0xffffffu) - p0;  // (a leaf word: record | count << 24)
-                        const uint4 pr = l_prims[lp];  // object, sub-object, sweep position, range
-                        const RtObject& ob = ka.objects[pr.x];
-                        if (ray_in_bounds(o, ts.inv, ob.min_bounds, ob.max_bounds)) {  // :431
-                            if (pr.w == kPrimRangeNone || (pr.w >> 27) >= kLeafTriSlots) {
-                                tri_leaf<true>(sv, ka, o, d, ts, leaf & 0xffffffu);  // no triangle block: from global memory
-                            } else {
-                                // the leaf's candidates, as the cooperative leaf batch tests and merges them
-                                const uint32_t cnt = pr.w >> 27, first = pr.w & ((1u << 27) - 1u);
-                                const uint4* blk = l_tris + (size_t)lp * kLeafTriWords;
-                                float cd = __builtin_inff();
-                                uint32_t cs = 0xffffffffu, ct = 0u;
-                                bool cnan = false;
-                                for (uint32_t j = 0; j < cnt; ++j) {
-                                    const uint4 q0 = blk[j], q1 = blk[kLeafTriSlots + j], q2 = blk[2u * kLeafTriSlots + j];
-                                    const f3 ta_ = mk(__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z));
-                                    const f3 cn = mk(__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w));
-                                    // the reference's test (:449-481), tri_leaf's operations
-                                    const float det = -dot(d, cn);
-                                    const float inv_det = 1.0f / det;
-                                    const f3 ao = o - ta_;
-                                    const float dist = dot(ao, cn) * inv_det;
-                                    // (a distance beyond the best hit cannot win; NaN goes on)
-                                    if (dist < 0.0f || dist > ts.tri.t) continue;
-                                    const f3 ab = mk(__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y));
-                                    const f3 ac = mk(__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x));
-                                    const f3 dao = cross(ao, d);
-                                    const float v = -dot(ab, dao) * inv_det;
-                                    if (v < 0.0f) continue;
-                                    const float u = dot(ac, dao) * inv_det;
-                                    if (u < 0.0f) continue;
-                                    const float w = 1.0f - u - v;
-                                    if (w < 0.0f) continue;
-                                    if (dist != dist) {
-                                        cnan = true;
-                                    } else {
-                                        const uint32_t seq = pr.z + j;
-                                        if (dist < cd || (dist == cd && seq < cs)) {
-                                            cd = dist;
-                                            cs = seq;
-                                            ct = min(first + j, ka.triangle_count - 1u) | (det > 0.0f ? 0x80000000u : 0u);
-                                        }
-                                    }
-                                }
-                                const bool beats = cd < ts.tri.t || (cd == ts.tri.t && cs < ts.tri.seq);
-                                if (cnan || beats) {
-                                    const RtSubObject so = ka.sub_objects[pr.y];  // :441, when the leaf would change the result
-                                    if (ray_in_bounds(o, ts.inv, so.min_bounds, so.max_bounds)) {
-                                        if (cnan) ts.nan_hit = true;
-                                        if (beats) ts.tri = TriHit{cd, cs, ct & 0x7fffffffu, pr.x, (ct >> 31) != 0u};
-                                    }
-                                }
-                            }
-                        }
-                    }
-                    node = __float_as_uint(lo.w) - root;  // the skip link, local
+        for (uint32_t k = tid; k < n; k += kTlThreads) out_list[s_out + k] = entries[k];
+        // Each lane walks one ray at a time and takes the chunk's next ray when it is done
+        // (claims by wave, from an LDS counter). Up to kTlSteps node steps per check; a lane that
+        // reaches a leaf waits with it, and the waiting lanes' leaves are tested together once
+        // they are at least as many as the walking lanes. The walk culls by box only, so the
+        // leaves' order does not matter (lexicographic minimum).
+        uint32_t slot = 0u, node = nn, pend = kTlNone;
+        bool live = false;
+        f3 o = mk(0.0f, 0.0f, 0.0f), d = o;
+        TraceState ts;
+        for (;;) {
+            const uint64_t idle = __ballot(!live);
+            if (idle != 0u) {
+                const uint32_t lead = (uint32_t)__builtin_ctzll(idle);
+                uint32_t b0 = 0u;
+                if ((tid & 63u) == lead) b0 = atomicAdd(&s_next, (uint32_t)__popcll(idle));
+                b0 = (uint32_t)__builtin_amdgcn_readlane((int)b0, (int)lead);
+                const uint32_t k = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (!live && k < n) {
+                    slot = entries[k];
+                    const size_t ns = ta.n_slots;
+                    const float4 a = ta.paths[slot], b = ta.paths[ns + slot];
+                    o = mk(a.x, a.y, a.z);
+                    d = mk(b.x, b.y, b.z);
+                    tl_load_best(ta, slot, ts);
+                    tl_ray_setup(ka, o, d, ts);
+                    node = 0u;
+                    pend = kTlNone;
+                    live = true;
                 }
-                tl_store_best(ta, slot, ts);
             }
-            tl_append(tl_walk_list(ta, q ^ 1u), ta.ctl + (q ^ 1u), k < n, slot);
+            if (__ballot(live) == 0u) break;
+            for (uint32_t step = 0; step < kTlSteps && live && pend == kTlNone && node < nn; ++step) {
+                const float4 lo = l_nodes[2u * node], hi = l_nodes[2u * node + 1u];
+                float near_t, far_t;
+                slab_hit(ts.slab, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, near_t, far_t);
+                const bool hit = near_t <= far_t && far_t >= 0.0f;
+                const uint32_t leaf = __float_as_uint(hi.w);
+                if (hit && leaf == kTlInternal) {
+                    node += 1u;
+                    continue;
+                }
+                if (hit) pend = (leaf & 0xffffffu) - p0;  // (a leaf word: record | count << 24)
+                node = __float_as_uint(lo.w) - root;      // the skip link, local
+            }
+            const uint64_t waiting = __ballot(pend != kTlNone);
+            const uint64_t walking = __ballot(live && pend == kTlNone && node < nn);
+            if (waiting != 0u && (walking == 0u || __popcll(waiting) >= __popcll(walking)) && pend != kTlNone) {
+                tl_leaf_lds(sv, ka, o, d, ts, l_prims[pend], l_tris + (size_t)pend * kLeafTriWords, p0 + pend);
+                pend = kTlNone;
+            }
+            if (live && pend == kTlNone && node >= nn) {  // left the treelet: its best hit so far
+                tl_store_best(ta, slot, ts);
+                live = false;
+            }
         }
     }
 }

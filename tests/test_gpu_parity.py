@@ -539,8 +539,8 @@ def test_gpu_triangle_pruning(gpu, oracle_lib, prune, octants, primary):
 def test_gpu_environment_has_no_effect(gpu, oracle_lib, monkeypatch):
     """The library reads no environment (ABI 12): with the round-1..5 switches set
     -- among them RT_TRI_PRUNE=2, the inexact pruning, and RT_BRUTE_FORCE=1 -- a default context
-    launches the default kernels and renders the oracle's bits on the grazing-ray scene where
-    the inexact mode differs from the sweep."""
+    on a small C5 heightfield launches the default kernels (the path kernel and the primary
+    pre-pass, scene in LDS mode 1) and renders the oracle's bits."""
     for k, v in {"RT_TRI_PRUNE": "2", "RT_BRUTE_FORCE": "1", "RT_LDS_MODE": "0", "RT_PRIMARY_PASS": "0",
                  "RT_FRAME_BATCH": "1", "RT_TRI_OCTANTS": "0", "RT_COOP_LEAVES": "0", "RT_TRI_BVH": "0"}.items():
         monkeypatch.setenv(k, v)
@@ -582,7 +582,7 @@ def test_gpu_tuning_keys_refuse_bad_input(gpu):
     ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 1, {}),
     ("c5_heightfield", dict(nx=200, nz=100), 2, 3, 1, {}),
     ("c5_heightfield", dict(nx=200, nz=100), 1, 4, 3, {}),  # tile split
-    ("c5_heightfield", dict(nx=60, nz=30), 1, 2, 1, {"primary_tile_major": 0}),
+    ("c5_heightfield", dict(nx=60, nz=30), 1, 2, 1, {"primary_tile_major": 0, "lds_mode": 1}),  # (fits LDS otherwise)
     ("c3_chess", dict(env_size=(512, 256)), 1, 3, 1, {"lds_mode": 1}),  # a mesh scene walked from global memory
     ("c5_heightfield", dict(nx=200, nz=100), 1, 5, 1, {"batch_memory_mb": 1}),  # a batch split over launches
 ])

@@ -44,6 +44,38 @@ case "$T" in
     timeout -k 10 300 python3 bench.py --config c5_heightfield --tune treelet_walk=1 --no-cpu-baseline --no-cadences > gpurun_out/$T/bench_c5_tl.json 2> gpurun_out/$T/bench_c5_tl.err || exit 1
     timeout -k 10 300 python3 bench.py --config c5_heightfield --no-cpu-baseline --no-cadences > gpurun_out/$T/bench_c5.json 2> gpurun_out/$T/bench_c5.err || exit 1
     ;;
+  r06e)
+    # where the treelet wavefront's time goes on C5: kernel trace of the bench (per-kernel stats;
+    # the count of rt_tl_top_kernel launches is the number of rounds)
+    export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/trace -o run -- python3 bench.py --config c5_heightfield --tune treelet_walk=1 --steps 20 --warmup 20 --settle-ms 0 --no-cpu-baseline --no-cadences > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace.err || exit 1
+    ;;
+  r06f)
+    # the treelet wavefront's kernels under SQ counters (one 4-frame C5 batch per pass)
+    export TMPDIR=/tmp
+    B="bench.py --config c5_heightfield --tune treelet_walk=1 --steps 4 --warmup 0 --settle-ms 0 --no-cpu-baseline --no-cadences"
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY --output-format csv -d gpurun_out/$T/pmc_a -o run -- python3 $B > gpurun_out/$T/a.json 2> gpurun_out/$T/a.err || exit 1
+    timeout -s KILL 120 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/$T/pmc_b -o run -- python3 $B > gpurun_out/$T/b.json 2> gpurun_out/$T/b.err || exit 1
+    ;;
+  r06z|r06y)
+    # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
+    # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
+    timeout -k 10 900 python3 -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    timeout -k 10 600 python3 -c "
+import subprocess, pathlib
+from rust_gpu_raytracing_amd import build as b
+subprocess.run(b.hipcc_command(pathlib.Path('/tmp/librt_srcbuild.so')), check=True)
+print('built /tmp/librt_srcbuild.so, sources', b.source_hash())" > gpurun_out/$T/srcbuild.log 2>&1 || exit 1
+    RT_LIB=/tmp/librt_srcbuild.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k "golden or full_frame_baseline_size" >> gpurun_out/$T/srcbuild.log 2>&1 || exit 1
+    RT_LIB=/tmp/librt_srcbuild.so timeout -k 10 100 python3 -c "
+from rust_gpu_raytracing_amd import _native as N, build as b
+lib = N.load_library()
+print('srcbuild library hash', lib.rt_build_hash().decode(), '== tree', b.source_hash())" >> gpurun_out/$T/srcbuild.log 2>&1 || exit 1
+    timeout -k 10 600 python3 tools/bench_all.py --frames 20 > gpurun_out/$T/bench_all.jsonl 2> gpurun_out/$T/bench_all.err || exit 1
+    timeout -k 10 300 python3 tools/strong_probe.py --steps 20 > gpurun_out/$T/strong_probe.jsonl 2> gpurun_out/$T/strong_probe.err || exit 1
+    ;;
   *)
     echo "unknown tag $T"; exit 2
     ;;
