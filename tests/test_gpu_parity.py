@@ -432,6 +432,26 @@ def test_gpu_sub_objects_in_lds(gpu, oracle_lib, stage):
     assert_same(acc, out, n, acc_o, out_o, n_o)
 
 
+def test_gpu_default_batch_at_4k_with_many_samples(gpu):
+    """the default frame batch (RT_DEFAULT_FRAME_BATCH) sizes its light
+    buffer per batch -- 3840x2160 at 24 samples per frame is 16 x 24 x 8.3 M x 16 B = 51 GB for
+    one 16-frame batch, more than the context's budget (an eighth of the device's memory), so
+    the library renders it as consecutive launches. The default context renders 16 frames
+    bit-identical to single-frame launches."""
+    scene, bounces = build_config("c2_rtiow", width=3840, height=2160)
+    rays = scene.camera.recalculate_ray_directions()
+    res = []
+    for fb in (None, 1):
+        with Renderer(scene, camera_rays=rays, compute_per_frame=24, frame_batch=fb) as r:
+            if fb is None:
+                assert r.frame_batch()[0] == N.RT_DEFAULT_FRAME_BATCH
+            r.submit_frames(bounces, 16)
+            r.synchronize()
+            res.append((r.read_accumulation(), r.read_output(), r.ray_count()))
+    (a0, o0, n0), (a1, o1, n1) = res
+    assert n0 == n1 and np.array_equal(o0, o1) and np.array_equal(a0.view(np.uint32), a1.view(np.uint32))
+
+
 def test_gpu_default_batching_and_device_display_copy(gpu, oracle_lib):
     """ABI 11: by default rt_compute_frame queues its frame (RT_DEFAULT_FRAME_BATCH) and the
     next observation launches the queue. The reference's loop -- one compute_frame per frame,
