@@ -57,6 +57,16 @@ case "$T" in
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY --output-format csv -d gpurun_out/$T/pmc_a -o run -- python3 $B > gpurun_out/$T/a.json 2> gpurun_out/$T/a.err || exit 1
     timeout -s KILL 120 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/$T/pmc_b -o run -- python3 $B > gpurun_out/$T/b.json 2> gpurun_out/$T/b.err || exit 1
     ;;
+  r06g)
+    # first hardware pass of the ABI-12 build and the treelet wavefront: every GPU test, smoke,
+    # the headline bench, C5 persistent walk vs treelet wavefront, both brute-force lines
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    timeout -k 10 300 python3 tools/ab_env.py "" "treelet_walk=1" --config c5_heightfield --frame-batch 20 --frames 40 --rounds 3 > gpurun_out/$T/ab_c5.jsonl 2> gpurun_out/$T/ab_c5.err || exit 1
+    timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_tiled.json 2> gpurun_out/$T/brute_tiled.err || exit 1
+    timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force stream --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_stream.json 2> gpurun_out/$T/brute_stream.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
