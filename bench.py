@@ -599,7 +599,13 @@ def main() -> int:
                 "bytes_per_launch": b_launch,
                 "tile_stream_bytes_per_launch": stream_launch,
                 "l2_stream_bytes_per_launch": stream_l2_launch,
-                "note": ("the reference's sweeps: VALU-bound on sub-object box tests (DESIGN §5.5)"
+                "note": ("the reference's sweeps: VALU-bound on sub-object box tests (DESIGN §5.5). "
+                         "bytes_per_launch carries SURVEY §8d's tile-streaming term, the sub-object "
+                         "records (32 B each) delivered once per started 256-ray tile of every bounce "
+                         "level: a fixed convention for bytes moved to the CUs, which the L2 and MALL "
+                         "serve (the whole record array is a few MB), so it exceeds the HBM traffic the "
+                         "PMC counters see (`traffic`); l2_stream_bytes_per_launch is what the kernel's "
+                         "own tiles (mode 1) or waves (mode 2) actually read from L2"
                          if args.brute_force else
                          "branchy f32 VALU-bound path (SURVEY §7); HBM fraction is low by construction"),
                 "valu": pmc_issue(pmc),

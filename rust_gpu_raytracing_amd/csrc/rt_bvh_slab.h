@@ -35,6 +35,17 @@ struct SlabRay {
 
 RT_SLAB_FN float slab_cap_inv(float v) { return fabsf(v) > 1e30f ? copysignf(1e30f, v) : v; }
 
+// v where keep, else +inf: a bitwise merge, so the compiler cannot branch around v's arithmetic.
+RT_SLAB_FN float keep_or_inf(float v, bool keep) {
+    const unsigned m = 0u - (unsigned)keep;
+    unsigned b;
+    __builtin_memcpy(&b, &v, 4);
+    b = (b & m) | (0x7f800000u & ~m);
+    float r;
+    __builtin_memcpy(&r, &b, 4);
+    return r;
+}
+
 // Upper bounds for quantities that only size the margins (bigger = more
 // conservative): 1/x and sqrt(x) from the hardware approximations (<= 1 ulp)
 // rounded up by 1.000001 (~8.4u), on the host from the IEEE results.
@@ -125,12 +136,13 @@ RT_SLAB_FN void sphere_cull_bounds(float olen, float extent, float r_min, float 
     const float X = (olen + extent) * 1.0000005f;
     const float quad = r_min > 0.0f ? ((40.0f * u) * (X * X)) * rcp_up(r_min) : INFINITY;  // >= 3 x 13.25u X^2 / r_min
     const float lin = 4.4e-3f * X;                                               // >= 2.5 x 7 sqrt(u) X
-    // |d|^2 < 2^-60 (or not finite): outside the bound's range, no culling. Selected, not
-    // branched on: a branch here, on the ray setup of every segment, cost the sphere walk
-    // 1.4% (round 6 bisect, profiles/r06/r06a)
+    // |d|^2 < 2^-60 (or not finite): outside the bound's range, no culling. Merged by bit mask,
+    // not by a select: the compiler turns `in_range ? expr : INFINITY` into a branch around the
+    // expression, and that branch on the ray setup of every segment cost the sphere walk 1.4%
+    // (round 6 bisect, profiles/r06/r06a, r06h)
     const bool in_range = inv_dlen <= 0x1p30f;
-    lateral = in_range ? fminf(quad, lin) + (16.0f * u) * X + (16.0f * u) * r_max + 1.0e-6f : INFINITY;
-    slack = in_range ? (4.4e-3f * (X + r_max) + (32.0f * u) * X) * (inv_dlen * 1.01f) + 1.0e-30f : INFINITY;
+    lateral = keep_or_inf(fminf(quad, lin) + (16.0f * u) * X + (16.0f * u) * r_max + 1.0e-6f, in_range);
+    slack = keep_or_inf((4.4e-3f * (X + r_max) + (32.0f * u) * X) * (inv_dlen * 1.01f) + 1.0e-30f, in_range);
 }
 
 // near/far parameters of the inflated box [lo, hi] (min/max ignore NaN operands).

@@ -67,6 +67,25 @@ case "$T" in
     timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_tiled.json 2> gpurun_out/$T/brute_tiled.err || exit 1
     timeout -k 10 200 python3 bench.py --config c5_heightfield --brute-force stream --steps 2 --warmup 1 --no-cpu-baseline --no-cadences > gpurun_out/$T/brute_stream.json 2> gpurun_out/$T/brute_stream.err || exit 1
     ;;
+  r06h)
+    # the ABI-12 head against the round-4 final (fcb6cf7) and round-5 head (797545e) kernels in one
+    # process (abship/, tools/build_at_commit.py), then the treelet wavefront's kernel trace on C5
+    L="rust_gpu_raytracing_amd/librt_pathtrace.so abship/lib_fcb6cf7.so abship/lib_797545e.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 5 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/trace -o run -- python3 bench.py --config c5_heightfield --tune treelet_walk=1 --steps 20 --warmup 20 --settle-ms 0 --no-cpu-baseline --no-cadences > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace.err || exit 1
+    ;;
+  r06i)
+    # the culling bound's range check as a bit-mask merge (no branch) against the round-4 final
+    # and round-5 head kernels, C2/C3/C5 in one process
+    L="rust_gpu_raytracing_amd/librt_pathtrace.so abship/lib_fcb6cf7.so abship/lib_797545e.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 5 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-cadences > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
