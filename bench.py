@@ -58,8 +58,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # 16 lanes x 2.4 GHz (a wave64 instruction issues over 4 cycles of a SIMD16)
 VALU_LANE_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 KERNEL_NAMES = {"path": "rt_pathtrace_kernel", "primary": "rt_primary_kernel", "resolve": "rt_resolve_frames_kernel",
-                "brute": "rt_brute_wf_kernel", "brute_stream": "(its records through the scalar cache)",
-                "treelet": "rt_tl_* (the treelet wavefront)"}
+                "brute": "rt_brute_wf_kernel", "brute_stream": "(its records through the scalar cache)"}
 # The reference computes a frame every >= 0.8 ms and displays every >= 5 ms
 # (src/main.rs:88-92, 365-375): about 6 computed frames per displayed image.
 DISPLAY_CADENCE_FRAMES = 6

@@ -362,8 +362,7 @@ RT_API int rt_set_triangle_pruning(rt_ctx* ctx, int mode);
  *   "sphere_octants" 1|0, "sphere_box_order" 1|0, "tri_bvh" 1|0 (0: the reference's sweep),
  *   "tri_octants" 1|0, "tri_qnodes" 1|0, "coop_leaves" 1|0, "stage_subs" 1|0,
  *   "primary_pass" -1|0|1 (-1: by scene), "primary_threads" 256|64|128|512|1024,
- *   "primary_waves" 8|0, "primary_tile_major" 1|0, "treelet_walk" -1|0|1 (the treelet wavefront
- *   for scenes whose triangle accelerator is walked from global memory; -1: by scene).
+ *   "primary_waves" 8|0, "primary_tile_major" 1|0.
  * RT_E_INVALID for an unknown key or a value out of range. */
 RT_API int rt_set_tuning(rt_ctx* ctx, const char* key, int32_t value);
 
@@ -444,14 +443,13 @@ RT_API int rt_launch_config(rt_ctx* ctx, uint32_t* threads, uint32_t* blocks, ui
 /* The kernels the last rt_dispatch ran (diagnostics, ABI 7), a mask of RT_PASS_*:
  * the path kernel, the coherent primary-ray pre-pass, the batch resolve pass, or the
  * brute-force sweep kernel instead of the path kernel (with RT_PASS_BRUTE_STREAM, ABI 12:
- * its scalar-cache variant, rt_set_brute_force mode 2), or the treelet wavefront instead of the
- * path kernel (RT_PASS_TREELET, ABI 12: tuning "treelet_walk"). */
+ * its scalar-cache variant, rt_set_brute_force mode 2). Bit 32 (RT_PASS_TREELET, an ABI-12
+ * treelet wavefront measured 2.9x slower than the path kernel on C5 and removed) is not set. */
 #define RT_PASS_PATH 1u
 #define RT_PASS_PRIMARY 2u
 #define RT_PASS_RESOLVE 4u
 #define RT_PASS_BRUTE 8u
 #define RT_PASS_BRUTE_STREAM 16u
-#define RT_PASS_TREELET 32u
 RT_API int rt_last_launch_passes(rt_ctx* ctx, uint32_t* passes);
 
 /* Diagnostic counters (filled only by builds compiled with -DRT_DIAG or

@@ -188,7 +188,7 @@ SIGNATURES = {
 }
 
 RT_DEFAULT_FRAME_BATCH = 16  # include/rt_abi.h (ABI 11)
-RT_PASS_PATH, RT_PASS_PRIMARY, RT_PASS_RESOLVE, RT_PASS_BRUTE, RT_PASS_BRUTE_STREAM, RT_PASS_TREELET = 1, 2, 4, 8, 16, 32
+RT_PASS_PATH, RT_PASS_PRIMARY, RT_PASS_RESOLVE, RT_PASS_BRUTE, RT_PASS_BRUTE_STREAM = 1, 2, 4, 8, 16
 RT_GROUP_COPY_TRANSPORT = 1  # rt_create_multi_ex flags
 RT_GATHER_IMAGE = 0
 RT_GATHER_ACCUMULATION = 1

@@ -21,10 +21,10 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 OUT = PKG / "librt_pathtrace.so"
 SOURCES = [CSRC / "pathtrace.hip", CSRC / "scene_edit.hip", CSRC / "rt_abi.cpp", CSRC / "sphere_bvh.cpp",
-           CSRC / "scene_build.cpp", CSRC / "rt_multi.cpp", CSRC / "treelet.hip"]
+           CSRC / "scene_build.cpp", CSRC / "rt_multi.cpp"]
 HEADERS = [CSRC / "rt_bvh_slab.h", CSRC / "rt_device_math.h", CSRC / "rt_kernel_args.h", CSRC / "sphere_bvh.h",
            CSRC / "rt_scene_math.h", CSRC / "tri_qnode.h", CSRC / "tri_cone.h", CSRC / "rt_path_common.h",
-           CSRC / "rt_treelet.h", INCLUDE / "rt_abi.h"]
+           INCLUDE / "rt_abi.h"]
 
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

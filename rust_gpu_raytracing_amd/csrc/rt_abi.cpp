@@ -24,7 +24,6 @@
 #include "sphere_bvh.h"
 #include "tri_cone.h"
 #include "tri_qnode.h"
-#include "rt_treelet.h"
 
 hipError_t rt_launch_math_selftest(uint32_t which, unsigned long long* mismatches, uint32_t* first_bad,
                                    hipStream_t stream);
@@ -53,11 +52,6 @@ hipError_t rt_launch_brute_wf(const KernelArgs& ka, bool tris, bool scalar_strea
                               hipStream_t stream);
 size_t rt_brute_wf_tile_bytes(bool scalar_stream);
 uint32_t rt_brute_wf_chunk();
-hipError_t rt_launch_tl(int kind, const KernelArgs& ka, const TreeletArgs& ta, uint32_t blocks, size_t lds_bytes,
-                        hipStream_t stream);
-hipError_t rt_launch_tl_derive_top(const float4* base, const uint32_t* src, const uint2* links, float4* top, uint32_t n,
-                                   hipStream_t stream);
-size_t rt_tl_subtree_lds_bytes(uint32_t nodes, uint32_t prims);
 hipError_t rt_launch_resolve(float4* accum, uint32_t* output, const float4* light, uint32_t width, uint32_t height,
                              uint32_t tiles_x, uint32_t owned_tiles, uint32_t rank, uint32_t world, uint32_t k0,
                              uint32_t samples, uint32_t frames, unsigned long long* clock, hipStream_t stream);
@@ -140,8 +134,6 @@ constexpr uint32_t kMaxFrameBatch = 64;
 // in order afterwards) up to this many frames x samples; larger batches run each
 // pixel's frames back to back on one lane.
 constexpr uint32_t kMaxParallelLights = 64;
-// The treelet wavefront by default where it applies (tuning "treelet_walk")
-constexpr bool kTreeletByDefault = false;
 
 }  // namespace
 
@@ -282,26 +274,6 @@ struct rt_ctx {
     // per-lane leaf tests
     bool use_coop_leaves = true;
     uint4* d_tri_ltris = nullptr;
-    // the treelet wavefront (treelet.hip): tuning "treelet_walk" 1 / 0 force it on /
-    // off, -1 by scene. The cut and the top layouts' links are host-built with the accelerator,
-    // the top layouts' boxes derived on the device after every upload or refit.
-    int treelet_walk = -1;
-    bool tl_built = false, tl_top_dirty = true;
-    uint32_t tl_n_sub = 0, tl_top_stride = 0, tl_max_leaves = 0;
-    uint4* d_tl_subtrees = nullptr;
-    uint32_t* d_tl_src = nullptr;
-    uint2* d_tl_links = nullptr;
-    float4* d_tl_top = nullptr;
-    size_t tl_subtrees_cap = 0, tl_src_cap = 0, tl_links_cap = 0, tl_top_cap = 0;
-    float4* d_tl_paths = nullptr;
-    uint4* d_tl_walk = nullptr;
-    uint32_t* d_tl_lists = nullptr;
-    uint32_t* d_tl_ctl = nullptr;
-    uint32_t* d_tl_cnt = nullptr;
-    uint4* d_tl_chunks = nullptr;
-    size_t tl_paths_cap = 0, tl_walk_cap = 0, tl_lists_cap = 0, tl_ctl_cap = 0, tl_cnt_cap = 0, tl_chunks_cap = 0;
-    uint32_t* h_tl_ctl = nullptr;  // pinned: the list lengths read back every few rounds
-    uint64_t tl_rounds = 0;        // wavefront rounds of the last treelet launch (diagnostics)
     size_t tri_ltris_cap = 0;
     bool ltris_dirty = true;
     // rt_set_brute_force: the reference's own sweeps (BASELINE config 5): 0 off, 1 LDS-tiled, 2
@@ -570,29 +542,6 @@ int refresh_tri_accel(rt_ctx* ctx, uint32_t object_count) {
             (rc = upload_raw(ctx, ctx->d_tri_skip8, skip.data(), b8)))
             return rc;
         ctx->tri_octants_built = true;
-    }
-    // the treelet cut and its top layouts (treelet.hip)
-    ctx->tl_built = false;
-    {
-        TreeletCut cut;
-        if (acc.nodes.size() > 1 && build_treelet_cut(acc.nodes, kTreeletNodes, &cut) &&
-            rt_tl_subtree_lds_bytes(kTreeletNodes, cut.max_leaves) <= 64u * 1024u) {
-            const size_t nt = cut.src.size();
-            if ((rc = ensure(reinterpret_cast<void**>(&ctx->d_tl_subtrees), &ctx->tl_subtrees_cap,
-                             std::max<size_t>(16, cut.subtrees.size() * 4))) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tl_src), &ctx->tl_src_cap, nt * 4)) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tl_links), &ctx->tl_links_cap, nt * 8)) ||
-                (rc = ensure(reinterpret_cast<void**>(&ctx->d_tl_top), &ctx->tl_top_cap, nt * 32)) ||
-                (rc = upload_raw(ctx, ctx->d_tl_subtrees, cut.subtrees.data(), cut.subtrees.size() * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_tl_src, cut.src.data(), nt * 4)) ||
-                (rc = upload_raw(ctx, ctx->d_tl_links, cut.links.data(), nt * 8)))
-                return rc;
-            ctx->tl_n_sub = (uint32_t)(cut.subtrees.size() / 4);
-            ctx->tl_top_stride = cut.top_stride;
-            ctx->tl_max_leaves = cut.max_leaves;
-            ctx->tl_built = true;
-            ctx->tl_top_dirty = true;
-        }
     }
     // depth levels for the device refit (preorder: a node precedes its children)
     std::vector<uint32_t> depth(acc.nodes.size(), 0);
@@ -875,13 +824,10 @@ void rt_destroy(rt_ctx* ctx) {
                     ctx->d_tile_sched[0], ctx->d_tile_sched[1], ctx->d_frame_light[0], ctx->d_frame_light[1],
                     ctx->d_clock, ctx->d_stream, ctx->d_primary[0], ctx->d_primary[1], ctx->d_tri_qnodes,
                     ctx->d_tri_qgrid, ctx->d_tri_src8, ctx->d_tri_skip8, ctx->d_tri_bvh8, ctx->d_tri_lcert,
-                    ctx->d_tri_ltris, ctx->d_brute_paths, ctx->d_brute_queue, ctx->d_brute_counts,
-                    ctx->d_tl_subtrees, ctx->d_tl_src, ctx->d_tl_links, ctx->d_tl_top, ctx->d_tl_paths,
-                    ctx->d_tl_walk, ctx->d_tl_lists, ctx->d_tl_ctl, ctx->d_tl_cnt, ctx->d_tl_chunks};
+                    ctx->d_tri_ltris, ctx->d_brute_paths, ctx->d_brute_queue, ctx->d_brute_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-    if (ctx->h_tl_ctl) (void)hipHostFree(ctx->h_tl_ctl);
     for (hipEvent_t ev : {ctx->staging_done, ctx->ev_resolved[0], ctx->ev_resolved[1], ctx->ev_aux_done,
                           ctx->ev_primary})
         if (ev) (void)hipEventDestroy(ev);
@@ -1115,156 +1061,6 @@ static int dispatch_frames(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     ctx->params.accumulation_index = k0;  // the batch's Params, as one launch leaves them
     return rc;
-}
-
-// The treelet wavefront (treelet.hip) for one batch: the primary pre-pass, the
-// first segments' shading, then rounds of {shading, top walk, treelet queues, treelet walks}
-// until every path has ended, then the batch's resolve pass; all on the primary stream. `ka` is
-// the batch's argument block (scene image offsets of LDS mode 1 in it), `image` that image's bytes.
-static int dispatch_treelet(rt_ctx* ctx, KernelArgs ka, uint32_t bounces, uint32_t frames, size_t image) {
-    const rt_params& p = ctx->params;
-    const uint32_t samples = p.compute_per_frame;
-    const uint64_t owned_px = (uint64_t)ctx->owned_tiles * 64u;
-    const uint64_t n_slots = owned_px * frames * samples;
-    RT_HIP(ctx, join_aux(ctx));
-    auto grow = [&](void** ptr, size_t* cap, size_t bytes) { return grow_buffer(ctx, ptr, cap, bytes); };
-    int rc;
-    // the batch's lights (resolved in order afterwards) and the pre-pass's records
-    if (n_slots > ctx->frame_light_cap) {
-        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        for (float4*& b : ctx->d_frame_light) {
-            if (b) RT_HIP(ctx, hipFree(b));
-            b = nullptr;
-        }
-        ctx->frame_light_cap = 0;
-        for (float4*& b : ctx->d_frame_light) {
-            const hipError_t ea = hipMalloc(reinterpret_cast<void**>(&b), n_slots * sizeof(float4));
-            if (ea != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("frame lights: ") + hipGetErrorString(ea));
-        }
-        ctx->frame_light_cap = n_slots;
-    }
-    if (n_slots > ctx->primary_cap) {
-        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        for (uint4*& b : ctx->d_primary) {
-            if (b) RT_HIP(ctx, hipFree(b));
-            b = nullptr;
-        }
-        ctx->primary_cap = 0;
-        for (uint4*& b : ctx->d_primary) {
-            const hipError_t ea = hipMalloc(reinterpret_cast<void**>(&b), n_slots * 16);
-            if (ea != hipSuccess) return fail(ctx, RT_E_NOMEM, std::string("primary records: ") + hipGetErrorString(ea));
-        }
-        ctx->primary_cap = n_slots;
-    }
-    if ((rc = grow(reinterpret_cast<void**>(&ctx->d_tl_paths), &ctx->tl_paths_cap, 4 * n_slots * sizeof(float4))) ||
-        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_walk), &ctx->tl_walk_cap, 2 * n_slots * sizeof(uint4))) ||
-        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_lists), &ctx->tl_lists_cap, 5 * n_slots * sizeof(uint32_t))) ||
-        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_ctl), &ctx->tl_ctl_cap, 8 * sizeof(uint32_t))) ||
-        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_cnt), &ctx->tl_cnt_cap, (2 * (size_t)ctx->tl_n_sub + 1) * 4)) ||
-        (rc = grow(reinterpret_cast<void**>(&ctx->d_tl_chunks), &ctx->tl_chunks_cap,
-                   ((size_t)ctx->tl_n_sub + n_slots / kTlChunk + 1) * sizeof(uint4))))
-        return rc;
-    if (!ctx->h_tl_ctl) RT_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_tl_ctl), 8 * sizeof(uint32_t), hipHostMallocDefault));
-    // the top layouts' boxes, from the base accelerator as it is now
-    if (ctx->tl_top_dirty) {
-        RT_HIP(ctx, rt_launch_tl_derive_top(reinterpret_cast<const float4*>(ctx->d_tri_bvh), ctx->d_tl_src, ctx->d_tl_links,
-                                            ctx->d_tl_top, 8u * ctx->tl_top_stride, ctx->stream));
-        ctx->tl_top_dirty = false;
-    }
-    // the leaves' triangle blocks (staged by the treelet walks)
-    {
-        const size_t bytes = (size_t)ka.tri_prim_count * kLeafTriWords * sizeof(uint4);
-        if (ctx->tri_ltris_cap < bytes) {
-            if ((rc = grow(reinterpret_cast<void**>(&ctx->d_tri_ltris), &ctx->tri_ltris_cap, bytes))) return rc;
-            ctx->ltris_dirty = true;
-        }
-        if (ctx->ltris_dirty) {
-            RT_HIP(ctx, rt_launch_tri_leaftris(ctx->d_tri_prims, ka.tri_prim_count, ctx->d_tri, ctx->n_tri_dev,
-                                               ctx->d_tri_ltris, ctx->stream));
-            ctx->ltris_dirty = false;
-        }
-        ka.tri_leaftris = ctx->d_tri_ltris;
-    }
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_tl_ctl, 0, 8 * sizeof(uint32_t), ctx->stream));
-    RT_HIP(ctx, hipMemsetAsync(ctx->d_tl_cnt, 0, (2 * (size_t)ctx->tl_n_sub + 1) * 4, ctx->stream));
-    ka.frame_light = ctx->d_frame_light[0];
-    ka.primary = ctx->d_primary[0];
-    ka.frames = frames;
-    ka.lds_srgb_offset = (uint32_t)(image - kLdsTailBytes);
-    ka.tri_prims = reinterpret_cast<const uint4*>(ctx->d_tri_prims);  // the base accelerator's leaf records
-    // timing: the pre-pass opens the span, a one-thread kernel after the last round closes it
-    ka.launch_clock = nullptr;
-    if (ctx->timing) {
-        if (ctx->clock_pending.size() >= kClockSlots && (rc = collect_timing(ctx))) return rc;
-        if (!ctx->d_clock && (rc = dev_alloc(ctx, &ctx->d_clock, kClockWords * (size_t)kClockSlots))) return rc;
-        const uint32_t slot = ctx->clock_next;
-        ctx->clock_next = (ctx->clock_next + 1) % kClockSlots;
-        ka.launch_clock = ctx->d_clock + kClockWords * (size_t)slot;
-        ctx->clock_pending.push_back(slot);
-    }
-    hipStream_t S = ctx->stream;
-    {
-        KernelArgs pka = ka;
-        pka.queue_units = ctx->owned_tiles * frames;  // one unit per (frame, tile)
-        pka.primary_tile_major = ctx->primary_tile_major ? 1u : 0u;
-        const uint32_t min_waves = ctx->primary_threads != 256u ? 0u : ctx->primary_min_waves;
-        RT_HIP(ctx, rt_launch_primary(pka, 1, true, image, ctx->primary_threads, min_waves, S));
-    }
-    TreeletArgs ta{};
-    ta.paths = ctx->d_tl_paths;
-    ta.walk = ctx->d_tl_walk;
-    ta.lists = ctx->d_tl_lists;
-    ta.ctl = ctx->d_tl_ctl;
-    ta.sub_cnt = ctx->d_tl_cnt;
-    ta.sub_off = ctx->d_tl_cnt + ctx->tl_n_sub;
-    ta.chunks = ctx->d_tl_chunks;
-    ta.subtrees = ctx->d_tl_subtrees;
-    ta.top = ctx->d_tl_top;
-    ta.base_nodes = reinterpret_cast<const float4*>(ctx->d_tri_bvh);
-    ta.top_stride = ctx->tl_top_stride;
-    ta.n_slots = (uint32_t)n_slots;
-    ta.n_sub = ctx->tl_n_sub;
-    const uint32_t grid = 4u * (uint32_t)std::max(1, ctx->n_cu);
-    // the top walk: dependent node loads per lane, so as many resident waves as fit (8 per SIMD)
-    const uint32_t top_grid = 8u * (uint32_t)std::max(1, ctx->n_cu);
-    // the treelet walks: as many workgroups as stay resident with their LDS image (5 per CU at 30 KB)
-    const uint32_t walk_grid = (uint32_t)std::min<uint64_t>(5u * (uint32_t)std::max(1, ctx->n_cu),
-                                                            (uint64_t)ctx->tl_n_sub + n_slots / kTlChunk + 1);
-    const size_t tl_lds = rt_tl_subtree_lds_bytes(kTreeletNodes, ctx->tl_max_leaves);
-    ta.round = 0;
-    RT_HIP(ctx, rt_launch_tl(0, ka, ta, (uint32_t)std::min<uint64_t>(grid, (n_slots + 255) / 256), image, S));
-    // rounds until every path has ended; the list lengths are read back every kCheck rounds (a
-    // round with empty lists is a few empty launches)
-    constexpr uint32_t kCheck = 8, kMaxRounds = 1u << 12;
-    uint32_t r = 0;
-    for (;; ++r) {
-        if (r >= kMaxRounds) return fail(ctx, RT_E_HIP, "treelet wavefront: paths still running after 4096 rounds");
-        ta.round = r;
-        if (r > 0) RT_HIP(ctx, rt_launch_tl(1, ka, ta, grid, image, S));
-        RT_HIP(ctx, rt_launch_tl(2, ka, ta, top_grid, 0, S));
-        RT_HIP(ctx, rt_launch_tl(3, ka, ta, 1, 0, S));
-        RT_HIP(ctx, rt_launch_tl(4, ka, ta, top_grid, 0, S));
-        RT_HIP(ctx, rt_launch_tl(5, ka, ta, walk_grid, tl_lds, S));
-        if (r % kCheck == kCheck - 1) {
-            RT_HIP(ctx, hipMemcpyAsync(ctx->h_tl_ctl, ctx->d_tl_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, S));
-            RT_HIP(ctx, hipStreamSynchronize(S));
-            const uint32_t nq = (r + 1) & 1u;  // the next round's walk and shading lists
-            if (ctx->h_tl_ctl[nq] == 0 && ctx->h_tl_ctl[2 + nq] == 0) break;
-        }
-    }
-    ctx->tl_rounds = r + 1;
-    if (ka.launch_clock) RT_HIP(ctx, rt_launch_tl(6, ka, ta, 1, 0, S));
-    if (ctx->batches > 0) RT_HIP(ctx, hipStreamWaitEvent(S, ctx->ev_resolved[(ctx->batches - 1) & 1u], 0));
-    RT_HIP(ctx, rt_launch_resolve(ctx->d_accum, ctx->d_out, ka.frame_light, ctx->width, ctx->height, ctx->tiles_x,
-                                  ctx->owned_tiles, ctx->rank, ctx->world, p.accumulation_index, samples, frames,
-                                  ka.launch_clock ? ka.launch_clock + 2 : nullptr, S));
-    RT_HIP(ctx, hipEventRecord(ctx->ev_resolved[ctx->batches & 1u], S));
-    ctx->batches += 1;
-    ctx->last_blocks = grid;
-    ctx->last_lds = (uint32_t)tl_lds;
-    ctx->last_passes = RT_PASS_TREELET | RT_PASS_PRIMARY | RT_PASS_RESOLVE;
-    ctx->primary_dirty = true;
-    return RT_OK;
 }
 
 // One launch rendering `frames` frames starting at Params.accumulation_index.
@@ -1612,18 +1408,6 @@ static int dispatch_batch(rt_ctx* ctx, uint32_t bounces, uint32_t frames) {
     }
     // per-thread LDS after the scene image: the cooperative leaf batch's per-wave scratch
     const size_t lane_pt = coop ? (size_t)kLeafBatchWaveBytes / 64u : 0u;
-    // The treelet wavefront, for scenes whose triangle accelerator is walked from global memory
-    // (LDS mode 1) and whose spheres are all in the brute-force set
-    {
-        const uint64_t tl_bytes =
-            (uint64_t)owned_px * frames * p.compute_per_frame * (sizeof(float4) * (2 + 4) + sizeof(uint4) * 3 + 4 * 5);
-        const bool treelet = ctx->tl_built && tris && mode == 1 && ka.tri_accel && ka.tri_nodes != 0 && ctx->n_nodes == 0 &&
-                             p.accumulate == 1u && p.compute_per_frame > 0 && bounces > 0 &&
-                             ka.tri_prim_count != 0 && tl_bytes <= ctx->batch_budget &&
-                             (uint64_t)owned_px * frames * p.compute_per_frame < (1ull << 31) &&
-                             (ctx->treelet_walk == 1 || (ctx->treelet_walk == -1 && kTreeletByDefault));
-        if (treelet) return dispatch_treelet(ctx, ka, bounces, frames, mode1_bytes);
-    }
     // Persistent grid: as many workgroups as can be resident (never more than
     // one wave per tile); waves then pull tiles from the queue.
     if (ctx->occ_blocks_per_cu == 0 || ctx->occ_lds_bytes != lds_bytes || ctx->occ_mode != mode ||
@@ -1965,7 +1749,6 @@ int rt_update_objects(rt_ctx* ctx, const rt_object_transform* transforms, uint32
         RT_HIP(ctx, rt_launch_refit(ctx->d_tri_bvh, ctx->d_tri_prims, ctx->d_sub, ctx->d_tri_order,
                                     ctx->d_tri_level_off, ctx->tri_levels, ctx->d_tri_extent, ctx->stream));
         ctx->qnodes_dirty = true;
-        ctx->tl_top_dirty = true;
     }
     ctx->cones_dirty = true;  // the triangles changed
     ctx->ltris_dirty = true;
@@ -2153,8 +1936,6 @@ int rt_set_tuning(rt_ctx* ctx, const char* key, int32_t value) {
         rc = flag(ctx->batch_schedule);
     } else if (k == "unit_tile_major") {
         rc = flag(ctx->unit_tile_major);
-    } else if (k == "treelet_walk") {
-        if ((rc = range(-1, 1)) == RT_OK) ctx->treelet_walk = v;
     } else if (k == "batch_memory_mb") {
         if ((rc = range(1, 1 << 30)) == RT_OK) ctx->batch_budget = (size_t)v << 20;
     } else {

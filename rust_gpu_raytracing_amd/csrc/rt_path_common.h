@@ -1,6 +1,6 @@
 // rt_path_common.h -- the device side of one path segment, shared by the path-tracing kernels
-// (pathtrace.hip: the persistent walk, the primary pre-pass, the brute-force wavefront) and the
-// treelet wavefront (treelet.hip): the reference's sphere and triangle tests, its sweep,
+// (pathtrace.hip: the persistent walk, the primary pre-pass, the brute-force wavefront): the
+// reference's sphere and triangle tests, its sweep,
 // trace_ray's result, the shading of the bounce loop, sampling, packing. Every function follows
 // compute_shader.wgsl decision for decision (line numbers in each); the numeric contract is in
 // rt_device_math.h.
@@ -615,7 +615,7 @@ __device__ __forceinline__ void primary_state(const PrimaryRecord& r, TraceState
     }
 }
 
-// The wavefront kernels' LDS scene image (brute force, treelet walk) (the persistent kernel's mode 1: spheres in slot
+// The wavefront kernel's LDS scene image (brute force) (the persistent kernel's mode 1: spheres in slot
 // order, materials + glass constants, objects, sRGB table and camera block); the caller
 // synchronises before reading it. Returns the view of it; `cam` receives the camera block.
 template <bool kTris, uint32_t kThreads>

@@ -376,82 +376,3 @@ void build_sphere_slots(const rt_scene_sphere* s, uint32_t count, bool use_bvh, 
     out->r_max = (float)r_max;
 }
 
-bool build_treelet_cut(const std::vector<SphereBvhNode>& nodes, uint32_t max_nodes, TreeletCut* out) {
-    constexpr uint32_t kInternal = 0xffffffffu, kTreelet = 0x40000000u, kEnd = 0x7fffffffu;
-    out->subtrees.clear();
-    out->src.clear();
-    out->links.clear();
-    out->top_stride = 0;
-    out->max_leaves = 0;
-    const uint32_t n = (uint32_t)nodes.size();
-    if (n == 0) return false;
-    // treelet roots: internal nodes whose pre-order range fits, whose parent's does not
-    std::vector<uint32_t> tid(n, kInternal);
-    std::function<void(uint32_t, uint32_t)> cut = [&](uint32_t i, uint32_t end) {
-        const uint32_t size = end - i;
-        if (nodes[i].leaf != kSphereBvhInternal) return;  // a lone leaf stays in the top
-        if (size <= max_nodes) {
-            uint32_t p0 = kInternal, np = 0;
-            for (uint32_t k = i; k < end; k++) {
-                if (nodes[k].leaf == kSphereBvhInternal) continue;
-                const uint32_t leaf = nodes[k].leaf & 0xffffffu;
-                if (np == 0) p0 = leaf;
-                if (leaf != p0 + np) return;  // not one range: stays in the top (checked below)
-                np++;
-            }
-            tid[i] = (uint32_t)(out->subtrees.size() / 4);
-            out->subtrees.insert(out->subtrees.end(), {i, size, p0, np});
-            out->max_leaves = std::max(out->max_leaves, np);
-            return;
-        }
-        const uint32_t a = i + 1, b = nodes[a].skip;  // left child's range [a, b), right child's [b, end)
-        cut(a, b);
-        cut(b, end);
-    };
-    cut(0, nodes[0].skip <= n ? nodes[0].skip : n);
-    // the 8 top layouts
-    for (uint32_t oct = 0; oct < 8; oct++) {
-        const uint32_t base = (uint32_t)out->src.size();
-        std::function<void(uint32_t)> emit = [&](uint32_t src) {
-            const uint32_t at = (uint32_t)out->src.size();
-            out->src.push_back(src);
-            out->links.insert(out->links.end(), {0u, 0u});
-            uint32_t leafw;
-            if (tid[src] != kInternal) {
-                leafw = kTreelet | tid[src];
-            } else if (nodes[src].leaf != kSphereBvhInternal) {
-                leafw = nodes[src].leaf & 0xffffffu;  // the leaf record
-            } else {
-                leafw = kInternal;
-                uint32_t a = src + 1, b = nodes[src + 1].skip;  // order_bvh_by_octant's child order
-                int axis = 0;
-                double best = -1.0, diff = 0.0;
-                for (int k = 0; k < 3; k++) {
-                    const double ca = 0.5 * ((double)nodes[a].bmin[k] + (double)nodes[a].bmax[k]);
-                    const double cb = 0.5 * ((double)nodes[b].bmin[k] + (double)nodes[b].bmax[k]);
-                    if (std::fabs(cb - ca) > best) {
-                        best = std::fabs(cb - ca);
-                        axis = k;
-                        diff = cb - ca;
-                    }
-                }
-                const bool negative = (oct >> axis) & 1u;
-                if ((diff < 0.0) != negative) std::swap(a, b);
-                emit(a);
-                emit(b);
-            }
-            const uint32_t after = (uint32_t)out->src.size();
-            out->links[2 * (size_t)at] = after == base + out->top_stride && oct > 0 ? kEnd : after;
-            out->links[2 * (size_t)at + 1] = leafw;
-        };
-        emit(0);
-        if (oct == 0) {
-            out->top_stride = (uint32_t)out->src.size();
-            for (uint32_t k = 0; k < out->top_stride; k++)  // (the layout's size is known only now)
-                if (out->links[2 * (size_t)k] == out->top_stride) out->links[2 * (size_t)k] = kEnd;
-        }
-        if (out->src.size() != (size_t)(oct + 1) * out->top_stride) return false;
-    }
-    return out->top_stride > 0 && out->top_stride < kTreelet;
-}
-

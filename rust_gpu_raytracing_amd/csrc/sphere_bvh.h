@@ -111,20 +111,3 @@ struct TriangleAccel {
 void build_triangle_accel(const rt_object_info* objects, uint32_t object_count, const rt_sub_object_info* subs,
                           uint32_t sub_count, TriangleAccel* out);
 
-// The treelet cut of the triangle accelerator (treelet.hip): the maximal
-// subtrees of at most `max_nodes` nodes with internal roots (the treelets: in the pre-order
-// layout a subtree is one range of nodes, and its leaf records one range of prims), and 8
-// direction-ordered layouts of the part above them (the child order of order_bvh_by_octant),
-// each treelet a pseudo-leaf there. subtrees: {root, nodes, first leaf record, leaf records};
-// per top position its base node (src) and {skip link, leaf word} (links; rt_treelet.h's
-// kTlInternal / kTlTreelet / kTlEnd); top_stride: positions per layout. False when the leaf
-// records of a subtree are not one ascending range (never for build_triangle_accel's trees).
-struct TreeletCut {
-    std::vector<uint32_t> subtrees;  // 4 per treelet
-    std::vector<uint32_t> src;
-    std::vector<uint32_t> links;     // 2 per top position
-    uint32_t top_stride = 0;
-    uint32_t max_leaves = 0;
-};
-bool build_treelet_cut(const std::vector<SphereBvhNode>& nodes, uint32_t max_nodes, TreeletCut* out);
-

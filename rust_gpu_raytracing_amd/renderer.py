@@ -420,7 +420,7 @@ class Renderer:
         v = ctypes.c_uint32()
         N.check(self._ctx, self._lib.rt_last_launch_passes(self._ctx, ctypes.byref(v)), self._lib)
         names = ((N.RT_PASS_PATH, "path"), (N.RT_PASS_PRIMARY, "primary"), (N.RT_PASS_RESOLVE, "resolve"),
-                 (N.RT_PASS_BRUTE, "brute"), (N.RT_PASS_BRUTE_STREAM, "brute_stream"), (N.RT_PASS_TREELET, "treelet"))
+                 (N.RT_PASS_BRUTE, "brute"), (N.RT_PASS_BRUTE_STREAM, "brute_stream"))
         return [n for bit, n in names if v.value & bit]
 
     @property

@@ -290,110 +290,6 @@ static Res accel(const TriangleAccel& A, const std::vector<rt_object_info>& ob, 
     return r;
 }
 
-// ---- the treelet wavefront (treelet.hip): top layouts, then treelets in base pre-order ----
-// The top walk visits the direction-ordered layout above the cut; an entered treelet is walked
-// in the base layout's order; every leaf is merged as the kernels merge it (object box, the
-// leaf's lexicographic minimum and NaN flag, the sub-object box only when it would change the
-// result), candidates beyond the best hit skipped. The order differs from every other walk's.
-static long tl_entries = 0, tl_top_visits = 0, tl_sub_visits = 0;
-
-static void tl_leaf(const TriangleAccel& A, const std::vector<rt_object_info>& ob, const std::vector<rt_sub_object_info>& sb,
-                    const std::vector<rt_scene_triangle>& tr, V o, V d, V inv, uint32_t prim, float& best,
-                    uint32_t& best_seq, Res& r, bool& nan_hit) {
-    const SubObjectPrim& p = A.prims[prim];
-    if (!rib(o, inv, ob[p.object].min_bounds, ob[p.object].max_bounds)) return;
-    const rt_sub_object_info& s = sb[p.sub];
-    const uint32_t first = s.first_triangle_index, count = s.triangle_count;
-    float cd = INFINITY;
-    uint32_t cs = 0xffffffffu;
-    int cti = -1, cfront = 0;
-    bool cnan = false;
-    for (uint32_t j = 0; j < count; j++) {
-        const rt_scene_triangle& t = tr[std::min<uint32_t>(first + j, (uint32_t)tr.size() - 1u)];
-        V cn = ld(t.calc_normal);
-        float det = -dot(d, cn), inv_det = 1.0f / det;
-        V ao = sub(o, ld(t.a));
-        float dist = dot(ao, cn) * inv_det;
-        if (dist < 0.0f || dist > best) continue;
-        V dao = cross(ao, d);
-        float v = -dot(ld(t.edge_ab), dao) * inv_det;
-        if (v < 0.0f) continue;
-        float u = dot(ld(t.edge_ac), dao) * inv_det;
-        if (u < 0.0f) continue;
-        float w = 1.0f - u - v;
-        if (w < 0.0f) continue;
-        if (dist != dist) { cnan = true; continue; }
-        const uint32_t seq = p.seq_base + j;
-        if (dist < cd || (dist == cd && seq < cs)) {
-            cd = dist;
-            cs = seq;
-            cti = (int)std::min<uint32_t>(first + j, (uint32_t)tr.size() - 1u);
-            cfront = det > 0.0f;
-        }
-    }
-    const bool beats = cd < best || (cd == best && cs < best_seq);
-    if ((cnan || beats) && rib(o, inv, s.min_bounds, s.max_bounds)) {
-        if (cnan) nan_hit = true;
-        if (beats) {
-            best = cd;
-            best_seq = cs;
-            r = {cd, cti, (int)p.object, cfront};
-        }
-    }
-}
-
-static Res treelet_walk(const TriangleAccel& A, const TreeletCut& C, const std::vector<rt_object_info>& ob,
-                        const std::vector<rt_sub_object_info>& sb, const std::vector<rt_scene_triangle>& tr, V o, V d,
-                        float scale) {
-    constexpr uint32_t kInternal = 0xffffffffu, kTreelet = 0x40000000u, kEnd = 0x7fffffffu;
-    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    const float m = scale * (std::sqrt(dot(o, o)) + A.extent) + 1.0e-30f;
-    const SlabRay sr = slab_ray(o.x, o.y, o.z, inv.x, inv.y, inv.z, m);
-    float best = F32_MAX_;
-    uint32_t best_seq = 0;
-    Res r{F32_MAX_, -1, -1, 0};
-    bool nan_hit = false;
-    uint32_t ib[3];
-    memcpy(ib, &inv, 12);
-    uint32_t pos = ((ib[0] >> 31) | ((ib[1] >> 31) << 1) | ((ib[2] >> 31) << 2)) * C.top_stride;
-    while (pos < kEnd) {
-        const SphereBvhNode& nd = A.nodes[C.src[pos]];
-        tl_top_visits++;
-        float nt, ft;
-        slab_hit(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2], nt, ft);
-        const bool hit = nt <= ft && ft >= 0.0f;
-        const uint32_t skip = C.links[2 * (size_t)pos], leaf = C.links[2 * (size_t)pos + 1];
-        if (hit && leaf == kInternal) {
-            pos += 1;
-            continue;
-        }
-        if (hit && (leaf & kTreelet)) {
-            tl_entries++;
-            const uint32_t* st = &C.subtrees[4 * (size_t)(leaf & ~kTreelet)];
-            const uint32_t root = st[0], nn = st[1];
-            uint32_t node = 0;
-            while (node < nn) {
-                const SphereBvhNode& sn = A.nodes[root + node];
-                tl_sub_visits++;
-                float a, b;
-                slab_hit(sr, sn.bmin[0], sn.bmin[1], sn.bmin[2], sn.bmax[0], sn.bmax[1], sn.bmax[2], a, b);
-                const bool h = a <= b && b >= 0.0f;
-                if (h && sn.leaf == kSphereBvhInternal) {
-                    node += 1;
-                    continue;
-                }
-                if (h) tl_leaf(A, ob, sb, tr, o, d, inv, sn.leaf & 0xffffffu, best, best_seq, r, nan_hit);
-                node = sn.skip - root;
-            }
-        } else if (hit) {
-            tl_leaf(A, ob, sb, tr, o, d, inv, leaf & 0xffffffu, best, best_seq, r, nan_hit);
-        }
-        pos = skip;
-    }
-    if (nan_hit) return {F32_MAX_, -2, -2, 0};  // the kernel reruns the sweep: checked by the caller
-    return r;
-}
-
 int main(int argc, char** argv) {
     if (argc < 5) return 2;
     auto ob = load<rt_object_info>(argv[1]);
@@ -442,12 +338,6 @@ int main(int argc, char** argv) {
         }
         lcert[pi] = tricone::leafcert_build(cnt, ta, tab, tac, tcn, lo, hi);
         lcert_valid += lcert[pi].w[7] != kLeafCertNone;
-    }
-    TreeletCut cut;
-    const bool cut_ok = build_treelet_cut(A.nodes, 128, &cut);
-    if (A.nodes.size() > 1 && !cut_ok) {
-        printf("TREELET CUT failed\n");
-        return 1;
     }
     std::vector<SphereBvhNode> oct;
     std::vector<uint32_t> qoct;
@@ -508,15 +398,9 @@ int main(int argc, char** argv) {
         g_qoct = nullptr;
         g_q = nullptr;
         g_lazy = false;
-        Res tw = b;
-        if (cut_ok) {
-            tw = treelet_walk(A, cut, ob, sb, tr, o, d, scale);
-            if (tw.tri == -2) tw = sweep(ob, sb, tr, o, d);
-        }
-        const Res* const walks[] = {&b, &e, &f, &h, &x, &y, &tw};
-        const char* const names[] = {"binary", "qnodes", "qnodes+lazy", "octants+prune", "certified", "kernel-default",
-                                     "treelet"};
-        for (int wi = 0; wi < 7; wi++) {
+        const Res* const walks[] = {&b, &e, &f, &h, &x, &y};
+        const char* const names[] = {"binary", "qnodes", "qnodes+lazy", "octants+prune", "certified", "kernel-default"};
+        for (int wi = 0; wi < 6; wi++) {
             const Res* w = walks[wi];
             uint32_t ta, tb;
             memcpy(&ta, &a.t, 4);
@@ -536,9 +420,6 @@ int main(int argc, char** argv) {
            (double)g_lcert_leaves / n, (double)g_lcert_skipped / n, (double)g_lcert_tris / n, lcert_valid,
            lcert.size());
     printf("heuristic_misses %ld\n", g_heur_miss);
-    // treelet <treelets> <top layout size> <entries/ray> <top visits/ray> <treelet visits/ray> <max leaves>
-    printf("treelet %zu %u %.2f %.2f %.2f %u\n", cut.subtrees.size() / 4, cut.top_stride, (double)tl_entries / n,
-           (double)tl_top_visits / n, (double)tl_sub_visits / n, cut.max_leaves);
     printf("kernel_default %ld %ld %ld %ld\n", g_gap_checked, g_gap_skipped, g_coop_leaves, g_coop_nan);
     if (!g_depth.empty()) {  // depth, visits per ray at that depth, nodes of one layout at that depth
         std::vector<long> per(64, 0);

@@ -193,5 +193,5 @@ def test_header_constants_match_binding():
     text = HEADER.read_text()
     assert re.search(r"#define RT_DEFAULT_FRAME_BATCH (\d+)", text).group(1) == str(N.RT_DEFAULT_FRAME_BATCH)
     assert re.search(r"#define RT_GROUP_COPY_TRANSPORT (\d+)u", text).group(1) == str(N.RT_GROUP_COPY_TRANSPORT)
-    for name in ("PATH", "PRIMARY", "RESOLVE", "BRUTE", "BRUTE_STREAM", "TREELET"):
+    for name in ("PATH", "PRIMARY", "RESOLVE", "BRUTE", "BRUTE_STREAM"):
         assert re.search(rf"#define RT_PASS_{name} (\d+)u", text).group(1) == str(getattr(N, f"RT_PASS_{name}"))

@@ -598,52 +598,6 @@ def test_gpu_tuning_keys_refuse_bad_input(gpu):
             r.copy_output_to_device(dev.data_ptr(), 4 * 64)
 
 
-@pytest.mark.parametrize("config,kw,spp,batch,world,tuning", [
-    ("c5_heightfield", dict(nx=200, nz=100), 1, 1, 1, {}),
-    ("c5_heightfield", dict(nx=200, nz=100), 2, 3, 1, {}),
-    ("c5_heightfield", dict(nx=200, nz=100), 1, 4, 3, {}),  # tile split
-    ("c5_heightfield", dict(nx=60, nz=30), 1, 2, 1, {"primary_tile_major": 0, "lds_mode": 1}),  # (fits LDS otherwise)
-    ("c3_chess", dict(env_size=(512, 256)), 1, 3, 1, {"lds_mode": 1}),  # a mesh scene walked from global memory
-    ("c5_heightfield", dict(nx=200, nz=100), 1, 5, 1, {"batch_memory_mb": 1}),  # a batch split over launches
-])
-def test_gpu_treelet_walk(gpu, oracle_lib, config, kw, spp, batch, world, tuning):
-    """The treelet wavefront (treelet.hip, tuning "treelet_walk" 1): the top walk, the treelet
-    queues and the treelet walks from LDS, the shading rounds and the batch's resolve give the
-    oracle's accumulation, image and ray count bit for bit -- several samples, batches of frames,
-    a tile split, frame-major pre-pass units, and batches split by the memory budget."""
-    scene, bounces = build_config(config, width=96, height=64, **kw)
-    rays = scene.camera.recalculate_ray_directions()
-    acc_o, out_o, n_o = oracle_frames(oracle_lib, scene, bounces, 5, rays, compute_per_frame=spp)
-    acc = np.zeros_like(acc_o)
-    out = np.zeros_like(out_o)
-    n = 0
-    for rank in range(world):
-        with Renderer(scene, camera_rays=rays, frame_batch=batch, rank=rank, world_size=world, compute_per_frame=spp,
-                      tuning=dict(tuning, treelet_walk=1)) as r:
-            for _ in range(5):
-                r.compute_frame(bounces)
-            r.synchronize()
-            assert "treelet" in r.last_launch_passes(), r.last_launch_passes()
-            a, o, k = r.read_accumulation(), r.read_output(), r.ray_count()
-        mask = owned_mask(96, 64, rank, world)
-        acc[mask] = a[mask]
-        out[mask] = o[mask]
-        n += k
-    assert_same(acc, out, n, acc_o, out_o, n_o)
-
-
-def test_gpu_full_size_sampled_c5_treelet(gpu, oracle_lib):
-    """C5 at BASELINE size through the treelet wavefront: the oracle's 20,000 sampled pixels of
-    2 frames, and every pixel bit-identical to the persistent kernel's walk."""
-    smp = _c5_full_size_oracle_sample(oracle_lib)
-    acc, out, n = gpu_render(smp["scene"], smp["bounces"], 2, rays=smp["rays"], frame_batch=2,
-                             tuning={"treelet_walk": 1})
-    _check_c5_sample(smp, acc, out)
-    acc_d, out_d, n_d = gpu_render(smp["scene"], smp["bounces"], 2, rays=smp["rays"], frame_batch=2,
-                                   tuning={"treelet_walk": 0})
-    assert n == n_d and np.array_equal(out, out_d) and np.array_equal(acc.view(np.uint32), acc_d.view(np.uint32))
-
-
 def test_gpu_leaf_certificates_match_host(gpu):
     """The leaf certificates the device builds (rt_tri_leafcert_kernel) are bit for bit the
     host's (tri_cone.h, the CPU harness's builder), and every C5 leaf carries one."""

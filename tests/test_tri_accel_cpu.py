@@ -72,10 +72,6 @@ def test_heightfield_and_grazing_rays(harness, tmp_path):
     # the 16-B quantized nodes (tri_qnode.h): every box contains its node's, the walk over them
     # returns the sweep's result on every ray (checked above), and the coarser boxes cost few visits
     q_valid, q_nodes = line(out, "qnodes")
-    # the treelet wavefront's walk (treelet.hip): top layouts + treelets, exact ray by ray (checked
-    # above); rays enter treelets, and the treelets hold at most 64 leaves (their LDS image)
-    n_tl, stride, entries, top_visits, tl_visits, max_leaves = line(out, "treelet")
-    assert int(n_tl) > 10 and float(entries) > 0 and int(max_leaves) <= 64
     assert int(q_valid) == 1 and float(q_nodes) < 1.1 * float(nodes)
     # the default global-memory walk: octant layouts + distance pruning, the
     # sweep's result on every ray (checked above) with fewer visits and triangle tests
