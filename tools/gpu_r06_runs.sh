@@ -86,6 +86,14 @@ case "$T" in
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-cadences > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
     ;;
+  r06j)
+    # the build without the treelet wavefront: every GPU test, smoke, the headline bench; then
+    # the RT_DIAG split of C2 and C3 (where the idle lanes are)
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow c3_chess > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
