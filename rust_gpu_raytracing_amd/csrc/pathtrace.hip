@@ -158,6 +158,12 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
 // measured slower there.
 template <bool kTris>
 constexpr bool kDeferLeaves = kTris;
+// Sphere-only scenes: a lane that reaches a leaf stops walking, and the group tests of every lane
+// that reached one run once, after the wave's unrolled node steps (kTravUnroll), instead of inside
+// each node step for the few lanes at a leaf in that step. The lane resumes with its pruning
+// distance updated, so it visits the nodes the on-the-spot test would, in the same order.
+template <bool kTris>
+constexpr bool kBlockLeaves = !kTris;
 // Node steps per wave-wide check of the traversal loop (the ballots of the
 // threshold and leaf-batch tests, exec-mask updates). Lanes that finish inside
 // the group idle for its remaining steps; the visit order is unchanged.
@@ -165,7 +171,10 @@ constexpr bool kDeferLeaves = kTris;
 // (profiles/r04/r04_z): global-memory walks 3 -> 4 / 5 / 6: C5 -4.0% / -4.3% / -1.6%;
 // LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%; sphere walks 2 or 4: C2 +1.5% / +0.8%.
 template <int kMode, bool kTris>
-constexpr int kTravUnroll = !kTris ? 3 : kMode <= 1 ? 5 : 2;
+#ifndef RT_SPHERE_UNROLL
+#define RT_SPHERE_UNROLL 3
+#endif
+constexpr int kTravUnroll = !kTris ? RT_SPHERE_UNROLL : kMode <= 1 ? 5 : 2;
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
@@ -234,7 +243,7 @@ __device__ __forceinline__ void node_visit(const SceneView& sv, const KernelArgs
         }
     }
 #endif
-    if (at_leaf && !kDeferLeaves<kTris>) {
+    if (at_leaf && !kDeferLeaves<kTris> && !kBlockLeaves<kTris>) {
         test_sphere_group(sv, leaf & 0xffffffu, o, d, ts.a4, ts.a2, ts.sph);
         ts.limit = prune_limit(ts);
     } else if (at_leaf) {
@@ -250,6 +259,7 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     const bool tri = kTris && ts.phase == 0;
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
+    if (kBlockLeaves<kTris> && ts.pending != kNoLeaf) return;  // waits for the block's group tests
     float4 lo, hi;
     if (kTris && tri && sv.tri_q) {
         qnode_decode(sv, sv.tri_q[ts.node], ts.node, lo, hi);
@@ -1071,6 +1081,26 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                             phase_end<kTris>(sv, ka, p.o, p.d, ts);
                             if (ts.phase == 2) mode = kDone;
                         }
+                    }
+                }
+                if constexpr (kBlockLeaves<kTris>) {
+                    // the block's group tests: every lane that reached a leaf in it, together
+#ifdef RT_DIAG
+                    {  // block group tests and the lanes in them
+                        const uint64_t gm = __ballot(mode == kTrav && ts.pending != kNoLeaf);
+                        if (gm && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(gm)) {
+                            atomicAdd(ka.diag + 26, 1ull);
+                            atomicAdd(ka.diag + 27, (unsigned long long)__popcll(gm));
+                        }
+                    }
+#endif
+                    if (mode == kTrav && ts.pending != kNoLeaf) {
+                        RT_ISA_MARK("sphere_leaves");
+                        test_sphere_group(sv, ts.pending, p.o, p.d, ts.a4, ts.a2, ts.sph);
+                        ts.limit = prune_limit(ts);
+                        ts.pending = kNoLeaf;
+                        phase_end<kTris>(sv, ka, p.o, p.d, ts);
+                        if (ts.phase == 2) mode = kDone;
                     }
                 }
             }

@@ -42,6 +42,9 @@ for name in argv or list(SIZES):
     # sphere-only kernels: wave-level node steps and their lanes, the sphere-group tests run inside
     # them (a group runs for the whole wave when any lane is at a leaf) and the lanes at a leaf
     n_steps, n_step_lanes, n_groups, n_group_lanes = c[22:26]
+    # sphere-only kernels since round 6: the group tests run once per block of unrolled node steps
+    # for every lane that reached a leaf in it (words 24/25 then count node steps with a lane at a leaf)
+    n_blocks, n_block_lanes = c[26:28]
     trav_occ = step_lanes / max(steps, 1) / 64
     shade_occ = sh_lanes / max(sh_pass, 1) / 64
     setup_occ = su_lanes / max(su_pass, 1) / 64
@@ -57,7 +60,9 @@ for name in argv or list(SIZES):
                       "leaf_share": leaf_cyc / total, "leaf_steps_per_ray": leaf_steps / rays,
                       "sphere_node_steps": {"per_ray": n_steps / rays, "lanes_per_step": n_step_lanes / max(n_steps, 1),
                                             "steps_with_a_group_test": n_groups / max(n_steps, 1),
-                                            "lanes_per_group_test": n_group_lanes / max(n_groups, 1)},
+                                            "lanes_per_group_test": n_group_lanes / max(n_groups, 1),
+                                            "block_group_tests_per_ray": n_blocks / rays,
+                                            "lanes_per_block_group_test": n_block_lanes / max(n_blocks, 1)},
                       "leaf_certificates_per_ray": {"checked": cert_checks / rays, "leaves_skipped": cert_leaves / rays,
                                                     "triangles_skipped": cert_tris / rays},
                       "occupancy": {"traversal": trav_occ, "shading": shade_occ, "setup": setup_occ},

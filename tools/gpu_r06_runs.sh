@@ -94,6 +94,23 @@ case "$T" in
     timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
     RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow c3_chess > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
     ;;
+  r06k)
+    # sphere-only walks: the group tests of a block of unrolled node steps run once for every lane
+    # that reached a leaf in it (the product build, 3 steps), against the previous build (head) and
+    # blocks of 2/4/6 steps; every GPU test first
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    L="rust_gpu_raytracing_amd/librt_pathtrace.so abship/lib_head.so abship/lib_blk2.so abship/lib_blk4.so abship/lib_blk6.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c1_four_spheres --width 800 --height 600 --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c1.json 2> gpurun_out/$T/ab_c1.err || exit 1
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-cadences > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    ;;
+  r06l)
+    # block sizes of the sphere-only group tests: 4, 5, 6, 8, 12 unrolled node steps
+    L="abship/lib_blk4.so abship/lib_blk5.so abship/lib_blk6.so abship/lib_blk8.so abship/lib_blk12.so abship/lib_head.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c1_four_spheres --width 800 --height 600 --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c1.json 2> gpurun_out/$T/ab_c1.err || exit 1
+    RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
