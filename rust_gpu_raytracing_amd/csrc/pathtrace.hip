@@ -154,14 +154,13 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
 // that reaches a second leaf while one is deferred stays on it until the batch.
 // Testing a leaf late only delays the pruning distance it would set: the result
 // is the lexicographic minimum over the tested primitives either way.
-// Sphere-only scenes test a group on the spot (kDeferLeaves false): deferring
-// measured slower there.
 template <bool kTris>
 constexpr bool kDeferLeaves = kTris;
 // Sphere-only scenes: a lane that reaches a leaf stops walking, and the group tests of every lane
 // that reached one run once, after the wave's unrolled node steps (kTravUnroll), instead of inside
 // each node step for the few lanes at a leaf in that step. The lane resumes with its pruning
-// distance updated, so it visits the nodes the on-the-spot test would, in the same order.
+// distance updated, so it visits the nodes the on-the-spot test would, in the same order (C2
+// -9.0% in one process; walking on past the leaf until a second one instead: -8.0%).
 template <bool kTris>
 constexpr bool kBlockLeaves = !kTris;
 // Node steps per wave-wide check of the traversal loop (the ballots of the
@@ -169,12 +168,11 @@ constexpr bool kBlockLeaves = !kTris;
 // the group idle for its remaining steps; the visit order is unchanged.
 // Measured (1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%. Round 4, per accelerator placement
 // (profiles/r04/r04_z): global-memory walks 3 -> 4 / 5 / 6: C5 -4.0% / -4.3% / -1.6%;
-// LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%; sphere walks 2 or 4: C2 +1.5% / +0.8%.
+// LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%. Sphere walks, with the block group tests
+// (round 6, profiles/r06/r06l, r06m): blocks of 3 / 4 / 5 / 6 / 8 / 12 steps, C2 0.2675 / 0.2580 /
+// 0.2636 / 0.2575 / 0.2614 / 0.2658 ms per frame.
 template <int kMode, bool kTris>
-#ifndef RT_SPHERE_UNROLL
-#define RT_SPHERE_UNROLL 3
-#endif
-constexpr int kTravUnroll = !kTris ? RT_SPHERE_UNROLL : kMode <= 1 ? 5 : 2;
+constexpr int kTravUnroll = !kTris ? 6 : kMode <= 1 ? 5 : 2;
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).

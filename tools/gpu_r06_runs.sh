@@ -111,6 +111,12 @@ case "$T" in
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c1_four_spheres --width 800 --height 600 --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c1.json 2> gpurun_out/$T/ab_c1.err || exit 1
     RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
     ;;
+  r06m)
+    # the sphere-only block group tests: lanes waiting at their leaf (blk) or walking on past it
+    # until a second leaf (wo), blocks of 4 and 6 node steps
+    L="abship/lib_blk4.so abship/lib_blk6.so abship/lib_wo4.so abship/lib_wo6.so abship/lib_head.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
