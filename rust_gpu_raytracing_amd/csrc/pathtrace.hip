@@ -156,23 +156,27 @@ __device__ __forceinline__ void phase_end(const SceneView& sv, const KernelArgs&
 // is the lexicographic minimum over the tested primitives either way.
 template <bool kTris>
 constexpr bool kDeferLeaves = kTris;
-// Sphere-only scenes: a lane that reaches a leaf stops walking, and the group tests of every lane
-// that reached one run once, after the wave's unrolled node steps (kTravUnroll), instead of inside
-// each node step for the few lanes at a leaf in that step. The lane resumes with its pruning
-// distance updated, so it visits the nodes the on-the-spot test would, in the same order (C2
-// -9.0% in one process; walking on past the leaf until a second one instead: -8.0%).
+// Sphere-only scenes: a lane that reaches a leaf stops walking, and the group tests of the lanes
+// waiting at a leaf run together after a block of the wave's unrolled node steps (kTravUnroll),
+// once at least kBlockLeafShare eighths of the traversing lanes wait, instead of inside each node
+// step for the few lanes at a leaf in that step. The lane resumes with its pruning distance
+// updated, so it visits the nodes the on-the-spot test would, in the same order (C2 0.2820 ->
+// 0.2481 ms per frame in one process; walking on past the leaf until a second one was slower;
+// DESIGN §5.2).
 template <bool kTris>
 constexpr bool kBlockLeaves = !kTris;
+constexpr uint32_t kBlockLeafShare = 3;
 // Node steps per wave-wide check of the traversal loop (the ballots of the
 // threshold and leaf-batch tests, exec-mask updates). Lanes that finish inside
 // the group idle for its remaining steps; the visit order is unchanged.
 // Measured (1 -> 3): C2 -2.8%, C3 -10%, C4 -11%, C5 -7%. Round 4, per accelerator placement
 // (profiles/r04/r04_z): global-memory walks 3 -> 4 / 5 / 6: C5 -4.0% / -4.3% / -1.6%;
 // LDS-resident walks 3 -> 2: C3 -1.2%, C4 (4K) +0.5%. Sphere walks, with the block group tests
-// (round 6, profiles/r06/r06l, r06m): blocks of 3 / 4 / 5 / 6 / 8 / 12 steps, C2 0.2675 / 0.2580 /
-// 0.2636 / 0.2575 / 0.2614 / 0.2658 ms per frame.
+// (round 6, profiles/r06/r06l, r06o, r06p): blocks of 4 with the tests once 3/8 of the lanes wait,
+// C2 0.2481 ms per frame; 3 / 5 / 6 steps 0.2522 / 0.2503 / 0.2503; every block tested (no
+// share) at 3 / 4 / 6 / 8 / 12 steps 0.2675 / 0.2580 / 0.2575 / 0.2614 / 0.2658.
 template <int kMode, bool kTris>
-constexpr int kTravUnroll = !kTris ? 6 : kMode <= 1 ? 5 : 2;
+constexpr int kTravUnroll = !kTris ? 4 : kMode <= 1 ? 5 : 2;
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
@@ -1092,7 +1096,10 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         }
                     }
 #endif
-                    if (mode == kTrav && ts.pending != kNoLeaf) {
+                    // (the lanes that traversed in this block are the active ones: the ballots count them)
+                    const uint32_t n_wait = (uint32_t)__popcll(__ballot(ts.pending != kNoLeaf));
+                    const uint32_t n_tr = (uint32_t)__popcll(__ballot(true));
+                    if (8u * n_wait >= kBlockLeafShare * n_tr && mode == kTrav && ts.pending != kNoLeaf) {
                         RT_ISA_MARK("sphere_leaves");
                         test_sphere_group(sv, ts.pending, p.o, p.d, ts.a4, ts.a2, ts.sph);
                         ts.limit = prune_limit(ts);

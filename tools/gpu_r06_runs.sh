@@ -117,6 +117,36 @@ case "$T" in
     L="abship/lib_blk4.so abship/lib_blk6.so abship/lib_wo4.so abship/lib_wo6.so abship/lib_head.so"
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
     ;;
+  r06n)
+    # the sphere group test's candidate arms as a per-lane loop over its candidates (cand) against
+    # the four predicated arms (b6, the product build): C2, C4
+    L="abship/lib_b6.so abship/lib_cand.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
+  r06o)
+    # adaptive block group tests: after every block of U node steps, once W/8 of the traversing
+    # lanes wait at a leaf (ad<U>_<W>), against the fixed 6-step block (b6, the product build)
+    L="abship/lib_b6.so abship/lib_ad3_2.so abship/lib_ad3_4.so abship/lib_ad2_3.so abship/lib_ad4_3.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    ;;
+  r06p)
+    # adaptive block group tests around blocks of 4 steps and a 3/8 waiting share
+    L="abship/lib_ad4_3.so abship/lib_ad4_2.so abship/lib_ad4_4.so abship/lib_ad5_3.so abship/lib_ad6_3.so abship/lib_ad3_3.so abship/lib_ad4_5.so abship/lib_b6.so"
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py abship/lib_ad4_3.so abship/lib_b6.so abship/lib_head.so --config c1_four_spheres --width 800 --height 600 --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c1.json 2> gpurun_out/$T/ab_c1.err || exit 1
+    ;;
+  r06q)
+    # the adaptive block build: every GPU test, smoke, A/B against the round's first build (head)
+    # on C1-C4, the headline bench, and the RT_DIAG split of C2
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    L="rust_gpu_raytracing_amd/librt_pathtrace.so abship/lib_head.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 5 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
+    RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
