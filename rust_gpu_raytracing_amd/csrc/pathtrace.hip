@@ -1044,7 +1044,12 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
             // one node.
             RT_ISA_MARK("traversal");
             bool leaves = false;
-            if constexpr (kDeferLeaves<kTris>) {
+#ifdef RT_FUSE2
+            constexpr bool kFuse = kTris && kMode == 2;
+#else
+            constexpr bool kFuse = false;
+#endif
+            if constexpr (kDeferLeaves<kTris> && !kFuse) {
                 const uint32_t n_pend = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
                 leaves = 8u * n_pend >= ka.leaf_batch * n_trav;
             }
@@ -1085,10 +1090,22 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         }
                     }
                 }
+                if constexpr (kFuse) {
+                    const uint32_t n_p = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
+                    const uint32_t n_t = (uint32_t)__popcll(__ballot(mode == kTrav));
+                    if (8u * n_p >= ka.leaf_batch * n_t && mode == kTrav && ts.pending != kNoLeaf) {
+                        leaf_step<kTris, false>(sv, ka, p.o, p.d, ts);
+                        phase_end<kTris>(sv, ka, p.o, p.d, ts);
+                        if (ts.phase == 2) mode = kDone;
+                    }
+                }
                 if constexpr (kBlockLeaves<kTris>) {
                     // the block's group tests: every lane that reached a leaf in it, together
+                    // (the lanes that traversed in this block are the active ones: the ballots count them)
+                    const uint32_t n_wait = (uint32_t)__popcll(__ballot(ts.pending != kNoLeaf));
+                    const uint32_t n_tr = (uint32_t)__popcll(__ballot(true));
 #ifdef RT_DIAG
-                    {  // block group tests and the lanes in them
+                    if (8u * n_wait >= kBlockLeafShare * n_tr) {  // the block group tests and their lanes
                         const uint64_t gm = __ballot(mode == kTrav && ts.pending != kNoLeaf);
                         if (gm && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(gm)) {
                             atomicAdd(ka.diag + 26, 1ull);
@@ -1096,9 +1113,6 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         }
                     }
 #endif
-                    // (the lanes that traversed in this block are the active ones: the ballots count them)
-                    const uint32_t n_wait = (uint32_t)__popcll(__ballot(ts.pending != kNoLeaf));
-                    const uint32_t n_tr = (uint32_t)__popcll(__ballot(true));
                     if (8u * n_wait >= kBlockLeafShare * n_tr && mode == kTrav && ts.pending != kNoLeaf) {
                         RT_ISA_MARK("sphere_leaves");
                         test_sphere_group(sv, ts.pending, p.o, p.d, ts.a4, ts.a2, ts.sph);

@@ -147,6 +147,13 @@ case "$T" in
     timeout -k 10 300 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || exit 1
     RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
     ;;
+  r06r)
+    # mode-2 (LDS-resident triangle walk) leaf batches fused into the node-step iteration (fuse2),
+    # at batch shares 6/8 (the scene default), 4/8, 3/8, 2/8, against the product build
+    L="abship/lib_final.so abship/lib_fuse2.so abship/lib_fuse2.so:leaf_batch=4 abship/lib_fuse2.so:leaf_batch=3 abship/lib_fuse2.so:leaf_batch=2"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
