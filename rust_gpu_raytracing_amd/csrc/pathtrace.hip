@@ -176,7 +176,18 @@ constexpr uint32_t kBlockLeafShare = 3;
 // C2 0.2481 ms per frame; 3 / 5 / 6 steps 0.2522 / 0.2503 / 0.2503; every block tested (no
 // share) at 3 / 4 / 6 / 8 / 12 steps 0.2675 / 0.2580 / 0.2575 / 0.2614 / 0.2658.
 template <int kMode, bool kTris>
-constexpr int kTravUnroll = !kTris ? 4 : kMode <= 1 ? 5 : 2;
+constexpr int kTravUnroll = !kTris ? 4 : kMode <= 1 ? 5 : 3;
+// Triangle walks: the leaf batch runs after the block's node steps in the same iteration (round 6)
+// instead of in an iteration of its own in which the walking lanes idle: the LDS-resident walk
+// (mode 2, C3 0.2645 -> 0.2463, C4 1.539 -> 1.416 ms per frame in one process with blocks of 3
+// steps; 2 / 4 / 5 steps: C3 0.2492 / 0.2478 / 0.2527, C4 1.460 / 1.413 / 1.437; shares of
+// 5/8-8/8 around the default 6/8 no better; profiles/r06/r06r-r06t).
+template <int kMode, bool kTris>
+#ifdef RT_FUSE1
+constexpr bool kFusedLeaves = kTris;
+#else
+constexpr bool kFusedLeaves = kTris && kMode == 2;
+#endif
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
@@ -1044,12 +1055,7 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
             // one node.
             RT_ISA_MARK("traversal");
             bool leaves = false;
-#ifdef RT_FUSE2
-            constexpr bool kFuse = kTris && kMode == 2;
-#else
-            constexpr bool kFuse = false;
-#endif
-            if constexpr (kDeferLeaves<kTris> && !kFuse) {
+            if constexpr (kDeferLeaves<kTris> && !kFusedLeaves<kMode, kTris>) {
                 const uint32_t n_pend = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
                 leaves = 8u * n_pend >= ka.leaf_batch * n_trav;
             }
@@ -1090,11 +1096,13 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         }
                     }
                 }
-                if constexpr (kFuse) {
+                if constexpr (kFusedLeaves<kMode, kTris> && !kCoopLeaves<kMode, kTris>) {
+                    // the leaf batch after the block's node steps, in the same iteration
                     const uint32_t n_p = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
                     const uint32_t n_t = (uint32_t)__popcll(__ballot(mode == kTrav));
                     if (8u * n_p >= ka.leaf_batch * n_t && mode == kTrav && ts.pending != kNoLeaf) {
-                        leaf_step<kTris, false>(sv, ka, p.o, p.d, ts);
+                        RT_ISA_MARK("leaf_batch");
+                        leaf_step<kTris, (kMode <= 1)>(sv, ka, p.o, p.d, ts);
                         phase_end<kTris>(sv, ka, p.o, p.d, ts);
                         if (ts.phase == 2) mode = kDone;
                     }
@@ -1118,6 +1126,24 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         test_sphere_group(sv, ts.pending, p.o, p.d, ts.a4, ts.a2, ts.sph);
                         ts.limit = prune_limit(ts);
                         ts.pending = kNoLeaf;
+                        phase_end<kTris>(sv, ka, p.o, p.d, ts);
+                        if (ts.phase == 2) mode = kDone;
+                    }
+                }
+            }
+            if constexpr (kFusedLeaves<kMode, kTris> && kCoopLeaves<kMode, kTris>) {
+                // the cooperative leaf batch after the block's node steps (a wave-wide call)
+                const uint32_t n_p = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
+                const uint32_t n_t = (uint32_t)__popcll(__ballot(mode == kTrav));
+                if (n_p != 0u && 8u * n_p >= ka.leaf_batch * n_t) {
+                    const bool act = mode == kTrav && ts.pending != kNoLeaf;
+                    if (ka.tri_leaftris) {
+                        RT_ISA_MARK("coop_leaf_batch");
+                        coop_leaf_batch(sv, ka, p.o, p.d, ts, act, lds);
+                    } else if (act) {  // (tuning "coop_leaves" 0: per-lane leaf tests)
+                        leaf_step<kTris, true>(sv, ka, p.o, p.d, ts);
+                    }
+                    if (act) {
                         phase_end<kTris>(sv, ka, p.o, p.d, ts);
                         if (ts.phase == 2) mode = kDone;
                     }

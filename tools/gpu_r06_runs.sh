@@ -154,6 +154,25 @@ case "$T" in
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     ;;
+  r06s)
+    # fused mode-2 leaf batches: shares 6/7/8 eighths, node-step blocks of 1, 2 (fuse2), 3
+    L="abship/lib_fuse2.so abship/lib_fuse2.so:leaf_batch=7 abship/lib_fuse2.so:leaf_batch=8 abship/lib_fuse2u3.so abship/lib_fuse2u3.so:leaf_batch=7 abship/lib_fuse2u1.so abship/lib_fuse2u1.so:leaf_batch=7"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 500 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
+  r06t)
+    # fused mode-2 leaf batches: node-step blocks of 3, 4, 5 at shares 5/8 and 6/8
+    L="abship/lib_fuse2u3.so abship/lib_fuse2u3.so:leaf_batch=5 abship/lib_fuse2u4.so abship/lib_fuse2u4.so:leaf_batch=5 abship/lib_fuse2u5.so abship/lib_fuse2u5.so:leaf_batch=5 abship/lib_final.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 500 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
+  r06u)
+    # the fused mode-2 leaf batch build (f2, the product): every GPU test; then the cooperative
+    # batches of the global-memory walks fused the same way (f1) on C5, against f2
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    L="abship/lib_f2.so abship/lib_f1.so abship/lib_f1.so:leaf_batch=5 abship/lib_f1.so:leaf_batch=3"
+    timeout -k 10 500 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
