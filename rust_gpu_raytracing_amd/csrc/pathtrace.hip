@@ -182,12 +182,10 @@ constexpr int kTravUnroll = !kTris ? 4 : kMode <= 1 ? 5 : 3;
 // (mode 2, C3 0.2645 -> 0.2463, C4 1.539 -> 1.416 ms per frame in one process with blocks of 3
 // steps; 2 / 4 / 5 steps: C3 0.2492 / 0.2478 / 0.2527, C4 1.460 / 1.413 / 1.437; shares of
 // 5/8-8/8 around the default 6/8 no better; profiles/r06/r06r-r06t).
+// The walks from global memory keep their batches apart: fusing the cooperative batch the same
+// way measured C5 +2.3% (profiles/r06/r06u).
 template <int kMode, bool kTris>
-#ifdef RT_FUSE1
-constexpr bool kFusedLeaves = kTris;
-#else
 constexpr bool kFusedLeaves = kTris && kMode == 2;
-#endif
 
 // Decoupled drain (see the kernel's step 4): triangle scenes whose accelerator
 // is read from global memory (LDS modes 0 and 1).
@@ -1096,7 +1094,7 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         }
                     }
                 }
-                if constexpr (kFusedLeaves<kMode, kTris> && !kCoopLeaves<kMode, kTris>) {
+                if constexpr (kFusedLeaves<kMode, kTris>) {
                     // the leaf batch after the block's node steps, in the same iteration
                     const uint32_t n_p = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
                     const uint32_t n_t = (uint32_t)__popcll(__ballot(mode == kTrav));
@@ -1126,24 +1124,6 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                         test_sphere_group(sv, ts.pending, p.o, p.d, ts.a4, ts.a2, ts.sph);
                         ts.limit = prune_limit(ts);
                         ts.pending = kNoLeaf;
-                        phase_end<kTris>(sv, ka, p.o, p.d, ts);
-                        if (ts.phase == 2) mode = kDone;
-                    }
-                }
-            }
-            if constexpr (kFusedLeaves<kMode, kTris> && kCoopLeaves<kMode, kTris>) {
-                // the cooperative leaf batch after the block's node steps (a wave-wide call)
-                const uint32_t n_p = (uint32_t)__popcll(__ballot(mode == kTrav && ts.pending != kNoLeaf));
-                const uint32_t n_t = (uint32_t)__popcll(__ballot(mode == kTrav));
-                if (n_p != 0u && 8u * n_p >= ka.leaf_batch * n_t) {
-                    const bool act = mode == kTrav && ts.pending != kNoLeaf;
-                    if (ka.tri_leaftris) {
-                        RT_ISA_MARK("coop_leaf_batch");
-                        coop_leaf_batch(sv, ka, p.o, p.d, ts, act, lds);
-                    } else if (act) {  // (tuning "coop_leaves" 0: per-lane leaf tests)
-                        leaf_step<kTris, true>(sv, ka, p.o, p.d, ts);
-                    }
-                    if (act) {
                         phase_end<kTris>(sv, ka, p.o, p.d, ts);
                         if (ts.phase == 2) mode = kDone;
                     }
