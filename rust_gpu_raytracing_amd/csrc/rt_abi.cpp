@@ -98,7 +98,9 @@ constexpr uint32_t kQueueStride = 64;
 // A wave goes back to shading once at most this many of its 64 lanes are still
 // traversing (pathtrace.hip, step 4 of the kernel loop). The longer a trace is
 // against a shading pass, the earlier it pays to shade the finished lanes
-// (measured: sphere scenes 8, C2 slower at 12+; triangle accelerator in LDS
+// (measured: sphere scenes 8, C2 slower at 12+ until round 6's block group tests, since then 12:
+// C2 0.2474 -> 0.2448 ms, 10 / 14 / 20: 0.2456 / 0.2444 / 0.2468, profiles/r06/r06v, r06w;
+// triangle accelerator in LDS
 // 24, C3/C4 -2%; in global memory 32, C5 -10%; with the pruned octant walk of round 3,
 // 48: C5 5.95 -> 5.72 ms, profiles/r03_ah/knobs_c5b.jsonl; C3 unchanged at 24-32).
 // certified: walks from global memory with the certified pruning, whose
@@ -107,7 +109,7 @@ constexpr uint32_t kQueueStride = 64;
 // once the certificate test moved into the leaf batch;
 // profiles/r04/r04_f/ab.jsonl; the slack keeps round 3's 48 / 5).
 uint32_t trav_threshold_for(int lds_mode, bool tris, bool certified) {
-    if (!tris) return 8;
+    if (!tris) return 12;
     return lds_mode == 2 ? 24 : certified ? 56 : 48;
 }
 // Triangle scenes test deferred leaves once this many eighths of the

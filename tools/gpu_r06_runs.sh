@@ -173,6 +173,20 @@ case "$T" in
     L="abship/lib_f2.so abship/lib_f1.so abship/lib_f1.so:leaf_batch=5 abship/lib_f1.so:leaf_batch=3"
     timeout -k 10 500 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
     ;;
+  r06v)
+    # traversal thresholds at the new build (the wave goes back to shading once this many lanes
+    # still traverse): C2 (default 8) 4/12/16, C3 (default 24) 16/32
+    F=abship/lib_f2.so
+    timeout -k 10 300 python3 tools/ab_bench.py $F $F:trav_threshold=4 $F:trav_threshold=12 $F:trav_threshold=16 --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $F $F:trav_threshold=16 $F:trav_threshold=32 --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    ;;
+  r06w)
+    # traversal thresholds, second pass: C2 10/12/14/20, C3 and C4 28/32/40
+    F=abship/lib_f2.so
+    timeout -k 10 300 python3 tools/ab_bench.py $F $F:trav_threshold=10 $F:trav_threshold=12 $F:trav_threshold=14 $F:trav_threshold=20 --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $F $F:trav_threshold=28 $F:trav_threshold=32 $F:trav_threshold=40 --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $F $F:trav_threshold=28 $F:trav_threshold=32 $F:trav_threshold=40 --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
   r06z|r06y)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
