@@ -187,7 +187,19 @@ case "$T" in
     timeout -k 10 300 python3 tools/ab_bench.py $F $F:trav_threshold=28 $F:trav_threshold=32 $F:trav_threshold=40 --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py $F $F:trav_threshold=28 $F:trav_threshold=32 $F:trav_threshold=40 --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     ;;
-  r06z|r06y)
+  r06x1)
+    # final-build profiles (kernel trace + FETCH/WRITE/SQ passes, tools/profile.sh): C2, C3, C4
+    timeout -k 10 600 bash tools/profile.sh r06_c2 > gpurun_out/$T.c2.log 2>&1 || exit 1
+    timeout -k 10 600 bash tools/profile.sh r06_c3 --config c3_chess > gpurun_out/$T.c3.log 2>&1 || exit 1
+    timeout -k 10 600 bash tools/profile.sh r06_c4 --config c4_mixed > gpurun_out/$T.c4.log 2>&1 || exit 1
+    ;;
+  r06x2)
+    # final-build profiles: C5 (exact walk), C5 brute force (LDS tiles, scalar-cache stream)
+    timeout -k 10 600 bash tools/profile.sh r06_c5 --config c5_heightfield > gpurun_out/$T.c5.log 2>&1 || exit 1
+    timeout -k 10 600 bash tools/profile.sh r06_c5b --config c5_heightfield --brute-force --steps 2 --warmup 2 > gpurun_out/$T.c5b.log 2>&1 || exit 1
+    timeout -k 10 600 bash tools/profile.sh r06_c5bs --config c5_heightfield --brute-force stream --steps 2 --warmup 2 > gpurun_out/$T.c5bs.log 2>&1 || exit 1
+    ;;
+  r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
     timeout -k 10 900 python3 -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
