@@ -216,7 +216,11 @@ from rust_gpu_raytracing_amd import _native as N, build as b
 lib = N.load_library()
 print('srcbuild library hash', lib.rt_build_hash().decode(), '== tree', b.source_hash())" >> gpurun_out/$T/srcbuild.log 2>&1 || exit 1
     timeout -k 10 600 python3 tools/bench_all.py --frames 20 > gpurun_out/$T/bench_all.jsonl 2> gpurun_out/$T/bench_all.err || exit 1
-    timeout -k 10 300 python3 tools/strong_probe.py --steps 20 > gpurun_out/$T/strong_probe.jsonl 2> gpurun_out/$T/strong_probe.err || exit 1
+    ;;
+  r06z2)
+    # strong-scaling probes at the final build, the bench's accumulation payload: C2, C4
+    timeout -k 10 400 python3 tools/strong_probe.py --steps 20 --gather accumulation > gpurun_out/$T/strong_c2_accumulation.jsonl 2> gpurun_out/$T/strong_c2.err || exit 1
+    timeout -k 10 500 python3 tools/strong_probe.py --config c4_mixed --steps 20 --gather accumulation > gpurun_out/$T/strong_c4_accumulation.jsonl 2> gpurun_out/$T/strong_c4.err || exit 1
     ;;
   *)
     echo "unknown tag $T"; exit 2
