@@ -199,6 +199,10 @@ case "$T" in
     timeout -k 10 600 bash tools/profile.sh r06_c5b --config c5_heightfield --brute-force --steps 2 --warmup 2 > gpurun_out/$T.c5b.log 2>&1 || exit 1
     timeout -k 10 600 bash tools/profile.sh r06_c5bs --config c5_heightfield --brute-force stream --steps 2 --warmup 2 > gpurun_out/$T.c5bs.log 2>&1 || exit 1
     ;;
+  r06x3)
+    # final-build profile of C4 at its BASELINE size (3840x2160, 16 bounces)
+    timeout -k 10 600 bash tools/profile.sh r06_c4k --config c4_mixed --width 3840 --height 2160 > gpurun_out/$T.c4k.log 2>&1 || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
