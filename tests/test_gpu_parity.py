@@ -937,6 +937,29 @@ def test_gpu_global_walk_variants(gpu, oracle_lib, config, kw, tuning):
     assert_same(*gpu_render(scene, bounces, 2, prune=prune, tuning=tuning), acc_o, out_o, rays_o)
 
 
+@pytest.mark.parametrize("tuning", [
+    {},
+    {"trav_threshold": 1},            # traverse (almost) to the end before shading
+    {"trav_threshold": 63},           # back to shading after every block
+    {"leaf_batch": 1},                # triangle leaf batches as soon as one lane waits
+    {"leaf_batch": 8},                # ... only once every traversing lane waits
+    {"sphere_leaf": 1},               # one sphere per BVH leaf: a leaf at nearly every step
+    {"block_threads": 256, "batch_overlap": 0},
+])
+@pytest.mark.parametrize("config,kw", [("c1_four_spheres", {}), ("c2_rtiow", {}),
+                                       ("c3_chess", dict(env_size=(512, 256))),
+                                       ("c4_mixed", dict(env_size=(256, 128)))])
+def test_gpu_leaf_scheduling_extremes(gpu, oracle_lib, config, kw, tuning):
+    """Round 6's leaf scheduling: sphere-only walks wait at a leaf and test the waiting lanes'
+    groups after a block of node steps (kBlockLeaves), and LDS-resident triangle walks run their
+    leaf batch in the node-step iteration (kFusedLeaves). Under extreme shading and batch
+    thresholds, one-sphere leaves and small workgroups, no lane waits forever (the launch
+    ends) and every image and ray count is the oracle's."""
+    scene, bounces = build_config(config, width=96, height=64, **kw)
+    acc_o, out_o, rays_o = oracle_lib.render_frames(scene, bounces, 3)
+    assert_same(*gpu_render(scene, bounces, 3, tuning=tuning, frame_batch=3), acc_o, out_o, rays_o)
+
+
 @pytest.mark.parametrize("config,kw,spp,accumulate,batch,world,env", [
     ("c3_chess", dict(env_size=(512, 256)), 2, 1, 3, 1, {"primary_pass": 1}),
     ("c3_chess", dict(env_size=(512, 256)), 1, 0, 3, 1, {"primary_pass": 1}),  # non-accumulating batch

@@ -203,6 +203,12 @@ case "$T" in
     # final-build profile of C4 at its BASELINE size (3840x2160, 16 bounces)
     timeout -k 10 600 bash tools/profile.sh r06_c4k --config c4_mixed --width 3840 --height 2160 > gpurun_out/$T.c4k.log 2>&1 || exit 1
     ;;
+  r06y2)
+    # the new leaf-scheduling test; then, in triangle kernels, sphere-phase lanes waiting at their
+    # leaf (sphwait) instead of walking on, on C4
+    timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k leaf_scheduling > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py abship/lib_f3.so abship/lib_sphwait.so --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
