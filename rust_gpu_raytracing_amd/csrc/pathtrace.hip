@@ -271,9 +271,6 @@ __device__ __forceinline__ void node_step(const SceneView& sv, const KernelArgs&
     if (kDeferLeaves<kTris> && ts.node >= (tri ? ka.tri_nodes : ka.sphere_nodes))
         return;  // walk over, a leaf still deferred
     if (kBlockLeaves<kTris> && ts.pending != kNoLeaf) return;  // waits for the block's group tests
-#ifdef RT_SPH_WAIT
-    if (kTris && !tri && ts.pending != kNoLeaf) return;
-#endif
     float4 lo, hi;
     if (kTris && tri && sv.tri_q) {
         qnode_decode(sv, sv.tri_q[ts.node], ts.node, lo, hi);
