@@ -535,7 +535,10 @@ def main() -> int:
         eff_launch_s = m["t_render"] / max(n_timed, 1)  # wall time per launch: overlapped launches pipeline
         workload = f"{args.config} {width}x{height}, {bounces} bounces, 1 spp/frame, accumulate"
         if args.brute_force:
-            workload += (", brute-force sweeps streamed through the scalar cache" if args.brute_force == "stream"
+            # named by the kernel that ran (rt_last_launch_passes): mode 2 streams the records only
+            # where the scene has triangles to sweep, else the LDS tiles run
+            streamed = "brute_stream" in m.get("passes", [])
+            workload += (", brute-force sweeps streamed through the scalar cache" if streamed
                          else ", brute-force LDS-tiled sweeps")
         # a non-default triangle walk is another workload for the PMC table (its counters are
         # not the default walk's): --triangle-pruning 0 = box culling, 2 = the round-3 slack (not exact)
