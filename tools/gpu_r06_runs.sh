@@ -209,6 +209,16 @@ case "$T" in
     timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k leaf_scheduling > gpurun_out/$T/tests.log 2>&1 || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py abship/lib_f3.so abship/lib_sphwait.so --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     ;;
+  r06y3)
+    # the decoupled drain for every instance (dd): C2's N=1 and N=8 shares, predicted by the probe,
+    # at drain thresholds / minimum steps, against the product build
+    P="python3 tools/strong_probe.py --steps 20 --gather accumulation --ns 1 8 --repeats 3"
+    timeout -k 10 200 $P > gpurun_out/$T/prod.jsonl 2> gpurun_out/$T/prod.err || exit 1
+    RT_LIB=abship/lib_dd.so timeout -k 10 200 $P > gpurun_out/$T/dd.jsonl 2> gpurun_out/$T/dd.err || exit 1
+    RT_LIB=abship/lib_dd.so timeout -k 10 200 $P --tune drain_threshold=16 > gpurun_out/$T/dd_t16.jsonl 2> gpurun_out/$T/dd_t16.err || exit 1
+    RT_LIB=abship/lib_dd.so timeout -k 10 200 $P --tune drain_threshold=48 drain_min_steps=16 > gpurun_out/$T/dd_t48m16.jsonl 2> gpurun_out/$T/dd_t48m16.err || exit 1
+    RT_LIB=abship/lib_dd.so timeout -k 10 200 $P --tune drain_min_steps=8 > gpurun_out/$T/dd_m8.jsonl 2> gpurun_out/$T/dd_m8.err || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe

@@ -26,10 +26,10 @@ from rust_gpu_raytracing_amd import Renderer  # noqa: E402
 from rust_gpu_raytracing_amd.scene import build_config  # noqa: E402
 
 
-def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms, what="image"):
+def time_rank(scene, bounces, rank, world, steps, warmup, fb, settle_ms, what="image", tuning=None):
     import torch
 
-    with Renderer(scene, rank=rank, world_size=world, frame_batch=fb) as r:
+    with Renderer(scene, rank=rank, world_size=world, frame_batch=fb, tuning=tuning or {}) as r:
         for _ in range(warmup):
             r.compute_frame(bounces)
         r.synchronize()
@@ -79,12 +79,14 @@ def main():
     ap.add_argument("--ns", type=int, nargs="*", default=[1, 2, 4, 8])
     ap.add_argument("--settle-ms", type=float, default=150.0, help="as bench.py --settle-ms")
     ap.add_argument("--frame-batch", type=int, default=0, help="override bench.default_frame_batch(N)")
+    ap.add_argument("--tune", nargs="*", default=[], help="key=value rt_set_tuning settings of every rank's context")
     ap.add_argument("--repeats", type=int, default=3, help="timed runs per rank (the median is used)")
     ap.add_argument("--gather", choices=["image", "accumulation"], default="image",
                     help="the gather payload priced (bench.py --gather; default image, 4 B/px)")
     ap.add_argument("--link-gbs", type=float, default=50.0,
                     help="xGMI bandwidth one peer achieves into rank 0 (GB/s, per link; 7 links)")
     args = ap.parse_args()
+    tuning = {k: int(v) for k, v in (kv.split("=", 1) for kv in args.tune)}
     scene, bounces = build_config(args.config)
     base = None
     for n in args.ns:
@@ -93,7 +95,7 @@ def main():
         for r in range(n):
             # the median of --repeats timed runs per rank (one 20-frame run is under 1 ms at N=8:
             # a single launch-latency hiccup would move it by several percent)
-            runs = sorted((time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms, args.gather)
+            runs = sorted((time_rank(scene, bounces, r, n, args.steps, args.warmup, fb, args.settle_ms, args.gather, tuning)
                            for _ in range(args.repeats)), key=lambda x: x[0])
             per.append(runs[len(runs) // 2])
         t_max = max(p[0] for p in per)
