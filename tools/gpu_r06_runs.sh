@@ -202,6 +202,8 @@ case "$T" in
   r06x3)
     # final-build profile of C4 at its BASELINE size (3840x2160, 16 bounces)
     timeout -k 10 600 bash tools/profile.sh r06_c4k --config c4_mixed --width 3840 --height 2160 > gpurun_out/$T.c4k.log 2>&1 || exit 1
+    # and the C5 walk's L1/TA/TD counters at the final build (tools/pmc_tcp.sh)
+    timeout -k 10 600 bash tools/pmc_tcp.sh r06_c5tcp --config c5_heightfield > gpurun_out/$T.c5tcp.log 2>&1 || exit 1
     ;;
   r06y2)
     # the new leaf-scheduling test; then, in triangle kernels, sphere-phase lanes waiting at their
