@@ -221,6 +221,13 @@ case "$T" in
     RT_LIB=abship/lib_dd.so timeout -k 10 200 $P --tune drain_threshold=48 drain_min_steps=16 > gpurun_out/$T/dd_t48m16.jsonl 2> gpurun_out/$T/dd_t48m16.err || exit 1
     RT_LIB=abship/lib_dd.so timeout -k 10 200 $P --tune drain_min_steps=8 > gpurun_out/$T/dd_m8.jsonl 2> gpurun_out/$T/dd_m8.err || exit 1
     ;;
+  r06y4)
+    # the packet pre-pass reading its records with scalar loads (the product build now) against
+    # the final profiled build (f3): every GPU test, then C5 in one process (wall and spans)
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 500 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abship/lib_f3.so --config c5_heightfield --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    timeout -k 10 300 python3 bench.py --config c5_heightfield --no-cpu-baseline --no-cadences > gpurun_out/$T/bench_c5.json 2> gpurun_out/$T/bench_c5.err || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
