@@ -228,6 +228,12 @@ case "$T" in
     timeout -k 10 500 python3 tools/ab_bench.py rust_gpu_raytracing_amd/librt_pathtrace.so abship/lib_f3.so --config c5_heightfield --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
     timeout -k 10 300 python3 bench.py --config c5_heightfield --no-cpu-baseline --no-cadences > gpurun_out/$T/bench_c5.json 2> gpurun_out/$T/bench_c5.err || exit 1
     ;;
+  r06y5)
+    # the sphere group test's candidate arms as selects instead of branches (csel)
+    L="abship/lib_f3.so abship/lib_csel.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
