@@ -234,6 +234,19 @@ case "$T" in
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 11 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     ;;
+  r06y6)
+    # the RT_DIAG split at the final build: C2, C3, C4 (1920x1080)
+    RT_LIB=abship/lib_diag.so timeout -k 10 300 python3 tools/diag_split.py --frame-batch 20 c2_rtiow c3_chess c4_mixed > gpurun_out/$T/diag_split.jsonl 2> gpurun_out/$T/diag_split.err || exit 1
+    ;;
+  r06y7)
+    # triangle walks that end wait for one phase switch per block (pd) instead of switching to the
+    # sphere walk inside every node step: the parity tests on that build, then C3/C4/C5 A/B
+    RT_LIB=abship/lib_pd.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    L="abship/lib_f3.so abship/lib_pd.so"
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
