@@ -247,6 +247,16 @@ case "$T" in
     timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
     ;;
+  r06y8)
+    # a tile's frames claimed from one stripe, i.e. on one XCD (xcd), against the product build (f3):
+    # the frame-batch parity tests on that build, then C5, C4, C3, C2 in one process
+    RT_LIB=abship/lib_xcd.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k "frame_batch or full_frame_baseline_size or sampled_c5 or leaf_scheduling or cost_ordered or tile_split or overlapped" > gpurun_out/$T/tests.log 2>&1 || exit 1
+    L="abship/lib_f3.so abship/lib_xcd.so"
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
