@@ -188,10 +188,10 @@ case "$T" in
     timeout -k 10 400 python3 tools/ab_bench.py $F $F:trav_threshold=28 $F:trav_threshold=32 $F:trav_threshold=40 --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     ;;
   r06x1)
-    # final-build profiles (kernel trace + FETCH/WRITE/SQ passes, tools/profile.sh): C2, C3, C4
+    # final-build profiles (kernel trace + FETCH/WRITE/SQ passes, tools/profile.sh): C2, C3, C4 (3840x2160)
     timeout -k 10 600 bash tools/profile.sh r06_c2 > gpurun_out/$T.c2.log 2>&1 || exit 1
     timeout -k 10 600 bash tools/profile.sh r06_c3 --config c3_chess > gpurun_out/$T.c3.log 2>&1 || exit 1
-    timeout -k 10 600 bash tools/profile.sh r06_c4 --config c4_mixed > gpurun_out/$T.c4.log 2>&1 || exit 1
+    timeout -k 10 600 bash tools/profile.sh r06_c4k --config c4_mixed --width 3840 --height 2160 > gpurun_out/$T.c4k.log 2>&1 || exit 1
     ;;
   r06x2)
     # final-build profiles: C5 (exact walk), C5 brute force (LDS tiles, scalar-cache stream)
@@ -254,6 +254,24 @@ case "$T" in
     L="abship/lib_f3.so abship/lib_xcd.so"
     timeout -k 10 400 python3 tools/ab_bench.py $L --config c5_heightfield --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
     timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    ;;
+  r06y9)
+    # mode-2 leaf batches of one kind (the triangle or the sphere leaves, whichever more lanes hold)
+    # instead of both (ps): the leaf tests on that build, then C4 and C3
+    RT_LIB=abship/lib_ps.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k "leaf_scheduling or fuzz or c4 or mixed" > gpurun_out/$T/tests.log 2>&1 || exit 1
+    L="abship/lib_f3.so abship/lib_ps.so"
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    ;;
+  r06v1)
+    # single-kind mode-2 leaf batches (the product build, f4): every GPU test, smoke, A/B against
+    # the previous final build (f3) on C2, C3, C4
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    L="abship/lib_f3.so abship/lib_f4.so"
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
     ;;
