@@ -1099,16 +1099,15 @@ __global__ void __launch_bounds__(kThreads, 1) rt_pathtrace_kernel(KernelArgs ka
                     // One kind of leaf per batch in scenes with both walks (C4): the triangle or
                     // the sphere leaves, whichever more lanes hold (the other lanes wait for the
                     // next batch), so the batch does not run both leaf bodies on part of the wave
-                    // each (C4 1.410 -> 1.361 ms per frame, profiles/r06/r06y9).
-                    const uint64_t mp = __ballot(mode == kTrav && ts.pending != kNoLeaf);
-                    const uint32_t n_p = (uint32_t)__popcll(mp);
+                    // each (C4 1.410 -> 1.361 ms per frame, profiles/r06/r06y9; the second ballot gated on a sphere BVH
+                    // measured C4 1.380).
+                    const uint64_t mt = __ballot(mode == kTrav && ts.pending != kNoLeaf && ts.phase == 0);
+                    const uint64_t ms = __ballot(mode == kTrav && ts.pending != kNoLeaf && ts.phase != 0);
+                    const uint32_t n_p = (uint32_t)__popcll(mt | ms);
                     const uint32_t n_t = (uint32_t)__popcll(__ballot(mode == kTrav));
-                    bool kind = true;  // this lane's leaf is of the kind the batch tests
-                    if (ka.sphere_nodes != 0u) {
-                        const uint64_t mt = __ballot(mode == kTrav && ts.pending != kNoLeaf && ts.phase == 0);
-                        kind = (ts.phase == 0) == (2u * (uint32_t)__popcll(mt) >= n_p);
-                    }
-                    if (8u * n_p >= ka.leaf_batch * n_t && mode == kTrav && ts.pending != kNoLeaf && kind) {
+                    const bool tri_first = __popcll(mt) >= __popcll(ms);
+                    if (8u * n_p >= ka.leaf_batch * n_t && mode == kTrav && ts.pending != kNoLeaf &&
+                        (ts.phase == 0) == tri_first) {
                         RT_ISA_MARK("leaf_batch");
                         leaf_step<kTris, (kMode <= 1)>(sv, ka, p.o, p.d, ts);
                         phase_end<kTris>(sv, ka, p.o, p.d, ts);

@@ -275,6 +275,17 @@ case "$T" in
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
     ;;
+  r06v2)
+    # the product build (f5: single-kind leaf batches, two ballots): every GPU test, smoke, A/B
+    # against f3 on C4/C3/C2, then the final-build profiles of C2, C3, C4 (r06x1)
+    timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || exit 1
+    timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || exit 1
+    L="abship/lib_f3.so abship/lib_f5.so"
+    timeout -k 10 400 python3 tools/ab_bench.py $L --config c4_mixed --width 3840 --height 2160 --rounds 5 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
+    timeout -k 10 300 python3 tools/ab_bench.py $L --config c2_rtiow --rounds 9 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c2.json 2> gpurun_out/$T/ab_c2.err || exit 1
+    bash tools/gpu_r06_runs.sh r06x1 || exit 1
+    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
