@@ -1,6 +1,9 @@
 #!/bin/bash
 # The round-6 GPU sessions, one case per run tag (outputs: gpurun_out/<tag>/, copied to
 # profiles/r06/<tag>/ when DESIGN.md cites them). usage (via gpurun): bash tools/gpu_r06_runs.sh <tag>
+# Cases r06d-r06h ran the treelet wavefront, since archived (profiles/archive/experiments/); they
+# need that code applied again. Cases naming abship/ libraries need those A/B builds
+# (tools/build_at_commit.py, tools/build_variant.py) in abship/ first.
 set -o pipefail
 T=$1
 mkdir -p gpurun_out/$T
