@@ -296,11 +296,6 @@ case "$T" in
     timeout -k 10 500 python3 tools/ab_bench.py $F $F:leaf_batch=5 $F:leaf_batch=7 $F:trav_threshold=16 $F:trav_threshold=32 --config c4_mixed --width 3840 --height 2160 --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c4.json 2> gpurun_out/$T/ab_c4.err || exit 1
     timeout -k 10 300 python3 tools/ab_bench.py $F $F:leaf_batch=5 $F:leaf_batch=7 $F:trav_threshold=16 $F:trav_threshold=32 --config c3_chess --rounds 7 --frames 60 --frame-batch 20 > gpurun_out/$T/ab_c3.json 2> gpurun_out/$T/ab_c3.err || exit 1
     ;;
-  r06v4)
-    # C5 knob re-check at the final build (runtime tuning): shading threshold, leaf share, drain
-    F=abship/lib_f5.so
-    timeout -k 10 600 python3 tools/ab_bench.py $F $F:trav_threshold=48 $F:trav_threshold=60 $F:leaf_batch=3 $F:leaf_batch=5 $F:drain_threshold=16 $F:drain_min_steps=32 --config c5_heightfield --rounds 3 --frames 40 --frame-batch 20 > gpurun_out/$T/ab_c5.json 2> gpurun_out/$T/ab_c5.err || exit 1
-    ;;
   r06z)
     # the final pass: every GPU test, smoke, the headline bench, the library rebuilt from source on
     # the box and its parity tests (provenance: DESIGN.md §6), all configurations, strong probe
